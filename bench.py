@@ -1,0 +1,198 @@
+"""Benchmark: rrLU GFLOP/s at (m, n, r) = (8192, 8192, 256) on MI355X (BASELINE.json metric), plus
+Pi-rows/s of the batch-evaluation kernel and the TCI2 sweep wall time of config 1.
+
+A "step" is one rrlu(A; maxrank=r) on a synthetic U[0,1) Float64 matrix resident in HBM
+(copy into the work buffer included, as rrlu = rrlu!(copy(A)), matrixlu.jl:462).
+value = sum_{k=1..r} 2(m-k)(n-k) flops x ranks / max-over-ranks time.
+
+  python bench.py [--gpus N --steps K --warmup W] [--m M --n N --r R] [--no-extras] [--no-cpu]
+N > 1: launched by torch.distributed.run, one process per GPU; each rank factorises its own
+matrix (weak scaling, no data-path collective; DESIGN.md "Multi-GPU").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tensorcrossinterpolation.jl_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 measured copy)
+
+
+def rrlu_flops(m, n, r):
+    k = np.arange(1, r + 1, dtype=np.float64)
+    return float(np.sum(2.0 * (m - k) * (n - k)))
+
+
+def update_bytes(m, n, r):
+    # fused update+argmax launches run for pivots k = 0..r-2 over the (m-k-1) x (n-k-1) trailing
+    # block: 8 B read + 8 B written per element (SURVEY 8(d) per-unit figure)
+    k = np.arange(0, r - 1, dtype=np.float64)
+    return float(np.sum(16.0 * (m - k - 1) * (n - k - 1)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--r", type=int, default=256)
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-pivots", type=int, default=256)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only: barrier + max of times
+        dist.init_process_group(backend="gloo", init_method="env://")
+
+    import tci_amd as T
+
+    ctx = T.context(local_rank)
+    m, n, r = args.m, args.n, args.r
+    A = T.DeviceMatrix(m, n, ctx=ctx)
+    A.fill_uniform(seed=rank)
+    W = T.DeviceMatrix(m, n, ctx=ctx)
+
+    def step():
+        W.copy_from(A)
+        return T.rrlu_inplace_device(W, maxrank=r, want_perms=False)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    ctx.set_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np_, err, _, _, _ = step()
+    barrier()
+    dt = time.perf_counter() - t0
+    upd_ms, upd_launches = ctx.kernel_stats(0)
+    ctx.set_timing(False)
+    assert np_ == min(r, m, n), np_
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ms_per_step = dt / args.steps * 1e3
+    flops = rrlu_flops(m, n, r)
+    value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
+    avg_launch_ms = upd_ms / max(upd_launches, 1)
+    bytes_per_launch = update_bytes(m, n, r) / max(r - 1, 1)
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    out = {
+        "metric": "rrLU GFLOP/s at (m,n,r)=(8192,8192,256)" if (m, n, r) == (8192, 8192, 256)
+        else f"rrLU GFLOP/s at (m,n,r)=({m},{n},{r})",
+        "value": round(value, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: U[0,1) splitmix64 matrix, seed = rank, resident in HBM",
+        "config": {"workload": "rrlu(A; maxrank=r, reltol=1e-14, abstol=0, leftorthogonal=true)",
+                   "m": m, "n": n, "r": r, "parallelism": f"replicas{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_argmax_update<true> (fused Schur rank-1 update + abs2 argmax)",
+                     "avg_launch_ms": round(avg_launch_ms, 5), "launches": upd_launches,
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
+    }
+    A.free()
+    W.free()
+
+    if rank == 0 and not args.no_extras:
+        out["extras"] = extras(T, ctx)
+    if rank == 0 and not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(m, n, r, args.cpu_pivots)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def extras(T, ctx):
+    """Pi-rows/s of the batch evaluation and the TCI2 wall time of BASELINE config 1."""
+    res = {}
+    # Pi assembly: 8192 x 8192, L = 20 legs, nl = nr = 10, d = 10, Lorentzian
+    rng = np.random.default_rng(1)
+    m = n = 8192
+    I = rng.integers(1, 11, (m, 10)).astype(np.int32)
+    J = rng.integers(1, 11, (n, 10)).astype(np.int32)
+    for name, f in (("lorentz", T.lorentz([10] * 20, ctx=ctx)),
+                    ("quantics_osc", T.GPUBatchEvaluator(5, T.batcheval.QOSC_PARAMS, [2] * 40, ctx=ctx))):
+        if name == "quantics_osc":
+            Ib = rng.integers(1, 3, (m, 20)).astype(np.int32)
+            Jb = rng.integers(1, 3, (n, 20)).astype(np.int32)
+        else:
+            Ib, Jb = I, J
+        dm = T.DeviceMatrix(m, n, ctx=ctx)
+        import ctypes as C
+        mx = C.c_double()
+        for _ in range(2):
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(Ib), m, Ib.shape[1], T._lib.ptr(Jb), n,
+                                              Jb.shape[1], 0, dm.ptr, dm.ld, C.byref(mx)))
+        ctx.set_timing(True)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(Ib), m, Ib.shape[1], T._lib.ptr(Jb), n,
+                                              Jb.shape[1], 0, dm.ptr, dm.ld, C.byref(mx)))
+        wall = (time.perf_counter() - t0) / reps
+        kms, kn = ctx.kernel_stats(1)
+        ctx.set_timing(False)
+        dev_s = kms / max(kn, 1) * 1e-3
+        res[f"pi_{name}"] = {"m": m, "n": n, "L": Ib.shape[1] + Jb.shape[1],
+                             "pi_rows_per_s_device": round(m / dev_s, 1),
+                             "pi_rows_per_s_call": round(m / wall, 1),
+                             "write_GBps_device": round(8.0 * m * n / dev_s / 1e9, 1)}
+        dm.free()
+    # TCI2 sweep wall time, config 1: 8d Lorentzian, localdims = fill(10, 8), tol = 1e-8
+    f = T.lorentz([10] * 8, ctx=ctx)
+    T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)  # warm
+    t0 = time.perf_counter()
+    tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)
+    res["tci2_config1"] = {"wall_s": round(time.perf_counter() - t0, 4), "ranks": ranks,
+                           "final_error": errors[-1], "mode": "nsearchglobalpivot=0"}
+    return res
+
+
+def cpu_baseline(m, n, r, pivots):
+    """The oracle (C restatement of _optimizerrlu!, one core) on the first `pivots` pivots of the
+    same (m, n) matrix: GFLOP/s over that bounded sample."""
+    import oracle_lib as O
+    a = O.fill_uniform(m * n, seed=0)
+    t0 = time.perf_counter()
+    npv, _, _, _ = O.rrlu_inplace_sample(a, m, n, r, pivots)
+    dt = time.perf_counter() - t0
+    fl = rrlu_flops(m, n, npv)
+    return {"value": round(fl / dt / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
+            "sample": f"oracle rrLU (tci_oracle.c, -O3, 1 thread) first {npv} of {r} pivots on the "
+                      f"same {m}x{n} matrix, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

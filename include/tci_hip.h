@@ -1,0 +1,149 @@
+/*
+ * tci_hip.h -- C ABI of libtci_hip.so, the MI355X (gfx950) engine behind the TCI2 hot path of
+ * TensorCrossInterpolation.jl (XiaoJiang-Phy fork of tensor4all v0.9.18).
+ *
+ * Plain pointers and sizes only; no torch/HIP types in any signature. A Julia shim binds these
+ * with `ccall`; this repo's Python host (tci_amd) binds them with ctypes.
+ *
+ * Conventions
+ *  - Matrices are column-major Float64, like Julia Matrix{Float64}.
+ *  - Index sets (MultiIndex = Vector{Int}, abstracttensortrain.jl:33) are passed as int32 tables
+ *    in row-major "entry" order: entry e occupies w consecutive values; values are 1-based.
+ *  - Permutations and pivot row/column indices are returned 1-based (Julia convention).
+ *  - `_h` entry points take host pointers (the library copies in and out, synchronous);
+ *    `_d` entry points take device pointers on the context's device and leave results there.
+ *  - Every call is synchronous with respect to the host for host outputs (stream synchronised
+ *    before return). One tci_ctx per host thread; contexts are independent.
+ *
+ * Errors: 0 = success; otherwise one of TCI_ERR_*; tci_last_error(ctx) gives the message, which
+ * matches the reference's exception text where one exists.
+ */
+#ifndef TCI_HIP_H
+#define TCI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCI_OK 0
+#define TCI_ERR_ARG 1    /* ArgumentError / DimensionMismatch (e.g. matrixlu.jl:58-67)         */
+#define TCI_ERR_NAN 2    /* error("lu.L contains NaNs") / ("lu.U ...") (matrixlu.jl:376-381)    */
+#define TCI_ERR_NONSQ 3  /* "Pivot matrix at bond $b is not square!" (tensorci2.jl:623)       */
+#define TCI_ERR_DEVICE 4 /* HIP / RCCL failure                                                 */
+#define TCI_ERR_NOMEM 5  /* device allocation failed                                           */
+
+/* Integrand catalog (DESIGN.md "Integrand catalog"); the reference's `f` is user Julia code,
+ * a device kernel needs it as data. */
+#define TCI_F_SUM 0      /* f(x) = sum(x)                               (test_batcheval.jl:19) */
+#define TCI_F_LORENTZ 1  /* f(x) = p0 / (sum(x.^2) + 1)                 (README.md:21-29)      */
+#define TCI_F_TABLE 2    /* f(x) = p[x] over a dense column-major tensor                       */
+#define TCI_F_GAUSS 3    /* f(x) = exp(-(p0 * sum((x .- p1).^2)))        (BASELINE config 3)    */
+#define TCI_F_GAUSSMIX 4 /* f(x) = sum_k w_k exp(-(a * sum((x .- c_k).^2)))                   */
+#define TCI_F_QOSC 5     /* quantics x: exp(-p0 x) sin(p1 x^p2)         (test_tensorci2.jl:437) */
+#define TCI_F_QEXP 6     /* quantics x: p0 exp(-p1 x) + p2 exp(-p3 x)   (test_tensorci2.jl:65)  */
+#define TCI_F_TT 7       /* tensor-train evaluation (test_tensorci2.jl:477-502, TTCache as f)   */
+
+typedef struct tci_ctx tci_ctx;
+typedef struct tci_func tci_func;
+
+/* ---------------------------------------------------------------- context */
+int tci_ctx_create(int device, tci_ctx** out);
+int tci_ctx_destroy(tci_ctx* ctx);
+const char* tci_last_error(const tci_ctx* ctx);
+/* Device stream the context launches on (a hipStream_t as an opaque pointer), e.g. for
+ * hipEvent timing around _d calls. */
+void* tci_ctx_stream(tci_ctx* ctx);
+int tci_ctx_synchronize(tci_ctx* ctx);
+/* Average device time (ms) of the last call's dominant kernel family, measured with hipEvents
+ * on the context stream: family 0 = rrLU fused Schur update + argmax, 1 = batch evaluation. */
+int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
+int tci_set_timing(tci_ctx* ctx, int enabled);
+
+/* ------------------------------------------------------------ integrands */
+/* Uploads an integrand's parameters to the device once; localdims has L entries. */
+int tci_func_create(tci_ctx* ctx, int kind, const double* params, int64_t nparams,
+                    const int32_t* localdims, int32_t L, tci_func** out);
+int tci_func_destroy(tci_func* f);
+
+/* ----------------------------------------------------------- batch eval
+ * Replaces _batchevaluate_dispatch (batcheval.jl:131-175) plus maxabs (util.jl:34-43) as used by
+ * updatemaxsample! (tensorci2.jl:636-638).
+ * out[i + m*c + m*D*j] = f([I_i..., c..., J_j...]) for M = 0 or 1 centre legs (D = localdims[nl]
+ * when M = 1). I: m x nl, J: n x nr (row-major entries, 1-based). *maxabs = max(|out|) with
+ * Julia's NaN-propagating max. ldo = leading dimension of out (>= m*D). */
+int tci_batcheval_h(tci_ctx* ctx, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                    const int32_t* J, int64_t n, int32_t nr, int32_t M, double* out, int64_t ldo,
+                    double* maxabs);
+int tci_batcheval_d(tci_ctx* ctx, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                    const int32_t* J, int64_t n, int32_t nr, int32_t M, double* d_out,
+                    int64_t ldo, double* maxabs);
+
+/* ------------------------------------------------------------------ rrLU
+ * Replaces rrlu / rrlu! / _optimizerrlu! (matrixlu.jl:346-463) with identical arithmetic: full
+ * pivoting by abs2 argmax (ties -> smallest column, then row; matrixlu.jl:46-87), physical row and
+ * column swaps, true-division normalisation and separate multiply/subtract rank-1 updates.
+ * Outputs mirror the rrLU struct (matrixlu.jl:200-207):
+ *   rowperm[m], colperm[n]  (1-based),  L: m x maxrank (ld m), U: maxrank x n (ld ldu >= maxrank),
+ *   only the first *npivot columns of L / rows of U are meaningful; *lasterror = lu.error.
+ * Pass NULL for L/U to skip them. */
+int tci_rrlu_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+               double reltol, double abstol, int leftorth, int64_t* rowperm, int64_t* colperm,
+               double* L, double* U, int64_t ldu, int64_t* npivot, double* lasterror);
+/* rrlu! on a device matrix: factorises d_A (column-major, ld lda; lda even) IN PLACE and leaves
+ * the packed factors there (L below the diagonal, U on/above it, like the reference's A after
+ * _optimizerrlu!). Permutations are returned to the host. */
+int tci_rrlu_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
+                       int64_t maxrank, double reltol, double abstol, int leftorth,
+                       int64_t* rowperm, int64_t* colperm, int64_t* npivot, double* lasterror,
+                       double* pivoterrors);
+
+/* ------------------------------------------------------------ MatrixLUCI
+ * Replaces MatrixLUCI(A; kw...) + left/right/pivoterrors (matrixluci.jl:55-57, 161-311):
+ * leftorth: left = colstimespivotinv (TRSM), right = rowmatrix (GEMM);
+ * otherwise left = colmatrix (GEMM), right = pivotinvtimesrows (TRSM).
+ * left: m x np (ld m), right: np x n (ld np), rowidx/colidx: np pivot indices (1-based),
+ * pivoterrors: np + 1 values (matrixlu.jl:799). Capacities: maxrank. */
+int tci_luci_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+               double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
+               double* pivoterrors, double* left, double* right, int64_t* npivot);
+
+/* --------------------------------------------------------- 2-site update
+ * Replaces the :full branch of updatepivots! (tensorci2.jl:842-928) with Pi kept on the device:
+ * Pi = f(rows x cols) -> maxabs -> rrLU -> pivot rows/cols -> (optionally) MatrixLUCI factors.
+ * rows: m x nl, cols: n x nr (row-major entries, 1-based, already the union/kronecker sets).
+ * Outputs: rowidx/colidx (np entries, 1-based positions into rows/cols, in pivot order),
+ * pivoterrors (np+1), *maxabs, and if want_factors: left (m x np), right (np x n).
+ * The same entry serves sweep1site! (tensorci2.jl:679-709) with rows = kronecker(Iset, d). */
+int tci_update_pivots_h(tci_ctx* ctx, const tci_func* f, const int32_t* rows, int64_t m,
+                        int32_t nl, const int32_t* cols, int64_t n, int32_t nr, int64_t maxrank,
+                        double reltol, double abstol, int leftorth, int want_factors,
+                        int64_t* rowidx, int64_t* colidx, double* pivoterrors, int64_t* npivot,
+                        double* maxabs, double* left, double* right);
+
+/* ---------------------------------------------------- site-tensor solve
+ * Replaces setsitetensor!(tci, f, b) (tensorci2.jl:599-629): Pi1 = f(Iset_b x d x Jset_b),
+ * P = f(Iset_{b+1} x Jset_b), T = Pi1 * P^-1 (partial-pivot LU of P^T, like getrf/getrs).
+ * If Inext is NULL (last site) T = Pi1. T: (|I_b| d) x |J_b| column-major. */
+int tci_sitetensor_h(tci_ctx* ctx, const tci_func* f, const int32_t* Ib, int64_t nIb, int32_t wI,
+                     const int32_t* Jb, int64_t nJb, int32_t wJ, const int32_t* Inext,
+                     int64_t nInext, double* T, double* maxabs);
+
+/* ----------------------------------------------------- synthetic inputs
+ * Fills d_A (m x n, ld lda) with U[0,1): splitmix64(seed * 0xD1B54A32D192ED03 + (i + m*j)) >> 11
+ * times 2^-53 -- the same stream as the oracle's orc_fill_uniform. */
+int tci_fill_uniform_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
+                       uint64_t seed);
+
+/* ------------------------------------------------------------ device mem */
+int tci_malloc_d(tci_ctx* ctx, void** p, int64_t bytes);
+int tci_free_d(tci_ctx* ctx, void* p);
+int tci_memcpy_h2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int tci_memcpy_d2h(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int tci_memcpy_d2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCI_HIP_H */

@@ -1,0 +1,627 @@
+// tci_abi.cpp -- the C ABI of libtci_hip.so (include/tci_hip.h): contexts, device workspaces and
+// the host-side orchestration of the per-pivot kernel sequence. All compute is in
+// tci_device.hip; nothing here falls back to the CPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/tci_hip.h"
+#include "tci_internal.h"
+
+using tci::Cand;
+using tci::FuncDev;
+using tci::RrluState;
+
+struct tci_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // workspaces (grown on demand, reused across calls)
+    double* dA = nullptr;
+    size_t capA = 0;  // doubles
+    Cand* cand = nullptr;
+    size_t capCand = 0;
+    RrluState* st = nullptr;
+    RrluState* hst = nullptr;  // pinned
+    int64_t* rowperm = nullptr;
+    int64_t* colperm = nullptr;
+    size_t capPerm = 0;
+    size_t capColperm = 0;
+    double* ybuf = nullptr;
+    size_t capY = 0;
+    int* flag = nullptr;
+    int* hflag = nullptr;  // pinned
+    unsigned long long* maxbits = nullptr;
+    unsigned long long* hmaxbits = nullptr;  // pinned
+    void* scratch = nullptr;
+    size_t capScratch = 0;
+    int32_t* dI = nullptr;
+    size_t capI = 0;
+    int32_t* dJ = nullptr;
+    size_t capJ = 0;
+    double* dF1 = nullptr;  // factor / auxiliary buffers
+    size_t capF1 = 0;
+    double* dF2 = nullptr;
+    size_t capF2 = 0;
+    double* dDiag = nullptr;
+    size_t capDiag = 0;
+    int* dPiv = nullptr;
+    size_t capPiv = 0;
+    // kernel timing (family 0: fused update+argmax, 1: batch evaluation)
+    bool timing = false;
+    std::vector<hipEvent_t> evpool;
+    size_t evused = 0;
+    std::vector<std::pair<int, size_t>> evpairs;  // (family, index of start event)
+    double fam_ms[2] = {0, 0};
+    int64_t fam_n[2] = {0, 0};
+};
+
+struct tci_func {
+    tci_ctx* ctx = nullptr;
+    int kind = 0;
+    int L = 0;
+    std::vector<int32_t> localdims;
+    double* dparams = nullptr;
+    int32_t* dld = nullptr;
+    int64_t* dstrides = nullptr;
+    int64_t nparams = 0;
+    FuncDev view() const {
+        FuncDev f;
+        f.kind = kind;
+        f.L = L;
+        f.localdims = dld;
+        f.params = dparams;
+        f.nparams = nparams;
+        f.strides = dstrides;
+        return f;
+    }
+};
+
+namespace {
+
+int set_err(tci_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                    \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, TCI_ERR_DEVICE,                                              \
+                           std::string(#expr) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+template <class T>
+int ensure(tci_ctx* c, T** p, size_t* cap, size_t n) {
+    if (n <= *cap && *p) return TCI_OK;
+    size_t want = std::max<size_t>(n, 64);
+    if (*p) {
+        hipStreamSynchronize(c->stream);
+        hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+    }
+    if (hipMalloc((void**)p, want * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return set_err(c, TCI_ERR_NOMEM, "device allocation of " + std::to_string(want * sizeof(T)) +
+                                             " bytes failed");
+    }
+    *cap = want;
+    return TCI_OK;
+}
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+void ev_begin(tci_ctx* c, int fam) {
+    if (!c->timing) return;
+    if (c->evused + 2 > c->evpool.size()) {
+        size_t add = std::max<size_t>(64, c->evpool.size());
+        for (size_t i = 0; i < add; ++i) {
+            hipEvent_t e;
+            hipEventCreate(&e);
+            c->evpool.push_back(e);
+        }
+    }
+    c->evpairs.push_back({fam, c->evused});
+    hipEventRecord(c->evpool[c->evused], c->stream);
+    c->evused += 2;
+}
+void ev_end(tci_ctx* c) {
+    if (!c->timing) return;
+    hipEventRecord(c->evpool[c->evpairs.back().second + 1], c->stream);
+}
+void ev_reset(tci_ctx* c) {
+    c->evused = 0;
+    c->evpairs.clear();
+    c->fam_ms[0] = c->fam_ms[1] = 0;
+    c->fam_n[0] = c->fam_n[1] = 0;
+}
+void ev_collect(tci_ctx* c) {
+    if (!c->timing) return;
+    hipStreamSynchronize(c->stream);
+    for (auto& pr : c->evpairs) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, c->evpool[pr.second], c->evpool[pr.second + 1]);
+        c->fam_ms[pr.first] += ms;
+        c->fam_n[pr.first] += 1;
+    }
+    c->evpairs.clear();
+    c->evused = 0;
+}
+
+constexpr int kCB = 16;       // columns per update tile
+constexpr int kMaxGrid = 2048;  // 8 workgroups per CU x 256 CUs
+
+// The per-pivot loop of _optimizerrlu! (matrixlu.jl:346-369) on a device matrix. Leaves
+// rowperm/colperm/state on the device; returns np and lu.error.
+int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+                double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out) {
+    int st;
+    if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
+    if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
+    const int mi = (int)m, ni = (int)n;
+    tci::launch_init_state(c->stream, c->st, c->rowperm, mi, c->colperm, ni);
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    if (m == 0 || n == 0 || mr == 0) {
+        HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *np_out = 0;
+        *err_out = (0 >= std::min(m, n)) ? 0.0 : c->hst->error;
+        return TCI_OK;
+    }
+    int ncand = tci::argmax_grid(mi, ni, -1, kCB, kMaxGrid);
+    tci::launch_argmax_update(c->stream, false, dA, lda, mi, ni, -1, c->ybuf, c->st, c->cand, ncand,
+                              kCB);
+    int64_t k = 0, chunk = 2;
+    bool stopped = false;
+    while (k < mr && !stopped) {
+        const int64_t kend = std::min<int64_t>(k + chunk, mr);
+        for (int64_t kk = k; kk < kend; ++kk) {
+            const int ki = (int)kk;
+            tci::launch_select(c->stream, dA, lda, mi, ni, ki, c->cand, ncand, c->st, reltol, abstol);
+            tci::launch_swap(c->stream, dA, lda, mi, ni, ki, c->st, c->rowperm, c->colperm, c->ybuf,
+                             leftorth);
+            if (kk + 1 < mr) {
+                const int g = tci::argmax_grid(mi, ni, ki, kCB, kMaxGrid);
+                ev_begin(c, 0);
+                tci::launch_argmax_update(c->stream, true, dA, lda, mi, ni, ki, c->ybuf, c->st,
+                                          c->cand, g, kCB);
+                ev_end(c);
+                ncand = g;
+            }
+        }
+        k = kend;
+        if (k < mr) {
+            HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (c->hst->done) stopped = true;
+            chunk = std::min<int64_t>(chunk * 2, 64);
+        }
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int64_t np = c->hst->np;
+    double err = c->hst->error;
+    if (np >= std::min(m, n)) err = 0.0;  // matrixlu.jl:391-393
+    *np_out = np;
+    *err_out = err;
+    return TCI_OK;
+}
+
+int nan_check(tci_ctx* c, const double* dA, int64_t lda, int64_t m, int64_t n, int64_t np) {
+    if (np <= 0) return TCI_OK;
+    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
+    tci::launch_nan_check(c->stream, dA, lda, (int)m, (int)n, (int)np, c->flag);
+    HIPCHK(c, hipMemcpyAsync(c->hflag, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (*c->hflag & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+    if (*c->hflag & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    return TCI_OK;
+}
+
+int fetch_perms(tci_ctx* c, int64_t m, int64_t n, int64_t* rowperm, int64_t* colperm,
+                int64_t nrow, int64_t ncol) {
+    if (rowperm && nrow > 0)
+        HIPCHK(c, hipMemcpyAsync(rowperm, c->rowperm, nrow * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                 c->stream));
+    if (colperm && ncol > 0)
+        HIPCHK(c, hipMemcpyAsync(colperm, c->colperm, ncol * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (rowperm)
+        for (int64_t i = 0; i < nrow; ++i) rowperm[i] += 1;
+    if (colperm)
+        for (int64_t j = 0; j < ncol; ++j) colperm[j] += 1;
+    (void)m;
+    (void)n;
+    return TCI_OK;
+}
+
+int pivot_errors(tci_ctx* c, const double* dA, int64_t lda, int64_t np, double err, double* out) {
+    if (!out) return TCI_OK;
+    int st;
+    if (np > 0) {
+        if ((st = ensure(c, &c->dDiag, &c->capDiag, (size_t)np + 1))) return st;
+        tci::launch_gather_diag(c->stream, dA, lda, (int)np, c->dDiag);
+        HIPCHK(c, hipMemcpyAsync(out, c->dDiag, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    out[np] = err;
+    return TCI_OK;
+}
+
+int upload_matrix(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, int64_t* ld_d) {
+    const int64_t ld = round_up(std::max<int64_t>(m, 1), 16);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(ld * std::max<int64_t>(n, 1))))) return st;
+    if (m > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(c->dA, ld * sizeof(double), A, lda * sizeof(double),
+                                   m * sizeof(double), n, hipMemcpyHostToDevice, c->stream));
+    *ld_d = ld;
+    return TCI_OK;
+}
+
+int upload_index(tci_ctx* c, int32_t** d, size_t* cap, const int32_t* h, int64_t count, int32_t w) {
+    int st;
+    size_t nel = (size_t)std::max<int64_t>(count * w, 1);
+    if ((st = ensure(c, d, cap, nel))) return st;
+    if (count * w > 0)
+        HIPCHK(c, hipMemcpyAsync(*d, h, count * w * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    return TCI_OK;
+}
+
+// batch evaluation into a device buffer (column-major, ld ldo). *maxabs = max|out|.
+int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
+                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo,
+                     double* maxabs) {
+    if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    if (M < 0 || M > 1) return set_err(c, TCI_ERR_ARG, "only M = 0 or M = 1 centre legs are supported");
+    const int D = M ? f->localdims[nl] : 1;
+    if (ldo < m * D) return set_err(c, TCI_ERR_ARG, "ldo < m * prod(centre dims)");
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    if (m > 0 && n > 0) {
+        FuncDev fv = f->view();
+        int st;
+        int64_t sb = tci::batcheval_scratch_bytes(fv, (int)m, D, (int)n);
+        if (sb > 0 && (st = ensure(c, (char**)&c->scratch, &c->capScratch, (size_t)sb))) return st;
+        ev_begin(c, 1);
+        tci::launch_batcheval(c->stream, fv, dI, (int)m, nl, dJ, (int)n, nr, M, D, dout, ldo,
+                              c->maxbits, c->scratch);
+        ev_end(c);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (maxabs) {
+        double v;
+        unsigned long long b = *c->hmaxbits;
+        memcpy(&v, &b, sizeof v);
+        *maxabs = v;
+    }
+    return TCI_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+int tci_ctx_create(int device, tci_ctx** out) {
+    if (!out) return TCI_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return TCI_ERR_DEVICE;
+    if (device < 0 || device >= ndev) return TCI_ERR_ARG;
+    tci_ctx* c = new tci_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return TCI_ERR_DEVICE;
+    }
+    bool ok = hipMalloc((void**)&c->st, sizeof(RrluState)) == hipSuccess &&
+              hipHostMalloc((void**)&c->hst, sizeof(RrluState), 0) == hipSuccess &&
+              hipMalloc((void**)&c->flag, sizeof(int)) == hipSuccess &&
+              hipHostMalloc((void**)&c->hflag, sizeof(int), 0) == hipSuccess &&
+              hipMalloc((void**)&c->maxbits, sizeof(unsigned long long)) == hipSuccess &&
+              hipHostMalloc((void**)&c->hmaxbits, sizeof(unsigned long long), 0) == hipSuccess;
+    if (!ok) {
+        tci_ctx_destroy(c);
+        return TCI_ERR_NOMEM;
+    }
+    *out = c;
+    return TCI_OK;
+}
+
+int tci_ctx_destroy(tci_ctx* c) {
+    if (!c) return TCI_OK;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    auto fr = [](void* p) { if (p) hipFree(p); };
+    fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->ybuf); fr(c->flag);
+    fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
+    fr(c->dPiv);
+    if (c->hst) hipHostFree(c->hst);
+    if (c->hflag) hipHostFree(c->hflag);
+    if (c->hmaxbits) hipHostFree(c->hmaxbits);
+    for (auto e : c->evpool) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return TCI_OK;
+}
+
+const char* tci_last_error(const tci_ctx* c) { return c ? c->err.c_str() : "null context"; }
+void* tci_ctx_stream(tci_ctx* c) { return c ? (void*)c->stream : nullptr; }
+int tci_ctx_synchronize(tci_ctx* c) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+int tci_set_timing(tci_ctx* c, int enabled) {
+    c->timing = enabled != 0;
+    ev_reset(c);
+    return TCI_OK;
+}
+int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* launches) {
+    if (family < 0 || family > 1) return set_err(c, TCI_ERR_ARG, "family must be 0 or 1");
+    ev_collect(c);
+    if (total_ms) *total_ms = c->fam_ms[family];
+    if (launches) *launches = c->fam_n[family];
+    return TCI_OK;
+}
+
+int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
+                    const int32_t* localdims, int32_t L, tci_func** out) {
+    if (!c || !out) return TCI_ERR_ARG;
+    if (kind < TCI_F_SUM || kind > TCI_F_TT) return set_err(c, TCI_ERR_ARG, "unknown integrand kind");
+    if (L < 1) return set_err(c, TCI_ERR_ARG, "L must be >= 1");
+    if (L > 62 && (kind == TCI_F_QOSC || kind == TCI_F_QEXP))
+        return set_err(c, TCI_ERR_ARG, "quantics integrands support at most 62 legs");
+    tci_func* f = new tci_func();
+    f->ctx = c;
+    f->kind = kind;
+    f->L = L;
+    f->localdims.assign(localdims, localdims + L);
+    f->nparams = nparams;
+    std::vector<int64_t> strides(L + 1, 1);
+    for (int t = 0; t < L; ++t) strides[t + 1] = strides[t] * localdims[t];
+    bool ok = hipMalloc((void**)&f->dparams, std::max<int64_t>(nparams, 1) * sizeof(double)) == hipSuccess &&
+              hipMalloc((void**)&f->dld, L * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc((void**)&f->dstrides, (L + 1) * sizeof(int64_t)) == hipSuccess;
+    if (!ok) {
+        tci_func_destroy(f);
+        return set_err(c, TCI_ERR_NOMEM, "integrand allocation failed");
+    }
+    if (nparams > 0) hipMemcpy(f->dparams, params, nparams * sizeof(double), hipMemcpyHostToDevice);
+    hipMemcpy(f->dld, localdims, L * sizeof(int32_t), hipMemcpyHostToDevice);
+    hipMemcpy(f->dstrides, strides.data(), (L + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
+    *out = f;
+    return TCI_OK;
+}
+
+int tci_func_destroy(tci_func* f) {
+    if (!f) return TCI_OK;
+    if (f->dparams) hipFree(f->dparams);
+    if (f->dld) hipFree(f->dld);
+    if (f->dstrides) hipFree(f->dstrides);
+    delete f;
+    return TCI_OK;
+}
+
+int tci_batcheval_d(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                    const int32_t* J, int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo,
+                    double* maxabs) {
+    if (!c || !f) return TCI_ERR_ARG;
+    int st;
+    if ((st = upload_index(c, &c->dI, &c->capI, I, m, nl))) return st;
+    if ((st = upload_index(c, &c->dJ, &c->capJ, J, n, nr))) return st;
+    return batcheval_device(c, f, c->dI, m, nl, c->dJ, n, nr, M, d_out, ldo, maxabs);
+}
+
+int tci_batcheval_h(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                    const int32_t* J, int64_t n, int32_t nr, int32_t M, double* out, int64_t ldo,
+                    double* maxabs) {
+    if (!c || !f) return TCI_ERR_ARG;
+    if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    const int64_t D = M ? f->localdims[nl] : 1;
+    const int64_t mR = m * D;
+    const int64_t ld = round_up(std::max<int64_t>(mR, 1), 2);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = tci_batcheval_d(c, f, I, m, nl, J, n, nr, M, c->dA, ld, maxabs))) return st;
+    if (mR > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(out, ldo * sizeof(double), c->dA, ld * sizeof(double),
+                                   mR * sizeof(double), n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_rrlu_inplace_d(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+                       double reltol, double abstol, int leftorth, int64_t* rowperm,
+                       int64_t* colperm, int64_t* npivot, double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || lda < m || (lda & 1) || ((uintptr_t)dA & 15))
+        return set_err(c, TCI_ERR_ARG, "rrlu: need lda >= m, lda even and a 16-byte aligned matrix");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int st;
+    if ((st = rrlu_device(c, dA, m, n, lda, maxrank, reltol, abstol, leftorth, npivot, lasterror)))
+        return st;
+    if ((st = nan_check(c, dA, lda, m, n, *npivot))) return st;
+    if ((st = fetch_perms(c, m, n, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    return pivot_errors(c, dA, lda, *npivot, *lasterror, pivoterrors);
+}
+
+int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+               double reltol, double abstol, int leftorth, int64_t* rowperm, int64_t* colperm,
+               double* L, double* U, int64_t ldu, int64_t* npivot, double* lasterror) {
+    if (!c || !npivot || !lasterror || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || lda < std::max<int64_t>(m, 1) - (m == 0))
+        return set_err(c, TCI_ERR_ARG, "rrlu: invalid dimensions");
+    int64_t ld;
+    int st;
+    if ((st = upload_matrix(c, A, m, n, lda, &ld))) return st;
+    if ((st = tci_rrlu_inplace_d(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, rowperm,
+                                 colperm, npivot, lasterror, nullptr)))
+        return st;
+    const int64_t np = *npivot;
+    if (np > 0 && (L || U)) {
+        if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(m * np)))) return st;
+        if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(np * n)))) return st;
+        tci::launch_extract_LU(c->stream, c->dA, ld, (int)m, (int)n, (int)np, leftorth,
+                               L ? c->dF1 : nullptr, m, U ? c->dF2 : nullptr, np);
+        if (L)
+            HIPCHK(c, hipMemcpyAsync(L, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
+                                     c->stream));
+        if (U)
+            HIPCHK(c, hipMemcpy2DAsync(U, ldu * sizeof(double), c->dF2, np * sizeof(double),
+                                       np * sizeof(double), n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return TCI_OK;
+}
+
+// factors + outputs after rrlu_device on c->dA (ld)
+static int luci_outputs(tci_ctx* c, int64_t m, int64_t n, int64_t ld, int leftorth, int64_t np,
+                        double err, int64_t* rowidx, int64_t* colidx, double* pivoterrs,
+                        double* left, double* right) {
+    int st;
+    if ((st = nan_check(c, c->dA, ld, m, n, np))) return st;
+    if ((st = pivot_errors(c, c->dA, ld, np, err, pivoterrs))) return st;
+    if (np > 0) {
+        if ((st = fetch_perms(c, m, n, rowidx, colidx, rowidx ? np : 0, colidx ? np : 0))) return st;
+    }
+    if (np > 0 && (left || right)) {
+        if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(m * np)))) return st;
+        if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(np * n)))) return st;
+        tci::launch_luci_factors(c->stream, c->dA, ld, (int)m, (int)n, (int)np, leftorth, c->rowperm,
+                                 c->colperm, left ? c->dF1 : nullptr, right ? c->dF2 : nullptr);
+        HIPCHK(c, hipGetLastError());
+        if (left)
+            HIPCHK(c, hipMemcpyAsync(left, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
+                                     c->stream));
+        if (right)
+            HIPCHK(c, hipMemcpyAsync(right, c->dF2, np * n * sizeof(double), hipMemcpyDeviceToHost,
+                                     c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return TCI_OK;
+}
+
+int tci_luci_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+               double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
+               double* pivoterrs, double* left, double* right, int64_t* npivot) {
+    if (!c || !npivot) return TCI_ERR_ARG;
+    int64_t ld, np;
+    double err;
+    int st;
+    if ((st = upload_matrix(c, A, m, n, lda, &ld))) return st;
+    if ((st = rrlu_device(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, &np, &err)))
+        return st;
+    *npivot = np;
+    return luci_outputs(c, m, n, ld, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
+}
+
+int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int64_t m, int32_t nl,
+                        const int32_t* cols, int64_t n, int32_t nr, int64_t maxrank, double reltol,
+                        double abstol, int leftorth, int want_factors, int64_t* rowidx,
+                        int64_t* colidx, double* pivoterrs, int64_t* npivot, double* maxabs,
+                        double* left, double* right) {
+    if (!c || !f || !npivot) return TCI_ERR_ARG;
+    if (nl + nr != f->L) return set_err(c, TCI_ERR_ARG, "rows/cols widths must add up to L");
+    const int64_t ld = round_up(std::max<int64_t>(m, 1), 16);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = upload_index(c, &c->dI, &c->capI, rows, m, nl))) return st;
+    if ((st = upload_index(c, &c->dJ, &c->capJ, cols, n, nr))) return st;
+    if ((st = batcheval_device(c, f, c->dI, m, nl, c->dJ, n, nr, 0, c->dA, ld, maxabs))) return st;
+    int64_t np;
+    double err;
+    if ((st = rrlu_device(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, &np, &err)))
+        return st;
+    *npivot = np;
+    return luci_outputs(c, m, n, ld, leftorth, np, err, rowidx, colidx, pivoterrs,
+                        want_factors ? left : nullptr, want_factors ? right : nullptr);
+}
+
+int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t nIb, int32_t wI,
+                     const int32_t* Jb, int64_t nJb, int32_t wJ, const int32_t* Inext,
+                     int64_t nInext, double* T, double* maxabs) {
+    if (!c || !f || !T) return TCI_ERR_ARG;
+    if (wI + 1 + wJ != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    const int64_t d = f->localdims[wI];
+    const int64_t R = nIb * d;
+    const int64_t ldR = std::max<int64_t>(R, 1);
+    int st;
+    if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(ldR * std::max<int64_t>(nJb, 1))))) return st;
+    if ((st = upload_index(c, &c->dI, &c->capI, Ib, nIb, wI))) return st;
+    if ((st = upload_index(c, &c->dJ, &c->capJ, Jb, nJb, wJ))) return st;
+    if ((st = batcheval_device(c, f, c->dI, nIb, wI, c->dJ, nJb, wJ, 1, c->dF1, ldR, maxabs)))
+        return st;
+    if (!Inext) {
+        if (R * nJb > 0)
+            HIPCHK(c, hipMemcpyAsync(T, c->dF1, R * nJb * sizeof(double), hipMemcpyDeviceToHost,
+                                     c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return TCI_OK;
+    }
+    if (nInext != nJb) return set_err(c, TCI_ERR_NONSQ, "Pivot matrix is not square!");
+    const int64_t r = nJb;
+    if (r == 0 || R == 0) return TCI_OK;
+    // P = f(Inext x Jb) (r x r) into dF2; T into dA
+    if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+    if ((st = upload_index(c, &c->dI, &c->capI, Inext, nInext, wI + 1))) return st;
+    if ((st = batcheval_device(c, f, c->dI, nInext, wI + 1, c->dJ, nJb, wJ, 0, c->dF2, r, nullptr)))
+        return st;
+    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_fill_uniform_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda, uint64_t seed) {
+    if (!c || lda < m) return TCI_ERR_ARG;
+    tci::launch_fill_uniform(c->stream, d_A, m, n, lda, seed);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_malloc_d(tci_ctx* c, void** p, int64_t bytes) {
+    if (hipMalloc(p, (size_t)std::max<int64_t>(bytes, 16)) != hipSuccess)
+        return set_err(c, TCI_ERR_NOMEM, "hipMalloc failed");
+    return TCI_OK;
+}
+int tci_free_d(tci_ctx* c, void* p) {
+    if (p) HIPCHK(c, hipFree(p));
+    return TCI_OK;
+}
+int tci_memcpy_h2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+int tci_memcpy_d2h(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+int tci_memcpy_d2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+}  // extern "C"

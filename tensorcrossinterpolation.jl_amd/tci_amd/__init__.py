@@ -1,0 +1,17 @@
+"""tci_amd -- MI355X-native TCI2 hot path for TensorCrossInterpolation.jl.
+
+Host-side mirror of the reference's API for the path this package replaces (rrlu / MatrixLUCI /
+batch evaluation / TensorCI2 / crossinterpolate2); all compute runs in libtci_hip.so (gfx950).
+"""
+from ._lib import Context, TCIArgumentError, TCIDeviceError, TCIError, context, load
+from .batcheval import (F_GAUSS, F_GAUSSMIX, F_LORENTZ, F_QEXP, F_QOSC, F_SUM, F_TABLE, F_TT,
+                        GPUBatchEvaluator, gauss, gaussmix, lorentz, quantics_bits, quantics_exp,
+                        quantics_osc, sum_, table, tensortrain_function)
+from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder
+from .matrixlu import (DeviceMatrix, colindices, diag, lastpivoterror, ldiv, left, npivots, pivoterrors,
+                       right, rowindices, rrLU, rrlu, rrlu_inplace_device)
+from .matrixluci import MatrixLUCI
+from .tensorci2 import (TensorCI2, convergencecriterion, crossinterpolate2, forwardsweep, kronecker_left,
+                        kronecker_right, union_sets)
+
+__all__ = [name for name in dir() if not name.startswith("_")]

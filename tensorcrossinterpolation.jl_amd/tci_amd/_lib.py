@@ -1,0 +1,166 @@
+"""ctypes binding of libtci_hip.so (include/tci_hip.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is visible, every entry
+point raises -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TCI_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libtci_hip.so"))
+
+TCI_OK, TCI_ERR_ARG, TCI_ERR_NAN, TCI_ERR_NONSQ, TCI_ERR_DEVICE, TCI_ERR_NOMEM = range(6)
+
+i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+vp = C.c_void_p
+dbl = C.c_double
+i64 = C.c_int64
+i32 = C.c_int32
+pi64 = C.POINTER(C.c_int64)
+pdbl = C.POINTER(C.c_double)
+
+
+class TCIError(RuntimeError):
+    """Raised for TCI_ERR_* codes; the message follows the reference's exception text."""
+
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+class TCIArgumentError(TCIError, ValueError):
+    pass
+
+
+class TCIDeviceError(TCIError):
+    pass
+
+
+# optional pointers (NULL allowed) use c_void_p and are passed via _ptr()
+SIGNATURES = {
+    "tci_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
+    "tci_ctx_destroy": ([vp], C.c_int),
+    "tci_last_error": ([vp], C.c_char_p),
+    "tci_ctx_stream": ([vp], vp),
+    "tci_ctx_synchronize": ([vp], C.c_int),
+    "tci_last_kernel_stats": ([vp, C.c_int, pdbl, pi64], C.c_int),
+    "tci_set_timing": ([vp, C.c_int], C.c_int),
+    "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
+    "tci_func_destroy": ([vp], C.c_int),
+    "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
+    "tci_batcheval_d": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
+    "tci_rrlu_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, i64, pi64, pdbl],
+                   C.c_int),
+    "tci_rrlu_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, pi64, pdbl, vp],
+                           C.c_int),
+    "tci_luci_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),
+    "tci_update_pivots_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i64, dbl, dbl, C.c_int, C.c_int, vp,
+                             vp, vp, pi64, pdbl, vp, vp], C.c_int),
+    "tci_sitetensor_h": ([vp, vp, vp, i64, i32, vp, i64, i32, vp, i64, vp, pdbl], C.c_int),
+    "tci_fill_uniform_d": ([vp, vp, i64, i64, i64, C.c_uint64], C.c_int),
+    "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
+    "tci_free_d": ([vp, vp], C.c_int),
+    "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),
+    "tci_memcpy_d2h": ([vp, vp, vp, i64], C.c_int),
+    "tci_memcpy_d2d": ([vp, vp, vp, i64], C.c_int),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Loads libtci_hip.so (raises if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise TCIDeviceError(TCI_ERR_DEVICE,
+                                     f"libtci_hip.so not found at {LIB_PATH}: build it with "
+                                     "`python -c 'import __graft_entry__ as g; g.build()'` "
+                                     "(no CPU fallback exists)")
+            lib = C.CDLL(LIB_PATH)
+            for name, (args, res) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = lib
+    return _lib
+
+
+def ptr(a):
+    """ctypes pointer of a numpy array (or None -> NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(vp)
+
+
+class Context:
+    """One tci_ctx (device stream + workspaces). Use `context()` for the per-thread default."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = vp()
+        st = self.lib.tci_ctx_create(device, C.byref(h))
+        if st != TCI_OK:
+            raise TCIDeviceError(st, f"tci_ctx_create(device={device}) failed with code {st} "
+                                     "(no visible MI355X / HIP runtime?)")
+        self.h = h
+        self.device = device
+
+    def check(self, st):
+        if st == TCI_OK:
+            return
+        msg = self.lib.tci_last_error(self.h).decode(errors="replace")
+        if st == TCI_ERR_ARG:
+            raise TCIArgumentError(st, msg)
+        if st == TCI_ERR_DEVICE or st == TCI_ERR_NOMEM:
+            raise TCIDeviceError(st, msg)
+        raise TCIError(st, msg)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tci_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, on):
+        self.check(self.lib.tci_set_timing(self.h, int(bool(on))))
+
+    def kernel_stats(self, family):
+        ms = C.c_double()
+        n = C.c_int64()
+        self.check(self.lib.tci_last_kernel_stats(self.h, family, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    @property
+    def stream(self):
+        return self.lib.tci_ctx_stream(self.h)
+
+    def synchronize(self):
+        self.check(self.lib.tci_ctx_synchronize(self.h))
+
+
+_tls = threading.local()
+
+
+def context(device=None):
+    """Default per-thread context on `device` (LOCAL_RANK or 0)."""
+    if device is None:
+        device = int(os.environ.get("TCI_DEVICE", "0"))
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    if device not in ctxs:
+        ctxs[device] = Context(device)
+    return ctxs[device]

@@ -1,0 +1,527 @@
+"""TCI2 driver -- host-side mirror of src/tensorci2.jl (plus the helpers it calls from
+globalsearch.jl, util.jl and sweepstrategies.jl), with the hot path on the GPU.
+
+This is what the Julia shim of INTEGRATION.md does inside Julia: the driver logic stays the
+reference's, and every Pi assembly + rrLU + MatrixLUCI of `updatepivots!` / `sweep1site!`, every
+`setsitetensor!` solve, runs in libtci_hip.so with Pi resident in HBM (tci_update_pivots_h,
+tci_sitetensor_h). Only index sets, pivot errors and site tensors cross PCIe.
+
+Conventions: sites/bonds are 1-based in this API like the reference (b in 1..L-1); index sets
+are (count, width) int32 arrays of 1-based local indices.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .batcheval import GPUBatchEvaluator
+
+INT64_MAX = np.iinfo(np.int64).max
+
+
+# ------------------------------------------------------------------ helpers
+def jl_max(x, y):
+    """Base.max for Float64 (NaN-propagating, max(-0.0, 0.0) == 0.0)."""
+    if (y > x) or (np.signbit(y) < np.signbit(x)):
+        return x if np.isnan(x) else y
+    return y if np.isnan(y) else x
+
+
+def maxabs(maxval, value):
+    """maxabs(maxval, updates) (util.jl:34-43) given max|updates| computed on the device."""
+    return jl_max(abs(maxval), abs(value))
+
+
+def kronecker_right(Iset, localdim):
+    """kronecker(Iset, localdim) (tensorci2.jl:512-517): [is..., j], Iset fastest."""
+    n, w = Iset.shape
+    left = np.tile(Iset, (localdim, 1))
+    loc = np.repeat(np.arange(1, localdim + 1, dtype=np.int32), n)[:, None]
+    return np.ascontiguousarray(np.concatenate([left, loc], axis=1), dtype=np.int32)
+
+
+def kronecker_left(localdim, Jset):
+    """kronecker(localdim, Jset) (tensorci2.jl:524-529): [i, js...], i fastest."""
+    n, w = Jset.shape
+    loc = np.tile(np.arange(1, localdim + 1, dtype=np.int32), n)[:, None]
+    right = np.repeat(Jset, localdim, axis=0)
+    return np.ascontiguousarray(np.concatenate([loc, right], axis=1), dtype=np.int32)
+
+
+def union_sets(a, b):
+    """Julia union(a, b) on Vector{MultiIndex}: first-seen order, deduplicated."""
+    if b is None or len(b) == 0:
+        cat = a
+    else:
+        cat = np.concatenate([a, b], axis=0)
+    if len(cat) == 0:
+        return np.ascontiguousarray(cat, np.int32)
+    if cat.shape[1] == 0:
+        return np.zeros((1, 0), np.int32)
+    _, first = np.unique(cat, axis=0, return_index=True)
+    return np.ascontiguousarray(cat[np.sort(first)], np.int32)
+
+
+def pushunique(s, e):
+    """pushunique! (util.jl:94-98) for one MultiIndex."""
+    e = np.asarray(e, np.int32).reshape(1, -1)
+    if len(s) and (s.shape[1] == 0 or np.any(np.all(s == e, axis=1))):
+        return s
+    return np.concatenate([s, e], axis=0)
+
+
+def forwardsweep(sweepstrategy, iteration):
+    """forwardsweep (sweepstrategies.jl:41-50)."""
+    return sweepstrategy == "forward" or (sweepstrategy == "backandforth" and iteration % 2 == 1)
+
+
+def convergencecriterion(ranks, errors, nglobalpivots, tolerance, maxbonddim, ncheckhistory,
+                         checkconvglobalpivot=True):
+    """convergencecriterion (tensorci2.jl:947-966)."""
+    if len(errors) < ncheckhistory:
+        return False
+    lastranks = list(ranks[len(ranks) - ncheckhistory:])
+    lastngp = list(nglobalpivots[len(nglobalpivots) - ncheckhistory:])
+    lasterr = list(errors[len(errors) - ncheckhistory:])
+    return (all(e < tolerance for e in lasterr)
+            and (all(g == 0 for g in lastngp) if checkconvglobalpivot else True)
+            and min(lastranks) == lastranks[-1]) or all(r >= maxbonddim for r in lastranks)
+
+
+# ---------------------------------------------------------------- TensorCI2
+class TensorCI2:
+    """mutable struct TensorCI2{ValueType} (tensorci2.jl:50-93) for ValueType = Float64."""
+
+    def __init__(self, localdims):
+        localdims = [int(d) for d in localdims]
+        if len(localdims) <= 1:
+            raise ValueError("localdims should have at least 2 elements!")
+        n = len(localdims)
+        self.localdims = localdims
+        self.Iset = [np.zeros((0, b), np.int32) for b in range(n)]
+        self.Jset = [np.zeros((0, n - 1 - b), np.int32) for b in range(n)]
+        self.sitetensors = [np.zeros((0, d, 0)) for d in localdims]
+        self.pivoterrors = np.zeros(0)
+        self.bonderrors = np.zeros(n - 1)
+        self.maxsamplevalue = 0.0
+        self.Iset_history = []  # only the last entry is ever read (tensorci2.jl:1214-1216)
+        self.Jset_history = []
+
+    @classmethod
+    def from_function(cls, f, localdims, initialpivots=None):
+        """TensorCI2{V}(func, localdims, initialpivots) (tensorci2.jl:105-116)."""
+        tci = cls(localdims)
+        L = len(tci.localdims)
+        if initialpivots is None:
+            initialpivots = [[1] * L]
+        piv = np.asarray(initialpivots, np.int32).reshape(-1, L)
+        tci.addglobalpivots(piv)
+        vals = f.points(piv)
+        mx = None
+        for v in np.abs(vals):
+            mx = v if mx is None else jl_max(mx, v)
+        tci.maxsamplevalue = float(mx)
+        if not abs(tci.maxsamplevalue) > 0.0:
+            raise RuntimeError("maxsamplevalue is zero!")
+        tci.invalidatesitetensors()
+        return tci
+
+    @classmethod
+    def from_sets(cls, f, localdims, Iset, Jset):
+        """TensorCI2{V}(func, localdims, Iset, Jset) (tensorci2.jl:123-137)."""
+        tci = cls(localdims)
+        tci.Iset = [np.ascontiguousarray(np.asarray(s, np.int32).reshape(len(s), b)) for b, s in enumerate(Iset)]
+        n = len(tci.localdims)
+        tci.Jset = [np.ascontiguousarray(np.asarray(s, np.int32).reshape(len(s), n - 1 - b)) for b, s in enumerate(Jset)]
+        pivots = reconstractglobalpivotsfromijset(tci.localdims, tci.Iset, tci.Jset)
+        vals = f.points(pivots)
+        mx = None
+        for v in np.abs(vals):
+            mx = v if mx is None else jl_max(mx, v)
+        tci.maxsamplevalue = float(mx)
+        if not abs(tci.maxsamplevalue) > 0.0:
+            raise RuntimeError("maxsamplevalue is zero!")
+        tci.invalidatesitetensors()
+        return tci
+
+    # -- basic accessors (tensorci2.jl:189-289)
+    def __len__(self):
+        return len(self.localdims)
+
+    def linkdims(self):
+        return [len(self.Iset[b + 1]) for b in range(len(self) - 1)]
+
+    def rank(self):
+        return max(self.linkdims()) if len(self) > 1 else 0
+
+    def invalidatesitetensors(self):
+        for b in range(len(self)):
+            self.sitetensors[b] = np.zeros((0, 0, 0))
+
+    def issitetensorsavailable(self):
+        return all(t.size != 0 for t in self.sitetensors)
+
+    def maxbonderror(self):
+        m = self.bonderrors[0]
+        for e in self.bonderrors[1:]:
+            m = jl_max(m, e)
+        return float(m)
+
+    def pivoterror(self):
+        return self.maxbonderror()
+
+    def updatepivoterror(self, errors):
+        """updatepivoterror! (tensorci2.jl:252-260): elementwise max over zero-padded vectors."""
+        a, b = self.pivoterrors, np.asarray(errors, float)
+        n = max(len(a), len(b))
+        out = np.zeros(n)
+        for i in range(n):
+            out[i] = jl_max(a[i] if i < len(a) else 0.0, b[i] if i < len(b) else 0.0)
+        self.pivoterrors = out
+
+    def flushpivoterror(self):
+        self.pivoterrors = np.zeros(0)
+
+    def updateerrors(self, b, errors):
+        """updateerrors! (tensorci2.jl:281-289); b is 1-based."""
+        self.bonderrors[b - 1] = errors[-1]
+        self.updatepivoterror(errors)
+
+    def updatemaxsample(self, value):
+        self.maxsamplevalue = maxabs(self.maxsamplevalue, value)
+
+    def addglobalpivots(self, pivots):
+        """addglobalpivots! (tensorci2.jl:335-357)."""
+        L = len(self)
+        piv = np.asarray(pivots, np.int32).reshape(-1, L) if len(pivots) else np.zeros((0, L), np.int32)
+        for p in piv:
+            for b in range(L):
+                self.Iset[b] = pushunique(self.Iset[b], p[:b])
+                self.Jset[b] = pushunique(self.Jset[b], p[b + 1:])
+        if len(piv) > 0:
+            self.invalidatesitetensors()
+
+    def setsitetensor_(self, b, T):
+        """setsitetensor!(tci, b, T) (tensorci2.jl:536-545); b is 1-based."""
+        self.sitetensors[b - 1] = np.asarray(T).reshape(
+            (len(self.Iset[b - 1]), self.localdims[b - 1], len(self.Jset[b - 1])), order="F")
+
+    # -- hot path
+    def updatepivots(self, b, f, leftorthogonal, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX,
+                     extraIset=None, extraJset=None, compute_factors=True):
+        """updatepivots! (tensorci2.jl:825-930), :full pivot search; b is 1-based.
+
+        Pi assembly, maxabs, rrLU and the MatrixLUCI factors run in one device call. When no
+        caller can observe the site tensors this sets (sweep2site! with fillsitetensors=true
+        overwrites them all), compute_factors=False skips the factor kernels; indices and errors
+        are identical either way."""
+        self.invalidatesitetensors()
+        Icomb = union_sets(kronecker_right(self.Iset[b - 1], self.localdims[b - 1]), extraIset)
+        Jcomb = union_sets(kronecker_left(self.localdims[b], self.Jset[b]), extraJset)
+        noextra = (extraIset is None or len(extraIset) == 0) and (extraJset is None or len(extraJset) == 0)
+        want = bool(compute_factors and noextra)
+        res = update_pivots_device(f, Icomb, Jcomb, maxbonddim, reltol, abstol, leftorthogonal, want)
+        self.updatemaxsample(res["maxabs"])
+        self.Iset[b] = Icomb[res["rowidx"] - 1]
+        self.Jset[b - 1] = Jcomb[res["colidx"] - 1]
+        if want:
+            self.setsitetensor_(b, res["left"])
+            self.setsitetensor_(b + 1, res["right"])
+        self.updateerrors(b, res["pivoterrors"])
+
+    def setsitetensor(self, f, b, leftorthogonal=True, solve=True):
+        """setsitetensor!(tci, f, b) (tensorci2.jl:599-629) on the device; b is 1-based.
+        solve=False only updates maxsamplevalue from Pi1 (used when the solved tensor is
+        unobservable because a later sweep overwrites it)."""
+        if not leftorthogonal:
+            raise ValueError("leftorthogonal==false is not supported!")
+        p = b - 1
+        Ib, Jb = self.Iset[p], self.Jset[p]
+        last = b == len(self)
+        Inext = None if last else self.Iset[p + 1]
+        if not last and len(Inext) != len(Jb):
+            raise RuntimeError(f"Pivot matrix at bond {b} is not square!")
+        T, mx = sitetensor_device(f, Ib, Jb, Inext, solve)
+        self.updatemaxsample(mx)
+        if solve:
+            self.setsitetensor_(b, T)
+            return self.sitetensors[p]
+        return None
+
+    def fillsitetensors(self, f, solve=True):
+        """fillsitetensors! (globalsearch.jl:202-208)."""
+        for b in range(1, len(self) + 1):
+            self.setsitetensor(f, b, solve=solve)
+
+    def sweep1site(self, f, sweepdirection="forward", reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX,
+                   updatetensors=True):
+        """sweep1site! (tensorci2.jl:659-725)."""
+        self.flushpivoterror()
+        self.invalidatesitetensors()
+        if sweepdirection not in ("forward", "backward"):
+            raise ValueError(f"Unknown sweep direction {sweepdirection}: choose between :forward, :backward.")
+        fwd = sweepdirection == "forward"
+        L = len(self)
+        bonds = range(1, L) if fwd else range(L, 1, -1)
+        for b in bonds:
+            p = b - 1
+            if fwd:
+                Is = kronecker_right(self.Iset[p], self.localdims[p])
+                Js = self.Jset[p]
+            else:
+                Is = self.Iset[p]
+                Js = kronecker_left(self.localdims[p], self.Jset[p])
+            res = update_pivots_device(f, Is, Js, maxbonddim, reltol, abstol, fwd, updatetensors,
+                                       want_left=fwd, want_right=not fwd)
+            self.updatemaxsample(res["maxabs"])
+            self.Iset[p + (1 if fwd else 0)] = Is[res["rowidx"] - 1]
+            self.Jset[p - (0 if fwd else 1)] = Js[res["colidx"] - 1]
+            if updatetensors:
+                self.setsitetensor_(b, res["left"] if fwd else res["right"])
+                if np.any(np.isnan(self.sitetensors[p])):
+                    raise RuntimeError(f"Error: NaN in tensor T[{b}]")
+            self.updateerrors(b - (0 if fwd else 1), res["pivoterrors"])
+        if updatetensors:
+            last = L if fwd else 1
+            T, _ = sitetensor_device(f, self.Iset[last - 1], self.Jset[last - 1], None, True)
+            self.setsitetensor_(last, T)
+
+    def makecanonical(self, f, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX):
+        """makecanonical! (tensorci2.jl:738-749)."""
+        self.sweep1site(f, "forward", reltol=0.0, abstol=0.0, maxbonddim=INT64_MAX, updatetensors=False)
+        self.sweep1site(f, "backward", reltol=reltol, abstol=abstol, maxbonddim=maxbonddim, updatetensors=False)
+        self.sweep1site(f, "forward", reltol=reltol, abstol=abstol, maxbonddim=maxbonddim, updatetensors=True)
+
+    def addglobalpivots1sitesweep(self, f, pivots, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX):
+        """addglobalpivots1sitesweep! (tensorci2.jl:367-377)."""
+        self.addglobalpivots(pivots)
+        self.makecanonical(f, reltol=reltol, abstol=abstol, maxbonddim=maxbonddim)
+
+    def sweep2site(self, f, niter, iter1=1, abstol=1e-8, maxbonddim=INT64_MAX, sweepstrategy="backandforth",
+                   pivotsearch="full", verbosity=0, strictlynested=False, fillsitetensors=True,
+                   lazy_sitetensors=False):
+        """sweep2site! (tensorci2.jl:1195-1258)."""
+        if pivotsearch != "full":
+            raise NotImplementedError("only pivotsearch=:full is implemented (the :rook search is random)")
+        self.invalidatesitetensors()
+        n = len(self)
+        for it in range(iter1, iter1 + niter):
+            extraI = [None] * n
+            extraJ = [None] * n
+            if not strictlynested and len(self.Iset_history) > 0:
+                extraI = self.Iset_history[-1]
+                extraJ = self.Jset_history[-1]
+            self.Iset_history = [[s.copy() for s in self.Iset]]
+            self.Jset_history = [[s.copy() for s in self.Jset]]
+            self.flushpivoterror()
+            # factors set here are always overwritten by fillsitetensors! below
+            cf = not fillsitetensors
+            if forwardsweep(sweepstrategy, it):
+                for b in range(1, n):
+                    self.updatepivots(b, f, True, abstol=abstol, maxbonddim=maxbonddim,
+                                      extraIset=extraI[b], extraJset=extraJ[b - 1], compute_factors=cf)
+            else:
+                for b in range(n - 1, 0, -1):
+                    self.updatepivots(b, f, False, abstol=abstol, maxbonddim=maxbonddim,
+                                      extraIset=extraI[b], extraJset=extraJ[b - 1], compute_factors=cf)
+        if fillsitetensors:
+            self.fillsitetensors(f, solve=not lazy_sitetensors)
+
+    def optimize(self, f, tolerance=None, pivottolerance=None, maxbonddim=INT64_MAX, maxiter=20,
+                 sweepstrategy="backandforth", pivotsearch="full", verbosity=0, loginterval=10,
+                 normalizeerror=True, ncheckhistory=3, globalpivotfinder=None, maxnglobalpivot=5,
+                 nsearchglobalpivot=5, tolmarginglobalsearch=10.0, strictlynested=False,
+                 checkbatchevaluatable=False, checkconvglobalpivot=True, rng=None):
+        """optimize! (tensorci2.jl:1018-1172). Returns (ranks, errors ./ errornormalization)."""
+        errors, ranks, nglobalpivots = [], [], []
+        if checkbatchevaluatable and not isinstance(f, GPUBatchEvaluator):
+            raise RuntimeError("Function `f` is not batch evaluatable")
+        if 0 < nsearchglobalpivot < maxnglobalpivot:
+            raise RuntimeError("nsearchglobalpivot < maxnglobalpivot!")
+        if pivottolerance is not None:
+            if tolerance is not None and tolerance != pivottolerance:
+                raise ValueError("Got different values for pivottolerance and tolerance in optimize!(TCI2). "
+                                 "For TCI2, both of these options have the same meaning. Please assign only "
+                                 "`tolerance`.")
+            tol = pivottolerance
+        elif tolerance is not None:
+            tol = tolerance
+        else:
+            tol = 1e-8
+        if maxbonddim >= INT64_MAX and tol <= 0:
+            raise ValueError("Specify either tolerance > 0 or some maxbonddim; otherwise, the convergence "
+                             "criterion is not reachable!")
+        if globalpivotfinder is None:
+            from .globalpivotfinder import DefaultGlobalPivotFinder
+            finder = DefaultGlobalPivotFinder(nsearch=nsearchglobalpivot, maxnglobalpivot=maxnglobalpivot,
+                                              tolmarginglobalsearch=tolmarginglobalsearch)
+        else:
+            finder = globalpivotfinder
+        # The solved site tensors of fillsitetensors! are read only by a global pivot search;
+        # with no search they are unobservable (sweep1site! below rebuilds all of them).
+        searches = getattr(finder, "nsearch", 1) > 0
+        for it in range(1, maxiter + 1):
+            errornormalization = self.maxsamplevalue if normalizeerror else 1.0
+            abstol = tol * errornormalization
+            self.sweep2site(f, 2, iter1=1, abstol=abstol, maxbonddim=maxbonddim, pivotsearch=pivotsearch,
+                            strictlynested=strictlynested, verbosity=verbosity, sweepstrategy=sweepstrategy,
+                            fillsitetensors=True, lazy_sitetensors=not searches)
+            errors.append(self.pivoterror())
+            globalpivots = finder(self, f, abstol, verbosity=verbosity, rng=rng) if searches else []
+            self.addglobalpivots(globalpivots)
+            nglobalpivots.append(len(globalpivots))
+            ranks.append(self.rank())
+            if verbosity > 0 and it % loginterval == 0:
+                print(f"iteration = {it}, rank = {ranks[-1]}, error= {errors[-1]}, "
+                      f"maxsamplevalue= {self.maxsamplevalue}, nglobalpivot={len(globalpivots)}")
+            if convergencecriterion(ranks, errors, nglobalpivots, abstol, maxbonddim, ncheckhistory,
+                                    checkconvglobalpivot):
+                break
+        errornormalization = self.maxsamplevalue if normalizeerror else 1.0
+        abstol = tol * errornormalization
+        self.sweep1site(f, abstol=abstol, maxbonddim=maxbonddim)
+        self._sanitycheck()
+        return ranks, [e / errornormalization for e in errors]
+
+    def _sanitycheck(self):
+        """_sanitycheck (globalsearch.jl:226-233)."""
+        for b in range(1, len(self)):
+            if len(self.Iset[b]) != len(self.Jset[b - 1]):
+                raise RuntimeError(f"Pivot matrix at bond {b} is not square!")
+        return True
+
+    # -- tensor-train view (abstracttensortrain.jl:328-342, 428-441)
+    def evaluate(self, idx):
+        v = np.ones((1, 1))
+        for p, i in enumerate(idx):
+            v = v @ self.sitetensors[p][:, int(i) - 1, :]
+        return float(v[0, 0])
+
+    def evaluate_many(self, X):
+        X = np.asarray(X, np.int64)
+        v = np.ones((len(X), 1))
+        for p in range(len(self)):
+            T = self.sitetensors[p]
+            v = np.einsum("na,anb->nb", v, T[:, X[:, p] - 1, :])
+        return v[:, 0]
+
+    def sum(self):
+        v = np.ones((1, 1))
+        for T in self.sitetensors:
+            v = v @ T.sum(axis=1)
+        return float(v[0, 0])
+
+
+def reconstractglobalpivotsfromijset(localdims, Isets, Jsets):
+    """reconstractglobalpivotsfromijset (tensorci2.jl:303-320)."""
+    seen = set()
+    out = []
+    for i in range(len(Isets)):
+        for I in Isets[i]:
+            for J in Jsets[i]:
+                for j in range(1, localdims[i] + 1):
+                    e = tuple(int(x) for x in I) + (j,) + tuple(int(x) for x in J)
+                    if e not in seen:
+                        seen.add(e)
+                        out.append(e)
+    return np.asarray(out, np.int32)
+
+
+# --------------------------------------------------------------- device calls
+def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                         want_left=True, want_right=True):
+    """One fused device call: Pi = f(rows x cols), maxabs, rrLU, pivots, MatrixLUCI factors."""
+    ctx = f.ctx
+    rows = np.ascontiguousarray(rows, np.int32)
+    cols = np.ascontiguousarray(cols, np.int32)
+    m, nl = rows.shape
+    n, nr = cols.shape
+    mr = int(max(min(int(maxrank), m, n), 0))
+    rowidx = np.zeros(max(mr, 1), np.int64)
+    colidx = np.zeros(max(mr, 1), np.int64)
+    pe = np.zeros(mr + 1)
+    npv = C.c_int64()
+    mx = C.c_double()
+    left = np.zeros(max(m * mr, 1)) if (want_factors and want_left) else None
+    right = np.zeros(max(mr * n, 1)) if (want_factors and want_right) else None
+    ctx.check(ctx.lib.tci_update_pivots_h(ctx.h, f.h, _lib.ptr(rows), m, nl, _lib.ptr(cols), n, nr,
+                                          int(min(maxrank, INT64_MAX)), float(reltol), float(abstol),
+                                          int(bool(leftorth)), int(bool(want_factors)), _lib.ptr(rowidx),
+                                          _lib.ptr(colidx), _lib.ptr(pe), C.byref(npv), C.byref(mx),
+                                          _lib.ptr(left), _lib.ptr(right)))
+    k = npv.value
+    res = {"rowidx": rowidx[:k].copy(), "colidx": colidx[:k].copy(), "pivoterrors": pe[: k + 1].copy(),
+           "maxabs": mx.value, "npivot": k}
+    if left is not None:
+        res["left"] = left[: m * k].reshape((m, k), order="F")
+    if right is not None:
+        res["right"] = right[: k * n].reshape((k, n), order="F")
+    return res
+
+
+def sitetensor_device(f, Ib, Jb, Inext, solve=True):
+    """T = Pi1 * P^-1 (tensorci2.jl:599-629) on the device; returns (T or None, max|Pi1|)."""
+    ctx = f.ctx
+    Ib = np.ascontiguousarray(Ib, np.int32)
+    Jb = np.ascontiguousarray(Jb, np.int32)
+    nI, wI = Ib.shape
+    nJ, wJ = Jb.shape
+    d = f.localdims[wI]
+    R = nI * d
+    mx = C.c_double()
+    if Inext is None:
+        T = np.zeros(max(R * nJ, 1)) if solve else None
+        nxt, nn = None, 0
+    else:
+        Inext = np.ascontiguousarray(Inext, np.int32)
+        nn = len(Inext)
+        T = np.zeros(max(R * nn, 1)) if solve else None
+        nxt = Inext
+    if not solve:
+        # only max|Pi1| is observable: evaluate Pi1 on the device, no solve, no copy back
+        I = Ib
+        out_mx = _batch_maxabs(f, I, Jb, 1)
+        return None, out_mx
+    ctx.check(ctx.lib.tci_sitetensor_h(ctx.h, f.h, _lib.ptr(Ib), nI, wI, _lib.ptr(Jb), nJ, wJ, _lib.ptr(nxt),
+                                       nn, _lib.ptr(T), C.byref(mx)))
+    cols = nJ if Inext is None else nn
+    return T[: R * cols].reshape((R, cols), order="F"), mx.value
+
+
+def _batch_maxabs(f, I, J, M):
+    ctx = f.ctx
+    m, nl = I.shape
+    n, nr = J.shape
+    D = f.localdims[nl] if M == 1 else 1
+    mx = C.c_double()
+    scratch = _scratch(ctx, m * D * n)
+    ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, _lib.ptr(I), m, nl, _lib.ptr(J), n, nr, M, scratch,
+                                      max(m * D, 1), C.byref(mx)))
+    return mx.value
+
+
+_scratch_cache = {}
+
+
+def _scratch(ctx, nelem):
+    key = id(ctx)
+    cur = _scratch_cache.get(key)
+    if cur is None or cur[1] < nelem:
+        if cur is not None:
+            ctx.lib.tci_free_d(ctx.h, cur[0])
+        p = C.c_void_p()
+        size = max(int(nelem * 1.5), 1024)
+        ctx.check(ctx.lib.tci_malloc_d(ctx.h, C.byref(p), size * 8))
+        _scratch_cache[key] = (p, size)
+        cur = _scratch_cache[key]
+    return cur[0]
+
+
+def crossinterpolate2(f, localdims=None, initialpivots=None, **kwargs):
+    """crossinterpolate2(Float64, f, localdims, initialpivots; kwargs...) (tensorci2.jl:1313-1323).
+    Returns (tci, ranks, errors)."""
+    if localdims is None:
+        localdims = f.localdims
+    tci = TensorCI2.from_function(f, localdims, initialpivots)
+    ranks, errors = tci.optimize(f, **kwargs)
+    return tci, ranks, errors

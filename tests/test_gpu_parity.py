@@ -1,0 +1,281 @@
+"""GPU parity: the HIP path (through the C-ABI, via tci_amd) against the CPU oracle.
+
+Bar: bit-exact for rrLU (permutations, L, U, npivot, error) and for the integer-valued integrand
+kinds; 1e-12 relative (factors, transcendental integrands) and 1e-10 relative for TCI2 errors, as
+stated per test.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+T = pytest.importorskip("tci_amd")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return T.context(0)
+
+
+def assert_lu_bitwise(lu, ref):
+    assert lu.npivot == ref.npivot
+    assert np.array_equal(lu.rowpermutation - 1, ref.rowpermutation)
+    assert np.array_equal(lu.colpermutation - 1, ref.colpermutation)
+    assert np.array_equal(lu.L, ref.L)
+    assert np.array_equal(lu.U, ref.U)
+    assert (lu.error == ref.error) or (np.isnan(lu.error) and np.isnan(ref.error))
+
+
+KAT_MATS = ["rrlu_exact_4x4", "rrlu_truncated_rank1", "rrlu_maxrank4_8x6", "rrlu_identity_pivoterrors",
+            "rrlu_limits_5x5", "rrlu_tiny_values"]
+
+
+@pytest.mark.parametrize("name", KAT_MATS)
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_rrlu_kats_bitwise(kats, ctx, name, leftorth):
+    k = kats[name]
+    A = np.array(k["A"], float) * k.get("scale", 1.0)
+    kw = dict(k.get("kwargs", {}))
+    cases = [c.get("kwargs", {}) for c in k["cases"]] if "cases" in k else [kw]
+    for kw in cases:
+        lu = T.rrlu(A, leftorthogonal=leftorth, ctx=ctx, **kw)
+        ref = O.OracleLU(A, leftorthogonal=leftorth, **kw)
+        assert_lu_bitwise(lu, ref)
+
+
+def test_rrlu_exact_rank3(kats, ctx):
+    k = kats["rrlu_exact_rank3"]
+    A = np.array(k["p"]) @ np.array(k["q"])
+    lu = T.rrlu(A, ctx=ctx)
+    assert lu.npivot == 3
+    assert_lu_bitwise(lu, O.OracleLU(A))
+
+
+@pytest.mark.parametrize("m,n,maxrank", [(1, 1, 5), (7, 3, 9), (513, 389, 120), (300, 700, 300),
+                                         (1024, 1024, 64)])
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_rrlu_random_bitwise(ctx, m, n, maxrank, leftorth):
+    A = O.fill_uniform(m * n, seed=m * 7 + n).reshape((m, n), order="F")
+    lu = T.rrlu(A, maxrank=maxrank, leftorthogonal=leftorth, ctx=ctx)
+    assert_lu_bitwise(lu, O.OracleLU(A, maxrank=maxrank, leftorthogonal=leftorth))
+
+
+def test_rrlu_ties_lorentzian_bitwise(ctx):
+    # Lorentzian Pi has many exactly equal entries: exercises the tie order everywhere
+    f = O.feval
+    I = np.array(list(itertools.product(range(1, 8), repeat=2)), np.int32)
+    J = np.array(list(itertools.product(range(1, 8), repeat=2)), np.int32)
+    Pi, _ = O.batcheval(1, [1.0], [7] * 4, I, J, 0)
+    Pi = Pi[:, 0, :]
+    for reltol in (1e-14, 1e-6):
+        lu = T.rrlu(Pi, reltol=reltol, ctx=ctx)
+        assert_lu_bitwise(lu, O.OracleLU(Pi, reltol=reltol))
+
+
+def test_rrlu_stop_tests_bitwise(ctx):
+    A = O.fill_uniform(200 * 160, seed=3).reshape((200, 160), order="F")
+    A = A[:, :40] @ A[:40, :] + 1e-9 * A  # numerically rank ~40
+    for kw in ({"reltol": 1e-6}, {"abstol": 1e-5}, {"maxrank": 17}, {"reltol": 0.0, "abstol": 0.0}):
+        assert_lu_bitwise(T.rrlu(A, ctx=ctx, **kw), O.OracleLU(A, **kw))
+
+
+def test_rrlu_nan_raises(ctx):
+    # NaN that reaches L (matrixlu.jl:376-378) raises; one that stays outside L/U does not
+    A = np.random.default_rng(4).random((5, 5))
+    A[3, 0] = np.nan
+    with pytest.raises(O.OracleError, match="lu.L contains NaNs"):
+        O.OracleLU(A)
+    with pytest.raises(T.TCIError, match="lu.L contains NaNs"):
+        T.rrlu(A, ctx=ctx)
+    B = np.ones((5, 5))
+    B[2, 3] = np.nan
+    B[0, 0] = 2.0
+    assert_lu_bitwise(T.rrlu(B, ctx=ctx), O.OracleLU(B))
+
+
+def test_rrlu_empty(ctx):
+    lu = T.rrlu(np.zeros((0, 4)), ctx=ctx)
+    assert lu.npivot == 0 and lu.error == 0.0
+
+
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_luci_factors(ctx, kats, leftorth):
+    for A in (np.array(kats["luci_maxrank4_8x6"]["A"]),
+              O.fill_uniform(300 * 200, 11).reshape((300, 200), order="F")):
+        for maxrank in (4, 50, 1000):
+            luci = T.MatrixLUCI(A, maxrank=maxrank, leftorthogonal=leftorth, ctx=ctx)
+            ref = O.OracleLU(A, maxrank=maxrank, leftorthogonal=leftorth)
+            assert np.array_equal(luci.rowindices() - 1, ref.rowindices())
+            assert np.array_equal(luci.colindices() - 1, ref.colindices())
+            assert np.array_equal(luci.pivoterrors(), ref.pivoterrors)
+            np.testing.assert_allclose(luci.left(), ref.left, rtol=1e-12, atol=1e-12 * np.abs(ref.left).max())
+            np.testing.assert_allclose(luci.right(), ref.right, rtol=1e-12, atol=1e-12 * np.abs(ref.right).max())
+
+
+KINDS = [
+    (O_SUM := 0, [], [3, 4, 2, 5, 3]),
+    (1, [1.0], [10] * 6),
+    (1, [0.5], [7] * 5),
+    (2, None, [3, 4, 2, 5]),
+    (3, [1.0 / 64, 8.5], [16] * 6),
+    (5, [10.0, 2 * np.pi * 100, 1.1], [2] * 20),
+    (6, [1.0, 1.0, 1e-4, 2.0], [2] * 12),
+]
+
+
+@pytest.mark.parametrize("kind,params,ld", KINDS)
+@pytest.mark.parametrize("M", [0, 1])
+def test_batcheval_vs_oracle(ctx, kind, params, ld, M):
+    rng = np.random.default_rng(kind * 10 + M)
+    if kind == 2:
+        params = rng.random(int(np.prod(ld))).tolist()
+    L = len(ld)
+    nl = L // 2 - (1 if M else 0)
+    nr = L - nl - M
+    I = np.stack([rng.integers(1, ld[t] + 1, 37) for t in range(nl)], axis=1).astype(np.int32) if nl else np.zeros((37, 0), np.int32)
+    J = np.stack([rng.integers(1, ld[nl + M + t] + 1, 29) for t in range(nr)], axis=1).astype(np.int32)
+    ref, rmx = O.batcheval(kind, params, ld, I, J, M)
+    f = T.GPUBatchEvaluator(kind, params, ld, ctx=ctx)
+    got = f.batch([list(r) for r in I] if nl else [[] for _ in range(37)], [list(r) for r in J], M)
+    ref = ref.reshape(got.shape, order="F")
+    if kind in (0, 1, 2):
+        assert np.array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=1e-14, atol=1e-300)
+    _, gmx = f.pi(I, J, M)
+    assert gmx == pytest.approx(rmx, rel=1e-14)
+
+
+def test_batcheval_tt_and_gaussmix(ctx):
+    rng = np.random.default_rng(5)
+    ld = [2, 3, 3, 2]
+    bd = [1, 2, 3, 2, 1]
+    cores = [rng.random((bd[p], ld[p], bd[p + 1])) for p in range(4)]
+    f = T.tensortrain_function(cores, ctx=ctx)
+    params = np.concatenate([np.array(bd, float)] + [c.ravel(order="F") for c in cores])
+    X = np.array(list(itertools.product(*[range(1, d + 1) for d in ld])), np.int32)
+    got = f.points(X)
+    ref = np.array([O.feval(7, params, ld, x) for x in X])
+    np.testing.assert_allclose(got, ref, rtol=1e-13)
+    cen = rng.random((4, 5)) * 6
+    g = T.gaussmix([6] * 5, 0.1, cen, [1.0, -0.5, 0.25, 2.0], ctx=ctx)
+    p2 = np.concatenate([[4, 0.1], cen.ravel(), [1.0, -0.5, 0.25, 2.0]])
+    X = rng.integers(1, 7, (50, 5)).astype(np.int32)
+    np.testing.assert_allclose(g.points(X), [O.feval(4, p2, [6] * 5, x) for x in X], rtol=1e-13)
+
+
+def test_sitetensor_solve(ctx):
+    rng = np.random.default_rng(9)
+    M = rng.random((12, 12))
+    f = T.table(M, ctx=ctx)
+    tci, ranks, errors = T.crossinterpolate2(f, maxbonddim=6, nsearchglobalpivot=0)
+    Ib, Jb, Inext = tci.Iset[0], tci.Jset[0], tci.Iset[1]
+    tens = tci.setsitetensor(f, 1)
+    P = M[np.ix_(Inext[:, 0] - 1, Jb[:, 0] - 1)]
+    Pi1 = M[:, Jb[:, 0] - 1]
+    ref = O.sitetensor_solve(P, Pi1)
+    np.testing.assert_allclose(tens.reshape(ref.shape, order="F"), ref, rtol=1e-10, atol=1e-12)
+
+
+# ------------------------------------------------------------------ TCI2
+def _compare_tci(tci, ranks, errors, rt, rranks, rerrors, rtol=1e-10):
+    assert ranks == rranks
+    np.testing.assert_allclose(errors, rerrors, rtol=rtol, atol=0)
+    for p in range(len(tci.localdims)):
+        assert np.array_equal(tci.Iset[p], rt.Iset(p)), p
+        assert np.array_equal(tci.Jset[p], rt.Jset(p)), p
+    np.testing.assert_allclose(tci.pivoterrors, rt.pivoterrors, rtol=rtol, atol=0)
+    assert tci.maxsamplevalue == rt.maxsamplevalue
+    for p in range(len(tci.localdims)):
+        ref = rt.sitetensor(p)
+        np.testing.assert_allclose(tci.sitetensors[p], ref, rtol=1e-9, atol=1e-12 * max(1.0, np.abs(ref).max()))
+
+
+def test_tci2_pivoterrors_kat(kats, ctx):
+    k = kats["tci2_pivoterrors"]
+    M = np.diag(k["diags"])
+    f = T.table(M, ctx=ctx)
+    tci, ranks, errors = T.crossinterpolate2(f, initialpivots=k["initialpivots"], tolerance=k["tolerance"],
+                                             nsearchglobalpivot=0)
+    assert list(tci.pivoterrors) == k["expect"]["pivoterrors"]
+
+
+def test_tci2_lorentz5d_kat(kats, ctx):
+    k = kats["tci2_lorentz5d"]
+    n, d = k["n"], k["d"]
+    f = T.lorentz([d] * n, ctx=ctx)
+    tci = T.TensorCI2.from_function(f, [d] * n)
+    assert tci.linkdims() == [1] * (n - 1)
+    for b in range(1, n):
+        tci.updatepivots(b, f, True, reltol=1e-8, maxbonddim=2)
+    assert tci.linkdims() == k["updatepivots_maxbonddim2"]["expect_linkdims"]
+    tci.addglobalpivots1sitesweep(f, [k["globalpivot"]], reltol=1e-12)
+    assert tci.linkdims() == k["after_global_1site"]["expect_linkdims"]
+    # same sequence on the oracle: identical sets and tensors
+    rt = O.OracleTCI2(1, [1.0], [d] * n)
+    for b in range(n - 1):
+        rt.updatepivots(b, True, 1e-8, 0.0, 2)
+    rt.addglobalpivots([k["globalpivot"]])
+    rt.makecanonical(reltol=1e-12)
+    for p in range(n):
+        assert np.array_equal(tci.Iset[p], rt.Iset(p)) and np.array_equal(tci.Jset[p], rt.Jset(p))
+        np.testing.assert_allclose(tci.sitetensors[p], rt.sitetensor(p), rtol=1e-9, atol=1e-14)
+    tci3, ranks, errors = T.crossinterpolate2(f, tolerance=1e-12, maxiter=200, nsearchglobalpivot=0)
+    assert tci3.pivoterror() <= 2e-12
+    for v in itertools.product(range(1, 4), repeat=n):
+        assert tci3.evaluate(v) == pytest.approx(1.0 / (sum(x * x for x in v) + 1), rel=1.5e-8)
+
+
+@pytest.mark.parametrize("strategy", ["backandforth", "forward"])
+@pytest.mark.parametrize("strict", [False, True])
+def test_tci2_lorentz_vs_oracle(ctx, strategy, strict):
+    ld = [10] * 6
+    f = T.lorentz(ld, ctx=ctx)
+    kw = dict(tolerance=1e-10, maxiter=10, sweepstrategy=strategy, strictlynested=strict)
+    tci, ranks, errors = T.crossinterpolate2(f, nsearchglobalpivot=0, **kw)
+    rt, rranks, rerrors = O.crossinterpolate2(1, [1.0], ld, **kw)
+    _compare_tci(tci, ranks, errors, rt, rranks, rerrors)
+
+
+def test_tci2_config1_readme_lorentzian(ctx):
+    """BASELINE config 1: f(v) = 1/(1+v'v), localdims = fill(10, 8), tol = 1e-8."""
+    ld = [10] * 8
+    f = T.lorentz(ld, ctx=ctx)
+    tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)
+    rt, rranks, rerrors = O.crossinterpolate2(1, [1.0], ld, tolerance=1e-8)
+    _compare_tci(tci, ranks, errors, rt, rranks, rerrors)
+
+
+def test_tci2_quantics_and_gauss_vs_oracle(ctx):
+    for kind, params, ld, kw in (
+        (5, [10.0, 2 * np.pi * 100, 1.1], [2] * 12, dict(tolerance=1e-10, maxbonddim=40, maxiter=8)),
+        (6, [1.0, 1.0, 1e-4, 2.0], [2] * 10, dict(tolerance=1e-12, maxiter=6)),
+        (3, [1.0 / 64, 8.5], [16] * 6, dict(tolerance=1e-10, maxbonddim=64, maxiter=6)),
+    ):
+        f = T.GPUBatchEvaluator(kind, params, ld, ctx=ctx)
+        tci, ranks, errors = T.crossinterpolate2(f, nsearchglobalpivot=0, **kw)
+        rt, rranks, rerrors = O.crossinterpolate2(kind, params, ld, **kw)
+        _compare_tci(tci, ranks, errors, rt, rranks, rerrors)
+
+
+def test_tci2_tt_function_reconstruction(ctx):
+    rng = np.random.default_rng(7)
+    ld = [2, 3, 3, 2]
+    bd = [1, 2, 3, 2, 1]
+    cores = [rng.random((bd[p], ld[p], bd[p + 1])) for p in range(4)]
+    f = T.tensortrain_function(cores, ctx=ctx)
+    tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-10, maxbonddim=10, nsearchglobalpivot=0)
+    X = np.array(list(itertools.product(*[range(1, d + 1) for d in ld])))
+    np.testing.assert_allclose(tci.evaluate_many(X), f.points(X), rtol=1e-8)
+
+
+def test_tci2_default_global_search_runs(ctx):
+    """Default nsearchglobalpivot=5 (random search; statistical parity only)."""
+    f = T.quantics_osc(10, ctx=ctx)
+    tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-12, maxbonddim=100, maxiter=30,
+                                             rng=np.random.default_rng(1234))
+    assert errors[-1] < 1e-10
