@@ -29,11 +29,25 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def update_bytes(m, n, r):
-    # fused update+argmax launches run for pivots k = 0..r-2 over the (m-k-1) x (n-k-1) trailing
-    # block: 8 B read + 8 B written per element (SURVEY 8(d) per-unit figure)
-    k = np.arange(0, r - 1, dtype=np.float64)
-    return float(np.sum(16.0 * (m - k - 1) * (n - k - 1)))
+def pass_bytes(m, n, r, nb):
+    """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-2, each over the
+    (m-k-1) x (n-k-1) trailing block: a read-only pass reads 8 B/element, every nb-th pass
+    (pending count reaches nb) also writes 8 B/element back. Returns (read_only, write_back)
+    as (bytes, launches)."""
+    ro_b = wb_b = 0.0
+    ro_n = wb_n = 0
+    pend = 0
+    for k in range(r - 1):
+        pend += 1
+        elems = float(m - k - 1) * float(n - k - 1)
+        if pend >= nb:
+            wb_b += 16.0 * elems
+            wb_n += 1
+            pend = 0
+        else:
+            ro_b += 8.0 * elems
+            ro_n += 1
+    return (ro_b, ro_n), (wb_b, wb_n)
 
 
 def main():
@@ -47,6 +61,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-pivots", type=int, default=256)
+    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "8")),
+                    help="deferred-update depth of the rrLU (results are identical for every nb)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,6 +76,7 @@ def main():
     import tci_amd as T
 
     ctx = T.context(local_rank)
+    ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, args.nb))
     m, n, r = args.m, args.n, args.r
     A = T.DeviceMatrix(m, n, ctx=ctx)
     A.fill_uniform(seed=rank)
@@ -84,7 +101,8 @@ def main():
         np_, err, _, _, _ = step()
     barrier()
     dt = time.perf_counter() - t0
-    upd_ms, upd_launches = ctx.kernel_stats(0)
+    wb_ms, wb_launches = ctx.kernel_stats(0)
+    ro_ms, ro_launches = ctx.kernel_stats(2)
     ctx.set_timing(False)
     assert np_ == min(r, m, n), np_
     if dist is not None:
@@ -96,9 +114,26 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     flops = rrlu_flops(m, n, r)
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
-    avg_launch_ms = upd_ms / max(upd_launches, 1)
-    bytes_per_launch = update_bytes(m, n, r) / max(r - 1, 1)
+    nb = args.nb
+    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb)
+    # dominant kernel: the read-only pass when nb > 1, else the write-back pass
+    if ro_n > 0 and ro_ms >= wb_ms:
+        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,false> (read-only: pending updates "
+                                                       "applied on the fly + abs2 argmax)", ro_ms,
+                                                       ro_launches, ro_b, ro_n)
+    else:
+        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,true> (pending updates applied and "
+                                                       "written back + abs2 argmax)", wb_ms, wb_launches,
+                                                       wb_b, wb_n)
+    avg_launch_ms = dom_ms / max(dom_launches, 1)
+    bytes_per_launch = dom_bytes / max(dom_n, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    other = {"write_back_pass": {"launches": wb_launches, "avg_ms": round(wb_ms / max(wb_launches, 1), 5),
+                                 "GBps": round(wb_b / max(wb_n, 1) / (wb_ms / max(wb_launches, 1) * 1e-3) / 1e9, 1)
+                                 if wb_launches else None},
+             "read_only_pass": {"launches": ro_launches, "avg_ms": round(ro_ms / max(ro_launches, 1), 5),
+                                "GBps": round(ro_b / max(ro_n, 1) / (ro_ms / max(ro_launches, 1) * 1e-3) / 1e9, 1)
+                                if ro_launches else None}}
     out = {
         "metric": "rrLU GFLOP/s at (m,n,r)=(8192,8192,256)" if (m, n, r) == (8192, 8192, 256)
         else f"rrLU GFLOP/s at (m,n,r)=({m},{n},{r})",
@@ -117,10 +152,17 @@ def main():
                    "m": m, "n": n, "r": r, "parallelism": f"replicas{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_argmax_update<true> (fused Schur rank-1 update + abs2 argmax)",
-                     "avg_launch_ms": round(avg_launch_ms, 5), "launches": upd_launches,
-                     "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
+                     "deferred_depth_nb": nb},
     }
+    # roofline calibration on the same buffers: 16-B stream read and stream copy
+    import ctypes as C
+    ms_r, ms_c = C.c_double(), C.c_double()
+    nel = A.ld * n
+    ctx.check(ctx.lib.tci_diag_stream_d(ctx.h, A.ptr, W.ptr, nel, 5, 0, C.byref(ms_r), C.byref(ms_c)))
+    out["roofline"]["measured_stream_read_GBps"] = round(8.0 * nel / (ms_r.value * 1e-3) / 1e9, 1)
+    out["roofline"]["measured_stream_copy_GBps"] = round(16.0 * nel / (ms_c.value * 1e-3) / 1e9, 1)
     A.free()
     W.free()
 

@@ -56,10 +56,16 @@ const char* tci_last_error(const tci_ctx* ctx);
  * hipEvent timing around _d calls. */
 void* tci_ctx_stream(tci_ctx* ctx);
 int tci_ctx_synchronize(tci_ctx* ctx);
-/* Average device time (ms) of the last call's dominant kernel family, measured with hipEvents
- * on the context stream: family 0 = rrLU fused Schur update + argmax, 1 = batch evaluation. */
+/* Device time (ms, summed) and launch count of a kernel family since tci_set_timing(ctx, 1),
+ * measured with hipEvents on the context stream: family 0 = rrLU pass that writes the Schur
+ * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
+ * 1 = batch evaluation. */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
 int tci_set_timing(tci_ctx* ctx, int enabled);
+/* Deferred-update depth of the rrLU (1..16; default 8, env TCI_RRLU_NB): up to nb rank-1
+ * updates are applied on the fly by read-only passes and written back every nb-th pivot.
+ * Results are bitwise identical for every nb. */
+int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
 
 /* ------------------------------------------------------------ integrands */
 /* Uploads an integrand's parameters to the device once; localdims has L entries. */
@@ -135,6 +141,12 @@ int tci_sitetensor_h(tci_ctx* ctx, const tci_func* f, const int32_t* Ib, int64_t
  * times 2^-53 -- the same stream as the oracle's orc_fill_uniform. */
 int tci_fill_uniform_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
                        uint64_t seed);
+
+/* Diagnostic roofline calibration: average device time (ms) of a 16-B-per-lane stream read of
+ * n doubles at d_a, and (if d_b) of a stream copy d_a -> d_b, over `reps` launches of `grid`
+ * 256-thread workgroups (grid <= 0: 2048). */
+int tci_diag_stream_d(tci_ctx* ctx, const double* d_a, double* d_b, int64_t n, int reps, int grid,
+                      double* ms_read, double* ms_copy);
 
 /* ------------------------------------------------------------ device mem */
 int tci_malloc_d(tci_ctx* ctx, void** p, int64_t bytes);

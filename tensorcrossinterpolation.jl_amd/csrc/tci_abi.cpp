@@ -3,6 +3,7 @@
 // tci_device.hip; nothing here falls back to the CPU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -32,8 +33,12 @@ struct tci_ctx {
     int64_t* colperm = nullptr;
     size_t capPerm = 0;
     size_t capColperm = 0;
+    double* xbuf = nullptr;  // pending rank-1 update vectors (tci_rrlu.hip)
+    size_t capX = 0;
     double* ybuf = nullptr;
     size_t capY = 0;
+    int flush_every = 8;  // deferred-update depth nb (1 = write back every pivot)
+    int pass_grid = 2048;  // workgroups of an rrLU pass (env TCI_PASS_GRID)
     int* flag = nullptr;
     int* hflag = nullptr;  // pinned
     unsigned long long* maxbits = nullptr;
@@ -52,13 +57,31 @@ struct tci_ctx {
     size_t capDiag = 0;
     int* dPiv = nullptr;
     size_t capPiv = 0;
-    // kernel timing (family 0: fused update+argmax, 1: batch evaluation)
+    // rrLU results (tci_rrlu.hip): position maps, pivot values, physical-order L / U, and the
+    // position-order L / U extracted from them
+    int32_t* rowpos = nullptr;
+    size_t capRowpos = 0;
+    int32_t* colpos = nullptr;
+    size_t capColpos = 0;
+    double* pivv = nullptr;
+    size_t capPivv = 0;
+    double* Lp = nullptr;
+    size_t capLp = 0;
+    double* Up = nullptr;
+    size_t capUp = 0;
+    int64_t ldUp = 1;
+    double* dL = nullptr;
+    size_t capL = 0;
+    double* dU = nullptr;
+    size_t capU = 0;
+    // kernel timing (family 0: rrLU pass with write-back, 1: batch evaluation,
+    //                2: rrLU read-only pass)
     bool timing = false;
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
     std::vector<std::pair<int, size_t>> evpairs;  // (family, index of start event)
-    double fam_ms[2] = {0, 0};
-    int64_t fam_n[2] = {0, 0};
+    double fam_ms[3] = {0, 0, 0};
+    int64_t fam_n[3] = {0, 0, 0};
 };
 
 struct tci_func {
@@ -139,8 +162,10 @@ void ev_end(tci_ctx* c) {
 void ev_reset(tci_ctx* c) {
     c->evused = 0;
     c->evpairs.clear();
-    c->fam_ms[0] = c->fam_ms[1] = 0;
-    c->fam_n[0] = c->fam_n[1] = 0;
+    for (int f = 0; f < 3; ++f) {
+        c->fam_ms[f] = 0;
+        c->fam_n[f] = 0;
+    }
 }
 void ev_collect(tci_ctx* c) {
     if (!c->timing) return;
@@ -155,22 +180,34 @@ void ev_collect(tci_ctx* c) {
     c->evused = 0;
 }
 
-constexpr int kCB = 16;       // columns per update tile
 constexpr int kMaxGrid = 2048;  // 8 workgroups per CU x 256 CUs
 
-// The per-pivot loop of _optimizerrlu! (matrixlu.jl:346-369) on a device matrix. Leaves
-// rowperm/colperm/state on the device; returns np and lu.error.
+// columns per rrLU tile (multiple of the kernel's 8-column batch): wide tiles when the matrix
+// is large, narrower ones so that small matrices still spread over every CU
+int pick_cb(int64_t m, int64_t n) {
+    const int64_t tiles_r = (m + tci::kRowsPerTile - 1) / tci::kRowsPerTile;
+    for (int cb = tci::kMaxCB; cb > 8; cb /= 2)
+        if (tiles_r * ((n + cb - 1) / cb) >= kMaxGrid) return cb;
+    return 8;
+}
+
+// The per-pivot loop of _optimizerrlu! (matrixlu.jl:346-369) on a device matrix (clobbered:
+// its trailing values are left stale). Leaves on the device: rowphys/colphys (= rowpermutation /
+// colpermutation, 0-based) in c->rowperm / c->colperm, pivot values in c->pivv, L columns in
+// physical row order in c->Lp (ld m) and U rows in physical column order in c->Up (ld mr).
 int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
                 double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out) {
     int st;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
-    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
+    if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
     const int mi = (int)m, ni = (int)n;
-    tci::launch_init_state(c->stream, c->st, c->rowperm, mi, c->colperm, ni);
+    tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, ni);
     int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
     if (mr < 0) mr = 0;
+    c->ldUp = std::max<int64_t>(mr, 1);
     if (m == 0 || n == 0 || mr == 0) {
         HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -178,26 +215,54 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         *err_out = (0 >= std::min(m, n)) ? 0.0 : c->hst->error;
         return TCI_OK;
     }
-    int ncand = tci::argmax_grid(mi, ni, -1, kCB, kMaxGrid);
-    tci::launch_argmax_update(c->stream, false, dA, lda, mi, ni, -1, c->ybuf, c->st, c->cand, ncand,
-                              kCB);
-    int64_t k = 0, chunk = 2;
+    if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
+    if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
+    if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * n)))) return st;
+    // pending rank-1 updates: X[i * ldx + s] (physical row i, slot s), Y[j * ldy + s]; one extra
+    // row so the 16-B loads of a tile's last odd row stay in bounds
+    const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
+    const int64_t ldx = tci::kMaxPend, ldy = tci::kMaxPend;
+    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)((m + 2) * ldx)))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)((n + 2) * ldy)))) return st;
+    tci::PassArgs g;
+    g.A = dA;
+    g.lda = lda;
+    g.m = mi;
+    g.n = ni;
+    g.k = -1;
+    g.X = c->xbuf;
+    g.ldx = ldx;
+    g.Y = c->ybuf;
+    g.ldy = ldy;
+    g.rowpos = c->rowpos;
+    g.colpos = c->colpos;
+    g.st = c->st;
+    g.Lp = c->Lp;
+    g.ldl = m;
+    g.Up = c->Up;
+    g.ldu = c->ldUp;
+    g.leftorth = leftorth;
+    g.cand = c->cand;
+    g.cb = pick_cb(m, n);
+    const int grid = tci::argmax_grid(mi, ni, -1, g.cb, std::min(c->pass_grid, kMaxGrid));
+    tci::launch_pass(c->stream, 0, false, g, grid);
+    int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
     while (k < mr && !stopped) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
-            const int ki = (int)kk;
-            tci::launch_select(c->stream, dA, lda, mi, ni, ki, c->cand, ncand, c->st, reltol, abstol);
-            tci::launch_swap(c->stream, dA, lda, mi, ni, ki, c->st, c->rowperm, c->colperm, c->ybuf,
-                             leftorth);
-            if (kk + 1 < mr) {
-                const int g = tci::argmax_grid(mi, ni, ki, kCB, kMaxGrid);
-                ev_begin(c, 0);
-                tci::launch_argmax_update(c->stream, true, dA, lda, mi, ni, ki, c->ybuf, c->st,
-                                          c->cand, g, kCB);
-                ev_end(c);
-                ncand = g;
-            }
+            tci::launch_select(c->stream, (int)kk, c->cand, grid, c->st, reltol, abstol, c->rowpos,
+                               c->colpos, c->rowperm, c->colperm, c->pivv);
+            // pass k: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
+            // finds the argmax for pivot k+1. After the last pivot only x_k / y_k are needed;
+            // that pass's argmax is discarded.
+            const int P = (int)(kk - t0) + 1;
+            const bool flush = (P >= nb) && (kk + 1 < mr);
+            g.k = (int)kk;
+            ev_begin(c, flush ? 0 : 2);
+            tci::launch_pass(c->stream, P, flush, g, grid);
+            ev_end(c);
+            if (flush) t0 = kk + 1;
         }
         k = kend;
         if (k < mr) {
@@ -219,10 +284,17 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     return TCI_OK;
 }
 
-int nan_check(tci_ctx* c, const double* dA, int64_t lda, int64_t m, int64_t n, int64_t np) {
+// Position-order L (m x np, ld m) into c->dL and U (np x n, ld np) into c->dU (either skipped when
+// want_* is false) with the NaN checks of matrixlu.jl:376-381.
+int extract_LU(tci_ctx* c, int64_t m, int64_t n, int64_t np, int leftorth, bool wantL, bool wantU) {
     if (np <= 0) return TCI_OK;
+    int st;
+    if (wantL && (st = ensure(c, &c->dL, &c->capL, (size_t)(m * np)))) return st;
+    if (wantU && (st = ensure(c, &c->dU, &c->capU, (size_t)(np * n)))) return st;
     HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
-    tci::launch_nan_check(c->stream, dA, lda, (int)m, (int)n, (int)np, c->flag);
+    tci::launch_extract(c->stream, c->Lp, m, c->Up, c->ldUp, c->pivv, c->rowperm, c->colperm, (int)m,
+                        (int)n, (int)np, leftorth, wantL ? c->dL : nullptr, m, wantU ? c->dU : nullptr,
+                        np, c->flag);
     HIPCHK(c, hipMemcpyAsync(c->hflag, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (*c->hflag & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
@@ -230,8 +302,7 @@ int nan_check(tci_ctx* c, const double* dA, int64_t lda, int64_t m, int64_t n, i
     return TCI_OK;
 }
 
-int fetch_perms(tci_ctx* c, int64_t m, int64_t n, int64_t* rowperm, int64_t* colperm,
-                int64_t nrow, int64_t ncol) {
+int fetch_perms(tci_ctx* c, int64_t* rowperm, int64_t* colperm, int64_t nrow, int64_t ncol) {
     if (rowperm && nrow > 0)
         HIPCHK(c, hipMemcpyAsync(rowperm, c->rowperm, nrow * sizeof(int64_t), hipMemcpyDeviceToHost,
                                  c->stream));
@@ -243,19 +314,16 @@ int fetch_perms(tci_ctx* c, int64_t m, int64_t n, int64_t* rowperm, int64_t* col
         for (int64_t i = 0; i < nrow; ++i) rowperm[i] += 1;
     if (colperm)
         for (int64_t j = 0; j < ncol; ++j) colperm[j] += 1;
-    (void)m;
-    (void)n;
     return TCI_OK;
 }
 
-int pivot_errors(tci_ctx* c, const double* dA, int64_t lda, int64_t np, double err, double* out) {
+// pivoterrors (matrixlu.jl:799): |pivot values| then lu.error
+int pivot_errors(tci_ctx* c, int64_t np, double err, double* out) {
     if (!out) return TCI_OK;
-    int st;
     if (np > 0) {
-        if ((st = ensure(c, &c->dDiag, &c->capDiag, (size_t)np + 1))) return st;
-        tci::launch_gather_diag(c->stream, dA, lda, (int)np, c->dDiag);
-        HIPCHK(c, hipMemcpyAsync(out, c->dDiag, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(out, c->pivv, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (int64_t t = 0; t < np; ++t) out[t] = std::fabs(out[t]);
     }
     out[np] = err;
     return TCI_OK;
@@ -326,6 +394,8 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (device < 0 || device >= ndev) return TCI_ERR_ARG;
     tci_ctx* c = new tci_ctx();
     c->device = device;
+    if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
+    if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -349,9 +419,10 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (!c) return TCI_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     auto fr = [](void* p) { if (p) hipFree(p); };
-    fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->ybuf); fr(c->flag);
+    fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
     fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
-    fr(c->dPiv);
+    fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
+    fr(c->dU);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
@@ -367,13 +438,20 @@ int tci_ctx_synchronize(tci_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }
+int tci_set_rrlu_flush(tci_ctx* c, int nb) {
+    if (nb < 1 || nb > tci::kMaxPend)
+        return set_err(c, TCI_ERR_ARG, "flush interval must be in 1.." + std::to_string(tci::kMaxPend));
+    c->flush_every = nb;
+    return TCI_OK;
+}
+
 int tci_set_timing(tci_ctx* c, int enabled) {
     c->timing = enabled != 0;
     ev_reset(c);
     return TCI_OK;
 }
 int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* launches) {
-    if (family < 0 || family > 1) return set_err(c, TCI_ERR_ARG, "family must be 0 or 1");
+    if (family < 0 || family > 2) return set_err(c, TCI_ERR_ARG, "family must be 0, 1 or 2");
     ev_collect(c);
     if (total_ms) *total_ms = c->fam_ms[family];
     if (launches) *launches = c->fam_n[family];
@@ -456,9 +534,9 @@ int tci_rrlu_inplace_d(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda
     int st;
     if ((st = rrlu_device(c, dA, m, n, lda, maxrank, reltol, abstol, leftorth, npivot, lasterror)))
         return st;
-    if ((st = nan_check(c, dA, lda, m, n, *npivot))) return st;
-    if ((st = fetch_perms(c, m, n, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
-    return pivot_errors(c, dA, lda, *npivot, *lasterror, pivoterrors);
+    if ((st = extract_LU(c, m, n, *npivot, leftorth, false, false))) return st;  // NaN checks
+    if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    return pivot_errors(c, *npivot, *lasterror, pivoterrors);
 }
 
 int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
@@ -470,41 +548,36 @@ int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
     int64_t ld;
     int st;
     if ((st = upload_matrix(c, A, m, n, lda, &ld))) return st;
-    if ((st = tci_rrlu_inplace_d(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, rowperm,
-                                 colperm, npivot, lasterror, nullptr)))
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    if ((st = rrlu_device(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, npivot, lasterror)))
         return st;
     const int64_t np = *npivot;
-    if (np > 0 && (L || U)) {
-        if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(m * np)))) return st;
-        if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(np * n)))) return st;
-        tci::launch_extract_LU(c->stream, c->dA, ld, (int)m, (int)n, (int)np, leftorth,
-                               L ? c->dF1 : nullptr, m, U ? c->dF2 : nullptr, np);
-        if (L)
-            HIPCHK(c, hipMemcpyAsync(L, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
-                                     c->stream));
-        if (U)
-            HIPCHK(c, hipMemcpy2DAsync(U, ldu * sizeof(double), c->dF2, np * sizeof(double),
-                                       np * sizeof(double), n, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-    }
+    if ((st = extract_LU(c, m, n, np, leftorth, L != nullptr, U != nullptr))) return st;
+    if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    if (np > 0 && L)
+        HIPCHK(c, hipMemcpyAsync(L, c->dL, m * np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (np > 0 && U)
+        HIPCHK(c, hipMemcpy2DAsync(U, ldu * sizeof(double), c->dU, np * sizeof(double),
+                                   np * sizeof(double), n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }
 
-// factors + outputs after rrlu_device on c->dA (ld)
-static int luci_outputs(tci_ctx* c, int64_t m, int64_t n, int64_t ld, int leftorth, int64_t np,
-                        double err, int64_t* rowidx, int64_t* colidx, double* pivoterrs,
-                        double* left, double* right) {
+// MatrixLUCI outputs after rrlu_device: pivot indices/errors and (optionally) the factors
+static int luci_outputs(tci_ctx* c, int64_t m, int64_t n, int leftorth, int64_t np, double err,
+                        int64_t* rowidx, int64_t* colidx, double* pivoterrs, double* left,
+                        double* right) {
     int st;
-    if ((st = nan_check(c, c->dA, ld, m, n, np))) return st;
-    if ((st = pivot_errors(c, c->dA, ld, np, err, pivoterrs))) return st;
-    if (np > 0) {
-        if ((st = fetch_perms(c, m, n, rowidx, colidx, rowidx ? np : 0, colidx ? np : 0))) return st;
-    }
-    if (np > 0 && (left || right)) {
+    const bool fac = np > 0 && (left || right);
+    if ((st = extract_LU(c, m, n, np, leftorth, fac, fac))) return st;
+    if ((st = pivot_errors(c, np, err, pivoterrs))) return st;
+    if (np > 0 && (st = fetch_perms(c, rowidx, colidx, rowidx ? np : 0, colidx ? np : 0))) return st;
+    if (fac) {
         if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(m * np)))) return st;
         if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(np * n)))) return st;
-        tci::launch_luci_factors(c->stream, c->dA, ld, (int)m, (int)n, (int)np, leftorth, c->rowperm,
-                                 c->colperm, left ? c->dF1 : nullptr, right ? c->dF2 : nullptr);
+        tci::launch_luci_factors(c->stream, c->dL, m, c->dU, np, (int)m, (int)n, (int)np, leftorth,
+                                 c->rowperm, c->colperm, left ? c->dF1 : nullptr,
+                                 right ? c->dF2 : nullptr);
         HIPCHK(c, hipGetLastError());
         if (left)
             HIPCHK(c, hipMemcpyAsync(left, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
@@ -528,7 +601,7 @@ int tci_luci_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
     if ((st = rrlu_device(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, &np, &err)))
         return st;
     *npivot = np;
-    return luci_outputs(c, m, n, ld, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
+    return luci_outputs(c, m, n, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
 }
 
 int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int64_t m, int32_t nl,
@@ -549,7 +622,7 @@ int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int6
     if ((st = rrlu_device(c, c->dA, m, n, ld, maxrank, reltol, abstol, leftorth, &np, &err)))
         return st;
     *npivot = np;
-    return luci_outputs(c, m, n, ld, leftorth, np, err, rowidx, colidx, pivoterrs,
+    return luci_outputs(c, m, n, leftorth, np, err, rowidx, colidx, pivoterrs,
                         want_factors ? left : nullptr, want_factors ? right : nullptr);
 }
 
@@ -596,6 +669,35 @@ int tci_fill_uniform_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t ld
     tci::launch_fill_uniform(c->stream, d_A, m, n, lda, seed);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_diag_stream_d(tci_ctx* c, const double* d_a, double* d_b, int64_t n, int reps, int grid,
+                      double* ms_read, double* ms_copy) {
+    if (!c || !d_a || n < 2 || reps < 1) return TCI_ERR_ARG;
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    tci::launch_stream_read(c->stream, d_a, n, c->maxbits, grid);  // warm
+    float ms = 0;
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    for (int r = 0; r < reps; ++r) tci::launch_stream_read(c->stream, d_a, n, c->maxbits, grid);
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventSynchronize(e1));
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms_read) *ms_read = ms / reps;
+    if (d_b && ms_copy) {
+        tci::launch_stream_copy(c->stream, d_a, d_b, n, grid);
+        HIPCHK(c, hipEventRecord(e0, c->stream));
+        for (int r = 0; r < reps; ++r) tci::launch_stream_copy(c->stream, d_a, d_b, n, grid);
+        HIPCHK(c, hipEventRecord(e1, c->stream));
+        HIPCHK(c, hipEventSynchronize(e1));
+        hipEventElapsedTime(&ms, e0, e1);
+        *ms_copy = ms / reps;
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
     return TCI_OK;
 }
 

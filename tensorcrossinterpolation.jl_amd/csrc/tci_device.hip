@@ -1,13 +1,7 @@
-// tci_device.hip -- gfx950 kernels for the TCI2 hot path.
-//
-// rrLU (matrixlu.jl:46-87, 254-322, 346-396) runs as three kernels per pivot on one stream:
-//   select  (1 block)   : reduce the per-block argmax candidates, stop test, record the pivot
-//   swap    (few blocks): physical row/column swap, true-division normalisation, pivot row -> ybuf
-//   update  (>= 1 block/CU x 8): A[i,j] -= x[i]*y[j] over the trailing block, fused with the
-//                          abs2 argmax of the *updated* values for the next pivot
-// Parity contract: compiled with -ffp-contract=off and written with __dmul_rn/__dsub_rn so the
-// rank-1 update is a separate multiply and subtract, exactly like Julia (matrixlu.jl:318); the
-// argmax compares abs2 = x*x with the reference's tie order (smallest column, then row).
+// tci_device.hip -- gfx950 kernels around the rrLU of tci_rrlu.hip: MatrixLUCI factors (matrixluci.jl:161-283), batch evaluation of
+// the integrand catalog (batcheval.jl:131-175 + util.jl:34-43), the site-tensor solve
+// (tensorci2.jl:620-627) and the synthetic-input generator.
+// Compiled with -ffp-contract=off: no multiply-add is fused unless written as such.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -18,408 +12,6 @@ namespace tci {
 
 static constexpr int32_t kBig = 0x7fffffff;
 
-// Julia Base.max for Float64 (NaN-propagating; max(-0.0, 0.0) == 0.0)
-__device__ __forceinline__ double jl_max(double x, double y) {
-    bool ysel = (y > x) || (signbit(y) < signbit(x));
-    if (ysel) return isnan(x) ? x : y;
-    return isnan(y) ? y : x;
-}
-
-__device__ __forceinline__ bool cand_better(double v1, int c1, int r1, double v2, int c2, int r2) {
-    return (v1 > v2) || (v1 == v2 && (c1 < c2 || (c1 == c2 && r1 < r2)));
-}
-
-__device__ __forceinline__ void wave_reduce_cand(double& v, int& c, int& r) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        double v2 = __shfl_xor(v, off);
-        int c2 = __shfl_xor(c, off);
-        int r2 = __shfl_xor(r, off);
-        if (cand_better(v2, c2, r2, v, c, r)) { v = v2; c = c2; r = r2; }
-    }
-}
-
-// Block reduction; every thread of wave 0 ends with the block winner.
-template <int NT>
-__device__ __forceinline__ void block_reduce_cand(double& v, int& c, int& r) {
-    __shared__ double sv[NT / 64];
-    __shared__ int sc[NT / 64];
-    __shared__ int sr[NT / 64];
-    wave_reduce_cand(v, c, r);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    if (l == 0) { sv[w] = v; sc[w] = c; sr[w] = r; }
-    __syncthreads();
-    if (w == 0) {
-        if (l < NT / 64) { v = sv[l]; c = sc[l]; r = sr[l]; }
-        else { v = -1.0; c = kBig; r = kBig; }
-        wave_reduce_cand(v, c, r);
-    }
-}
-
-// ---------------------------------------------------------------- update
-// One tile = 512 rows (256 lanes x double2) x CB columns of the trailing block. Rows are read
-// from an even base so every lane does 16-B loads/stores (lda even, base 16-B aligned); rows
-// outside the trailing block are written back unchanged (no other thread touches them).
-template <bool UPDATE>
-__global__ __launch_bounds__(kUpdThreads) void k_argmax_update(
-    double* __restrict__ A, int64_t lda, int m, int n, int k, const double* __restrict__ ybuf,
-    const RrluState* __restrict__ st, Cand* __restrict__ cand, int cb) {
-    if (UPDATE && st->done) return;
-    const int r_lo = k + 1, c_lo = k + 1;
-    const int rowBase = r_lo & ~1;
-    const int tiles_r = (m - rowBase + kRowsPerTile - 1) / kRowsPerTile;
-    const int ncols = n - c_lo;
-    const int tiles_c = (ncols + cb - 1) / cb;
-    const int ntiles = tiles_r * tiles_c;
-    double bv = -1.0;
-    int bc = kBig, br = kBig;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int tr = t % tiles_r, tc = t / tiles_r;
-        const int r0 = rowBase + tr * kRowsPerTile + 2 * threadIdx.x;
-        const bool in0 = (r0 >= r_lo) && (r0 < m);
-        const bool in1 = (r0 + 1 >= r_lo) && (r0 + 1 < m);
-        if (!(in0 || in1)) continue;
-        double x0 = 0.0, x1 = 0.0;
-        if (UPDATE) {
-            const double2 xv = *reinterpret_cast<const double2*>(A + r0 + (int64_t)k * lda);
-            x0 = xv.x;
-            x1 = xv.y;
-        }
-        const int j0 = c_lo + tc * cb;
-        const int j1 = min(j0 + cb, n);
-#pragma unroll 4
-        for (int j = j0; j < j1; ++j) {
-            double2* pa = reinterpret_cast<double2*>(A + r0 + (int64_t)j * lda);
-            double2 a = *pa;
-            if (UPDATE) {
-                const double y = ybuf[j];
-                if (in0) a.x = __dsub_rn(a.x, __dmul_rn(x0, y));
-                if (in1) a.y = __dsub_rn(a.y, __dmul_rn(x1, y));
-                *pa = a;
-            }
-            const double v0 = __dmul_rn(a.x, a.x), v1 = __dmul_rn(a.y, a.y);
-            if (in0 && cand_better(v0, j, r0, bv, bc, br)) { bv = v0; bc = j; br = r0; }
-            if (in1 && cand_better(v1, j, r0 + 1, bv, bc, br)) { bv = v1; bc = j; br = r0 + 1; }
-        }
-    }
-    block_reduce_cand<kUpdThreads>(bv, bc, br);
-    if (threadIdx.x == 0) cand[blockIdx.x] = Cand{bv, bc, br};
-}
-
-int argmax_grid(int m, int n, int k, int cb, int max_grid) {
-    const int r_lo = k + 1;
-    const int rowBase = r_lo & ~1;
-    const int tiles_r = (m - rowBase + kRowsPerTile - 1) / kRowsPerTile;
-    const int tiles_c = (n - (k + 1) + cb - 1) / cb;
-    long long nt = (long long)tiles_r * tiles_c;
-    if (nt < 1) nt = 1;
-    return (int)(nt < max_grid ? nt : max_grid);
-}
-
-void launch_argmax_update(hipStream_t s, bool update, double* A, int64_t lda, int m, int n, int k,
-                          const double* ybuf, const RrluState* st, Cand* cand, int grid, int cb) {
-    if (update)
-        hipLaunchKernelGGL(k_argmax_update<true>, dim3(grid), dim3(kUpdThreads), 0, s, A, lda, m, n,
-                           k, ybuf, st, cand, cb);
-    else
-        hipLaunchKernelGGL(k_argmax_update<false>, dim3(grid), dim3(kUpdThreads), 0, s, A, lda, m,
-                           n, k, ybuf, st, cand, cb);
-}
-
-// ---------------------------------------------------------------- select
-// Pivot k (0-based): winner over the candidates, then the stop test of _optimizerrlu!
-// (matrixlu.jl:359-368): error = |A[p,q]|; stop if (error < reltol*maxerror || error < abstol)
-// and npivot > 0; else maxerror = max(maxerror, error) and the pivot is accepted.
-__global__ __launch_bounds__(kSelThreads) void k_select(const double* __restrict__ A, int64_t lda,
-                                                        int k, const Cand* __restrict__ cand,
-                                                        int ncand, RrluState* st, double reltol,
-                                                        double abstol) {
-    if (st->done) return;
-    double bv = -1.0;
-    int bc = kBig, br = kBig;
-    for (int i = threadIdx.x; i < ncand; i += kSelThreads) {
-        const Cand c = cand[i];
-        if (cand_better(c.v, c.col, c.row, bv, bc, br)) { bv = c.v; bc = c.col; br = c.row; }
-    }
-    block_reduce_cand<kSelThreads>(bv, bc, br);
-    if (threadIdx.x == 0) {
-        int p = br, q = bc;
-        if (!(bv >= 0.0)) { p = k; q = k; }  // all NaN: Julia keeps (first(rows), first(cols))
-        const double a = A[p + (int64_t)q * lda];
-        const double err = fabs(a);
-        st->error = err;
-        if (((fabs(err) < reltol * st->maxerror) || (fabs(err) < abstol)) && k > 0) {
-            st->done = 1;
-            return;
-        }
-        st->maxerror = jl_max(st->maxerror, err);
-        st->p = p;
-        st->q = q;
-        st->pval = a;
-        st->np = k + 1;
-    }
-}
-
-void launch_select(hipStream_t s, const double* A, int64_t lda, int m, int n, int k,
-                   const Cand* cand, int ncand, RrluState* st, double reltol, double abstol) {
-    (void)m;
-    (void)n;
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s, A, lda, k, cand, ncand, st, reltol,
-                       abstol);
-}
-
-// ------------------------------------------------------------------ swap
-// addpivot! (matrixlu.jl:295-309): swaprow!(k,p) then swapcol!(k,q), then normalise column k
-// (leftorth) or row k. Every element is moved by exactly one thread: rows i not in {k,p} move
-// within their row, columns j not in {k,q} within their column, and thread 0 permutes the (up
-// to) four corners. ybuf[j] = A[k,j] after normalisation, the y of the rank-1 update.
-__global__ __launch_bounds__(256) void k_swap(double* __restrict__ A, int64_t lda, int m, int n,
-                                              int k, const RrluState* __restrict__ st,
-                                              int64_t* __restrict__ rowperm,
-                                              int64_t* __restrict__ colperm,
-                                              double* __restrict__ ybuf, int leftorth) {
-    if (st->done || st->np != k + 1) return;
-    const int p = (int)st->p, q = (int)st->q;
-    const double piv = st->pval;
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int stride = gridDim.x * blockDim.x;
-    for (int i = gid; i < m; i += stride) {
-        if (i == k || i == p) continue;
-        const double ak = A[i + (int64_t)k * lda], aq = A[i + (int64_t)q * lda];
-        double nk = aq;
-        if (leftorth && i > k) nk = nk / piv;
-        A[i + (int64_t)k * lda] = nk;
-        if (q != k) A[i + (int64_t)q * lda] = ak;
-    }
-    for (int j = gid; j < n; j += stride) {
-        if (j == k || j == q) continue;
-        const double bk = A[k + (int64_t)j * lda], bp = A[p + (int64_t)j * lda];
-        double nk = bp;
-        if (!leftorth && j > k) nk = nk / piv;
-        A[k + (int64_t)j * lda] = nk;
-        if (p != k) A[p + (int64_t)j * lda] = bk;
-        if (j > k) ybuf[j] = nk;
-    }
-    if (gid == 0) {
-        const double pre_kk = A[k + (int64_t)k * lda];
-        const double pre_kq = A[k + (int64_t)q * lda];
-        const double pre_pk = A[p + (int64_t)k * lda];
-        // post(k,k) = pre(p,q) = piv
-        A[k + (int64_t)k * lda] = piv;
-        if (q != k) {
-            double v = pre_pk;  // post(k,q) = pre(p,k)
-            if (!leftorth) v = v / piv;
-            A[k + (int64_t)q * lda] = v;
-            ybuf[q] = v;
-        }
-        if (p != k) {
-            double v = pre_kq;  // post(p,k) = pre(k,q)
-            if (leftorth) v = v / piv;
-            A[p + (int64_t)k * lda] = v;
-        }
-        if (p != k && q != k) A[p + (int64_t)q * lda] = pre_kk;  // post(p,q) = pre(k,k)
-        int64_t t = rowperm[k];
-        rowperm[k] = rowperm[p];
-        rowperm[p] = t;
-        t = colperm[k];
-        colperm[k] = colperm[q];
-        colperm[q] = t;
-    }
-}
-
-void launch_swap(hipStream_t s, double* A, int64_t lda, int m, int n, int k, const RrluState* st,
-                 int64_t* rowperm, int64_t* colperm, double* ybuf, int leftorth) {
-    int work = m > n ? m : n;
-    int grid = (work + 255) / 256;
-    if (grid > 64) grid = 64;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_swap, dim3(grid), dim3(256), 0, s, A, lda, m, n, k, st, rowperm, colperm,
-                       ybuf, leftorth);
-}
-
-__global__ void k_init_state(RrluState* st, int64_t* rowperm, int m, int64_t* colperm, int n) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int stride = gridDim.x * blockDim.x;
-    if (gid == 0) {
-        st->np = 0;
-        st->done = 0;
-        st->maxerror = 0.0;
-        st->error = __longlong_as_double(0x7ff8000000000000LL);  // rrLU{T}(...): error = NaN
-        st->p = st->q = 0;
-        st->pval = 0.0;
-    }
-    for (int i = gid; i < m; i += stride) rowperm[i] = i;
-    for (int j = gid; j < n; j += stride) colperm[j] = j;
-}
-
-void launch_init_state(hipStream_t s, RrluState* st, int64_t* rowperm, int m, int64_t* colperm,
-                       int n) {
-    int work = m > n ? m : n;
-    int grid = (work + 255) / 256;
-    if (grid > 256) grid = 256;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_init_state, dim3(grid), dim3(256), 0, s, st, rowperm, m, colperm, n);
-}
-
-// ----------------------------------------------------- extraction / checks
-// NaN check over L = tril(A[:, 1:np]) and U = triu(A[1:np, :]) (matrixlu.jl:372-381).
-// flag bit 0: NaN in L, bit 1: NaN in U.
-__global__ void k_nan_check(const double* __restrict__ A, int64_t lda, int m, int n, int np,
-                            int* flag) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int f = 0;
-    const int64_t nL = (int64_t)m * np;
-    for (int64_t e = gid; e < nL; e += stride) {
-        const int i = (int)(e % m), j = (int)(e / m);
-        if (i >= j && isnan(A[i + j * lda])) f |= 1;
-    }
-    const int64_t nU = (int64_t)np * n;
-    for (int64_t e = gid; e < nU; e += stride) {
-        const int i = (int)(e % np), j = (int)(e / np);
-        if (i <= j && isnan(A[i + j * lda])) f |= 2;
-    }
-    if (f) atomicOr(flag, f);
-}
-
-void launch_nan_check(hipStream_t s, const double* A, int64_t lda, int m, int n, int np,
-                      int* flag) {
-    long long work = (long long)m * np + (long long)np * n;
-    int grid = (int)((work + 255) / 256);
-    if (grid > 2048) grid = 2048;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_nan_check, dim3(grid), dim3(256), 0, s, A, lda, m, n, np, flag);
-}
-
-__global__ void k_gather_diag(const double* __restrict__ A, int64_t lda, int np, double* out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < np) out[i] = fabs(A[i + (int64_t)i * lda]);
-}
-
-void launch_gather_diag(hipStream_t s, const double* A, int64_t lda, int np, double* out) {
-    if (np <= 0) return;
-    hipLaunchKernelGGL(k_gather_diag, dim3((np + 255) / 256), dim3(256), 0, s, A, lda, np, out);
-}
-
-// L = tril(A[:,1:np]) (unit diagonal if leftorth), U = triu(A[1:np,:]) (unit diagonal otherwise)
-__global__ void k_extract_LU(const double* __restrict__ A, int64_t lda, int m, int n, int np,
-                             int leftorth, double* __restrict__ L, int64_t ldl,
-                             double* __restrict__ U, int64_t ldu) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    if (L) {
-        for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
-            const int i = (int)(e % m), j = (int)(e / m);
-            double v = (i >= j) ? A[i + j * lda] : 0.0;
-            if (leftorth && i == j) v = 1.0;
-            L[i + j * ldl] = v;
-        }
-    }
-    if (U) {
-        for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
-            const int i = (int)(e % np), j = (int)(e / np);
-            double v = (i <= j) ? A[i + j * lda] : 0.0;
-            if (!leftorth && i == j) v = 1.0;
-            U[i + j * ldu] = v;
-        }
-    }
-}
-
-void launch_extract_LU(hipStream_t s, const double* A, int64_t lda, int m, int n, int np,
-                       int leftorth, double* L, int64_t ldl, double* U, int64_t ldu) {
-    long long work = (long long)m * np + (long long)np * n;
-    int grid = (int)((work + 255) / 256);
-    if (grid > 4096) grid = 4096;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_extract_LU, dim3(grid), dim3(256), 0, s, A, lda, m, n, np, leftorth, L, ldl,
-                       U, ldu);
-}
-
-// -------------------------------------------------------- MatrixLUCI factors
-// leftorth: left = colstimespivotinv (matrixluci.jl:194-213): rows >= np solve X L11 = L21 in
-// place (one thread per row, back substitution over columns), then scatter by rowperm.
-__global__ void k_trsm_rows_lower(double* __restrict__ A, int64_t lda, int m, int np) {
-    const int i = np + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    for (int j = np - 1; j >= 0; --j) {
-        double s = A[i + (int64_t)j * lda];
-        for (int t = j + 1; t < np; ++t)
-            s = __dsub_rn(s, __dmul_rn(A[i + (int64_t)t * lda], A[t + (int64_t)j * lda]));
-        A[i + (int64_t)j * lda] = s;  // L11[j,j] == 1
-    }
-}
-
-// !leftorth: right = pivotinvtimesrows (matrixluci.jl:227-241): columns >= np solve
-// U11 x = U[:, c] in place (unit diagonal), one thread per column.
-__global__ void k_trsm_cols_upper(double* __restrict__ A, int64_t lda, int n, int np) {
-    const int c = np + blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    double* col = A + (int64_t)c * lda;
-    for (int a = np - 1; a >= 0; --a) {
-        double s = col[a];
-        for (int t = a + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(A[a + (int64_t)t * lda], col[t]));
-        col[a] = s;
-    }
-}
-
-// left (m x np, ld m) scatter for leftorth: out[rowperm[i], j] = i < np ? (i==j) : X[i,j]
-__global__ void k_left_scatter_lo(const double* __restrict__ A, int64_t lda, int m, int np,
-                                  const int64_t* __restrict__ rowperm, double* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
-        const int i = (int)(e % m), j = (int)(e / m);
-        const double v = (i < np) ? (i == j ? 1.0 : 0.0) : A[i + (int64_t)j * lda];
-        out[rowperm[i] + (int64_t)j * m] = v;
-    }
-}
-
-// right (np x n, ld np) for leftorth: rowmatrix = L11 * U, column-scattered (matrixluci.jl:175)
-__global__ void k_right_gemm_lo(const double* __restrict__ A, int64_t lda, int n, int np,
-                                const int64_t* __restrict__ colperm, double* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
-        const int a = (int)(e % np), j = (int)(e / np);
-        double s = 0.0;
-        const int tmax = a < j ? a : j;  // L11[a,t] = 0 for t > a; U[t,j] = 0 for t > j
-        for (int t = 0; t <= tmax; ++t) {
-            const double l = (t == a) ? 1.0 : A[a + (int64_t)t * lda];
-            s = __dadd_rn(s, __dmul_rn(l, A[t + (int64_t)j * lda]));
-        }
-        out[a + colperm[j] * (int64_t)np] = s;
-    }
-}
-
-// left (m x np) for !leftorth: colmatrix = left(lu) * U11 (matrixluci.jl:161-165)
-__global__ void k_left_gemm_ro(const double* __restrict__ A, int64_t lda, int m, int np,
-                               const int64_t* __restrict__ rowperm, double* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
-        const int i = (int)(e % m), j = (int)(e / m);
-        double s = 0.0;
-        const int tmax = i < j ? i : j;  // L[i,t] = 0 for t > i; U11[t,j] = 0 for t > j
-        for (int t = 0; t <= tmax; ++t) {
-            const double u = (t == j) ? 1.0 : A[t + (int64_t)j * lda];
-            s = __dadd_rn(s, __dmul_rn(A[i + (int64_t)t * lda], u));
-        }
-        out[rowperm[i] + (int64_t)j * m] = s;
-    }
-}
-
-// right (np x n) scatter for !leftorth: out[a, colperm[j]] = j < np ? (a==j) : X[a,j]
-__global__ void k_right_scatter_ro(const double* __restrict__ A, int64_t lda, int n, int np,
-                                   const int64_t* __restrict__ colperm, double* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
-        const int a = (int)(e % np), j = (int)(e / np);
-        const double v = (j < np) ? (a == j ? 1.0 : 0.0) : A[a + (int64_t)j * lda];
-        out[a + colperm[j] * (int64_t)np] = v;
-    }
-}
-
 static int grid_for(long long work, int cap) {
     long long g = (work + 255) / 256;
     if (g > cap) g = cap;
@@ -427,32 +19,118 @@ static int grid_for(long long work, int cap) {
     return (int)g;
 }
 
-void launch_luci_factors(hipStream_t s, double* A, int64_t lda, int m, int n, int np, int leftorth,
-                         const int64_t* rowperm, const int64_t* colperm, double* left,
-                         double* right) {
+// -------------------------------------------------------- MatrixLUCI factors
+// Inputs: position-order L (m x np, ld ldl) and U (np x n, ld ldu) with the reference's
+// diagonals (L unit if leftorth, U unit otherwise).
+// leftorth: left = colstimespivotinv (matrixluci.jl:194-213): rows >= np solve X L11 = L21 in
+// place (one thread per row, back substitution over columns), then scatter by rowperm.
+__global__ void k_trsm_rows_lower(double* __restrict__ L, int64_t ldl, int m, int np) {
+    const int i = np + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int j = np - 1; j >= 0; --j) {
+        double s = L[i + (int64_t)j * ldl];
+        for (int t = j + 1; t < np; ++t)
+            s = __dsub_rn(s, __dmul_rn(L[i + (int64_t)t * ldl], L[t + (int64_t)j * ldl]));
+        L[i + (int64_t)j * ldl] = s;  // L11[j,j] == 1
+    }
+}
+
+// !leftorth: right = pivotinvtimesrows (matrixluci.jl:227-241): columns >= np solve
+// U11 x = U[:, c] in place (unit diagonal), one thread per column.
+__global__ void k_trsm_cols_upper(double* __restrict__ U, int64_t ldu, int n, int np) {
+    const int c = np + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double* col = U + (int64_t)c * ldu;
+    for (int a = np - 1; a >= 0; --a) {
+        double s = col[a];
+        for (int t = a + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(U[a + (int64_t)t * ldu], col[t]));
+        col[a] = s;
+    }
+}
+
+// left (m x np, ld m) scatter for leftorth: out[rowperm[i], j] = i < np ? (i==j) : X[i,j]
+__global__ void k_left_scatter_lo(const double* __restrict__ L, int64_t ldl, int m, int np,
+                                  const int64_t* __restrict__ rowperm, double* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
+        const int i = (int)(e % m), j = (int)(e / m);
+        const double v = (i < np) ? (i == j ? 1.0 : 0.0) : L[i + (int64_t)j * ldl];
+        out[rowperm[i] + (int64_t)j * m] = v;
+    }
+}
+
+// right (np x n, ld np) for leftorth: rowmatrix = L11 * U, column-scattered (matrixluci.jl:175)
+__global__ void k_right_gemm_lo(const double* __restrict__ L, int64_t ldl,
+                                const double* __restrict__ U, int64_t ldu, int n, int np,
+                                const int64_t* __restrict__ colperm, double* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
+        const int a = (int)(e % np), j = (int)(e / np);
+        double s = 0.0;
+        const int tmax = a < j ? a : j;  // L11[a,t] = 0 for t > a; U[t,j] = 0 for t > j
+        for (int t = 0; t <= tmax; ++t)
+            s = __dadd_rn(s, __dmul_rn(L[a + (int64_t)t * ldl], U[t + (int64_t)j * ldu]));
+        out[a + colperm[j] * (int64_t)np] = s;
+    }
+}
+
+// left (m x np) for !leftorth: colmatrix = left(lu) * U11 (matrixluci.jl:161-165)
+__global__ void k_left_gemm_ro(const double* __restrict__ L, int64_t ldl,
+                               const double* __restrict__ U, int64_t ldu, int m, int np,
+                               const int64_t* __restrict__ rowperm, double* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
+        const int i = (int)(e % m), j = (int)(e / m);
+        double s = 0.0;
+        const int tmax = i < j ? i : j;  // L[i,t] = 0 for t > i; U11[t,j] = 0 for t > j
+        for (int t = 0; t <= tmax; ++t)
+            s = __dadd_rn(s, __dmul_rn(L[i + (int64_t)t * ldl], U[t + (int64_t)j * ldu]));
+        out[rowperm[i] + (int64_t)j * m] = s;
+    }
+}
+
+// right (np x n) scatter for !leftorth: out[a, colperm[j]] = j < np ? (a==j) : X[a,j]
+__global__ void k_right_scatter_ro(const double* __restrict__ U, int64_t ldu, int n, int np,
+                                   const int64_t* __restrict__ colperm, double* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
+        const int a = (int)(e % np), j = (int)(e / np);
+        const double v = (j < np) ? (a == j ? 1.0 : 0.0) : U[a + (int64_t)j * ldu];
+        out[a + colperm[j] * (int64_t)np] = v;
+    }
+}
+
+
+void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
+                         int n, int np, int leftorth, const int64_t* rowperm,
+                         const int64_t* colperm, double* left, double* right) {
     if (np <= 0) return;
     if (leftorth) {
-        // right first: it reads the untouched L11/U; the TRSM then overwrites L21 in place
+        // right first: it reads the untouched L11; the TRSM then overwrites L21 in place
         if (right)
             hipLaunchKernelGGL(k_right_gemm_lo, dim3(grid_for((long long)np * n, 8192)), dim3(256),
-                               0, s, A, lda, n, np, colperm, right);
+                               0, s, L, ldl, U, ldu, n, np, colperm, right);
         if (left) {
             if (m > np)
-                hipLaunchKernelGGL(k_trsm_rows_lower, dim3((m - np + 127) / 128), dim3(128), 0, s, A,
-                                   lda, m, np);
+                hipLaunchKernelGGL(k_trsm_rows_lower, dim3((m - np + 127) / 128), dim3(128), 0, s, L,
+                                   ldl, m, np);
             hipLaunchKernelGGL(k_left_scatter_lo, dim3(grid_for((long long)m * np, 8192)), dim3(256),
-                               0, s, A, lda, m, np, rowperm, left);
+                               0, s, L, ldl, m, np, rowperm, left);
         }
     } else {
         if (left)
             hipLaunchKernelGGL(k_left_gemm_ro, dim3(grid_for((long long)m * np, 8192)), dim3(256), 0,
-                               s, A, lda, m, np, rowperm, left);
+                               s, L, ldl, U, ldu, m, np, rowperm, left);
         if (right) {
             if (n > np)
-                hipLaunchKernelGGL(k_trsm_cols_upper, dim3((n - np + 127) / 128), dim3(128), 0, s, A,
-                                   lda, n, np);
+                hipLaunchKernelGGL(k_trsm_cols_upper, dim3((n - np + 127) / 128), dim3(128), 0, s, U,
+                                   ldu, n, np);
             hipLaunchKernelGGL(k_right_scatter_ro, dim3(grid_for((long long)np * n, 8192)),
-                               dim3(256), 0, s, A, lda, n, np, colperm, right);
+                               dim3(256), 0, s, U, ldu, n, np, colperm, right);
         }
     }
 }
@@ -473,6 +151,52 @@ __global__ void k_fill_uniform(double* A, int64_t m, int64_t n, int64_t lda, uin
         const int64_t i = e % m, j = e / m;
         A[i + j * lda] = (double)(splitmix64(base + (uint64_t)e) >> 11) * 0x1.0p-53;
     }
+}
+
+// Diagnostic: stream-read roofline calibration (max |a| over n doubles, 16-B loads).
+__global__ __launch_bounds__(256) void k_stream_read(const double2* __restrict__ a, int64_t n2,
+                                                     unsigned long long* out) {
+    double mx = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; e + 7 * stride < n2; e += 8 * stride) {  // 8 independent 16-B loads in flight
+        double2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a[e + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mx = fmax(mx, fmax(fabs(v[u].x), fabs(v[u].y)));
+    }
+    for (; e < n2; e += stride) {
+        const double2 v = a[e];
+        mx = fmax(mx, fmax(fabs(v.x), fabs(v.y)));
+    }
+    for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(mx));
+}
+
+// Diagnostic: stream-copy roofline calibration (b = a, 16-B loads and stores).
+__global__ __launch_bounds__(256) void k_stream_copy(const double2* __restrict__ a,
+                                                     double2* __restrict__ b, int64_t n2) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; e + 7 * stride < n2; e += 8 * stride) {
+        double2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a[e + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[e + u * stride] = v[u];
+    }
+    for (; e < n2; e += stride) b[e] = a[e];
+}
+
+void launch_stream_read(hipStream_t s, const double* a, int64_t n, unsigned long long* out, int grid) {
+    hipLaunchKernelGGL(k_stream_read, dim3(grid > 0 ? grid : grid_for(n / 2, 2048)), dim3(256), 0, s,
+                       reinterpret_cast<const double2*>(a), n / 2, out);
+}
+
+void launch_stream_copy(hipStream_t s, const double* a, double* b, int64_t n, int grid) {
+    hipLaunchKernelGGL(k_stream_copy, dim3(grid > 0 ? grid : grid_for(n / 2, 2048)), dim3(256), 0, s,
+                       reinterpret_cast<const double2*>(a), reinterpret_cast<double2*>(b), n / 2);
 }
 
 void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda,

@@ -1,17 +1,27 @@
-// tci_internal.h -- shared declarations between the device code (tci_device.hip) and the
-// C-ABI host layer (tci_abi.cpp). Not part of the public ABI (include/tci_hip.h).
+// tci_internal.h -- shared declarations between the device code (tci_rrlu.hip, tci_device.hip)
+// and the C-ABI host layer (tci_abi.cpp). Not part of the public ABI (include/tci_hip.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace tci {
 
-// Argmax candidate: abs2 value, column and row in the *current permuted* coordinates.
-// Sentinel (no finite candidate): v = -1, col = row = INT32_MAX.
+constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at most
+constexpr int kUpdThreads = 256;   // rrLU pass: 4 waves
+constexpr int kRowsPerTile = 512;  // 256 lanes x double2
+constexpr int kSelThreads = 1024;
+constexpr int kMaxCB = 32;         // rrLU pass: at most this many columns per tile
+
+// Argmax candidate: abs2 value, the (current, pending-updated) value itself, its column and row
+// *positions* (the reference's permuted coordinates: the tie-break keys) and its physical column
+// and row. Sentinel: v = -1, positions = INT32_MAX.
 struct Cand {
     double v;
-    int32_t col;
-    int32_t row;
+    double val;
+    int32_t cpos;
+    int32_t rpos;
+    int32_t pcol;
+    int32_t prow;
 };
 
 // Device-resident rrLU state (mirrors rrLU.npivot / rrLU.error and the loop-local maxerror of
@@ -22,8 +32,29 @@ struct RrluState {
     int32_t pad;
     double maxerror;
     double error;    // lu.error (last |A[p,q]| examined)
-    int64_t p, q;    // accepted pivot position (0-based, permuted coordinates)
-    double pval;     // A[p,q]
+    int64_t p, q;    // accepted pivot: PHYSICAL row / column
+    double pval;     // its current value
+};
+
+// Arguments of one rrLU pass (tci_rrlu.hip, k_pass).
+struct PassArgs {
+    double* A;
+    int64_t lda;
+    int m, n, k;
+    double* X;  // pending x's, [physical row][ldx]
+    int64_t ldx;
+    double* Y;  // pending y's, [physical column][ldy]
+    int64_t ldy;
+    const int32_t* rowpos;
+    const int32_t* colpos;
+    const RrluState* st;
+    double* Lp;  // L columns in physical row order (m x maxrank, ld ldl)
+    int64_t ldl;
+    double* Up;  // U rows in physical column order (maxrank x n, ld ldu)
+    int64_t ldu;
+    int leftorth;
+    Cand* cand;
+    int cb;
 };
 
 // Device view of an integrand (tci_func).
@@ -36,28 +67,31 @@ struct FuncDev {
     const int64_t* strides;    // device, column-major strides for TCI_F_TABLE
 };
 
-constexpr int kUpdThreads = 256;   // fused Schur update: 4 waves
-constexpr int kRowsPerTile = 512;  // 256 lanes x double2
-constexpr int kSelThreads = 1024;
-
-// ---- launchers (tci_device.hip)
-void launch_argmax_update(hipStream_t s, bool update, double* A, int64_t lda, int m, int n, int k,
-                          const double* ybuf, const RrluState* st, Cand* cand, int grid, int cb);
+// ---- rrLU (tci_rrlu.hip)
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
-void launch_select(hipStream_t s, const double* A, int64_t lda, int m, int n, int k,
-                   const Cand* cand, int ncand, RrluState* st, double reltol, double abstol);
-void launch_swap(hipStream_t s, double* A, int64_t lda, int m, int n, int k, const RrluState* st,
-                 int64_t* rowperm, int64_t* colperm, double* ybuf, int leftorth);
-void launch_init_state(hipStream_t s, RrluState* st, int64_t* rowperm, int m, int64_t* colperm, int n);
-void launch_nan_check(hipStream_t s, const double* A, int64_t lda, int m, int n, int np,
-                      int* flag);
-void launch_gather_diag(hipStream_t s, const double* A, int64_t lda, int np, double* out);
-void launch_extract_LU(hipStream_t s, const double* A, int64_t lda, int m, int n, int np,
-                       int leftorth, double* L, int64_t ldl, double* U, int64_t ldu);
-void launch_luci_factors(hipStream_t s, double* A, int64_t lda, int m, int n, int np,
-                         int leftorth, const int64_t* rowperm, const int64_t* colperm,
-                         double* left, double* right);
+// pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k)
+void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid);
+void launch_select(hipStream_t s, int k, const Cand* cand, int ncand, RrluState* st, double reltol,
+                   double abstol, int32_t* rowpos, int32_t* colpos, int64_t* rowphys,
+                   int64_t* colphys, double* pivvals);
+void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
+                       int32_t* colpos, int64_t* colphys, int n);
+// L (m x np, ld ldl) / U (np x n, ld ldu) in position order from the physical-order factors;
+// either output may be null (NaN check only). flag |= 1 (NaN in L), 2 (NaN in U).
+void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double* Up, int64_t ldup,
+                    const double* pivvals, const int64_t* rowphys, const int64_t* colphys, int m,
+                    int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
+                    int* flag);
+
+// ---- factors, batch evaluation, solve (tci_device.hip)
+// MatrixLUCI factors from position-order L (m x np) / U (np x n); L rows >= np (leftorth) or U
+// columns >= np (otherwise) are overwritten by the triangular solve.
+void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
+                         int n, int np, int leftorth, const int64_t* rowperm,
+                         const int64_t* colperm, double* left, double* right);
 void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed);
+void launch_stream_read(hipStream_t s, const double* a, int64_t n, unsigned long long* out, int grid);
+void launch_stream_copy(hipStream_t s, const double* a, double* b, int64_t n, int grid);
 
 // batch evaluation: I (m x nl) and J (n x nr) device int32 tables, row-major entries.
 // scratch must hold batcheval_scratch_bytes() bytes. maxbits: device uint64, zeroed.

@@ -1,0 +1,418 @@
+// tci_rrlu.hip -- exact full-pivoting rank-revealing LU (matrixlu.jl:46-87, 254-322, 346-396) on
+// gfx950, with deferred rank-1 updates and logical row/column swaps.
+//
+// The reference does, per pivot k: argmax of abs2 over the trailing block, swaprow!(k,p),
+// swapcol!(k,q), normalise, and A[i,j] -= x[i]*y[j] over the trailing block (24 B/element/pivot
+// on the CPU: a read pass + a read/write pass).
+//
+// Here the matrix never moves. The reference's swaps only permute positions, so they are kept as
+// maps: rowpos[i] / colpos[j] give the current position of physical row i / column j, rowphys /
+// colphys the inverse (= rowpermutation / colpermutation, since physical = original index). The
+// trailing block is the set of physical rows/columns whose position is > k, and the argmax key of
+// an element is (colpos[j], rowpos[i]): exactly the reference's column-major scan order over the
+// permuted matrix (ties -> smallest column position, then row position).
+//
+// Rank-1 updates are deferred: the trailing values live "stale" in HBM and up to P <= kMaxPend
+// pending updates x_s (per physical row) and y_s (per physical column) are applied on the fly,
+// in the reference's order and rounding (separate multiply and subtract), by every pass:
+//   v = stale[i,j]; for s in pending: v = v - x_s[i]*y_s[j]        (bit-identical values)
+// A pass only reads the block (8 B/element) except every nb-th, which writes the values back
+// (16 B/element) and empties the pending list. Physical indexing means the pending vectors need
+// no swapping. The new pivot's x_k (its column, normalised if leftorth) and y_k (its row,
+// normalised otherwise) are computed inside the pass by each workgroup for its own tile, and
+// written once (by designated workgroups) as the k-th column of L / row of U, kept in physical
+// order until extraction.
+//
+// Per pivot: select (1 workgroup: winner, stop test, map update) -> pass (<= 2048 workgroups).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "tci_internal.h"
+
+namespace tci {
+
+static constexpr int32_t kBig = 0x7fffffff;
+
+__device__ __forceinline__ double jl_max(double x, double y) {
+    bool ysel = (y > x) || (signbit(y) < signbit(x));
+    if (ysel) return isnan(x) ? x : y;
+    return isnan(y) ? y : x;
+}
+
+// (v1,c1,r1) beats (v2,c2,r2): larger abs2, then smaller column position, then smaller row
+// position -- the order in which the reference's column-major scan with strict '>' meets them.
+__device__ __forceinline__ bool cand_better(double v1, int c1, int r1, double v2, int c2, int r2) {
+    return (v1 > v2) || (v1 == v2 && (c1 < c2 || (c1 == c2 && r1 < r2)));
+}
+
+struct CandR {  // register form of Cand
+    double v, val;
+    int cpos, rpos, pc, pr;
+};
+
+__device__ __forceinline__ void cand_take(CandR& a, const CandR& b) {
+    if (cand_better(b.v, b.cpos, b.rpos, a.v, a.cpos, a.rpos)) a = b;
+}
+
+__device__ __forceinline__ void wave_reduce_cand(CandR& c) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        CandR o;
+        o.v = __shfl_xor(c.v, off);
+        o.val = __shfl_xor(c.val, off);
+        o.cpos = __shfl_xor(c.cpos, off);
+        o.rpos = __shfl_xor(c.rpos, off);
+        o.pc = __shfl_xor(c.pc, off);
+        o.pr = __shfl_xor(c.pr, off);
+        cand_take(c, o);
+    }
+}
+
+__device__ __forceinline__ CandR cand_none() { return CandR{-1.0, 0.0, kBig, kBig, 0, 0}; }
+
+// Block reduction; wave 0 ends with the winner.
+template <int NT>
+__device__ __forceinline__ void block_reduce_cand(CandR& c) {
+    __shared__ CandR sc[NT / 64];
+    wave_reduce_cand(c);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) sc[w] = c;
+    __syncthreads();
+    if (w == 0) {
+        c = (l < NT / 64) ? sc[l] : cand_none();
+        wave_reduce_cand(c);
+    }
+}
+
+// ------------------------------------------------------------------ pass
+// Runs after pivot k has been selected (k = -1: the initial argmax, no pending update). Tiles
+// cover the physical matrix: 512 rows (256 lanes x double2, 16-B accesses; lda even) x cb
+// columns; elements outside the trailing block are skipped (columns: uniformly; rows: masked).
+// P = pending updates including pivot k's own, which the workgroup derives for its tile:
+//   x_k[i] = (stale[i,b] - sum_{s<P-1} x_s[i] y_s[b]) (/ piv if leftorth)
+//   y_k[j] = (stale[a,j] - sum_{s<P-1} x_s[a] y_s[j]) (/ piv otherwise)
+// with (a, b) the pivot's physical row/column. Workgroups of column tile 0 store x_k (pending
+// slot P-1 and L column k), those of row tile 0 store y_k (slot and U row k).
+template <int P, bool FLUSH>
+__global__ __launch_bounds__(kUpdThreads) void k_pass(
+    double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
+    double* __restrict__ Y, int64_t ldy, const int32_t* __restrict__ rowpos,
+    const int32_t* __restrict__ colpos, const RrluState* __restrict__ st, double* __restrict__ Lp,
+    int64_t ldl, double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand,
+    int cb) {
+    if (st->done) return;
+    constexpr int U = 8;  // columns whose loads are in flight together
+    constexpr int PP = P > 0 ? P : 1;
+    __shared__ double ys[kMaxCB * PP];  // the tile's y_s, [column][slot]; slot P-1 = y_k
+    __shared__ int cpos_s[kMaxCB];
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const int tiles_c = (n + cb - 1) / cb;
+    const int ntiles = tiles_r * tiles_c;
+    int a = 0, b = 0;
+    double piv = 1.0;
+    if (P > 0) {
+        a = (int)st->p;  // physical row / column of pivot k
+        b = (int)st->q;
+        piv = st->pval;
+    }
+    CandR best = cand_none();
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform tile sequence
+        const int tr = t % tiles_r, tc = t / tiles_r;
+        const int j0 = tc * cb;
+        const int j1 = min(j0 + cb, n);
+        __syncthreads();  // previous tile's readers are done with ys / cpos_s
+        for (int c = threadIdx.x; c < j1 - j0; c += kUpdThreads) {
+            const int j = j0 + c;
+            const int cp = colpos[j];
+            cpos_s[c] = cp;
+            if (P > 0 && cp > k) {
+                const double* yj = Y + (int64_t)j * ldy;
+                const double* xa = X + (int64_t)a * ldx;
+                double yk = A[a + (int64_t)j * lda];
+                for (int s = 0; s < P - 1; ++s) {
+                    const double ysv = yj[s];
+                    ys[c * PP + s] = ysv;
+                    yk = __dsub_rn(yk, __dmul_rn(xa[s], ysv));
+                }
+                if (!leftorth) yk = yk / piv;
+                ys[c * PP + P - 1] = yk;
+                if (tr == 0) {
+                    Y[(int64_t)j * ldy + P - 1] = yk;
+                    Up[k + (int64_t)j * ldu] = yk;
+                }
+            }
+        }
+        __syncthreads();
+        const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;
+        if (r0 >= m) continue;
+        const bool has1 = r0 + 1 < m;
+        const int rp0 = rowpos[r0];
+        const int rp1 = has1 ? rowpos[r0 + 1] : -1;
+        const bool in0 = rp0 > k, in1 = rp1 > k;
+        if (!(in0 || in1)) continue;
+        double x0[PP], x1[PP];
+        if (P > 0) {
+            const double* xr = X + (int64_t)r0 * ldx;
+#pragma unroll
+            for (int s = 0; s < P - 1; s += 2) {
+                if (s + 1 < P - 1) {
+                    const double2 u = *reinterpret_cast<const double2*>(xr + s);
+                    const double2 w = *reinterpret_cast<const double2*>(xr + ldx + s);
+                    x0[s] = u.x;
+                    x0[s + 1] = u.y;
+                    x1[s] = w.x;
+                    x1[s + 1] = w.y;
+                } else {
+                    x0[s] = xr[s];
+                    x1[s] = xr[ldx + s];
+                }
+            }
+            // x_k for this thread's two rows
+            const double2 cb2 = *reinterpret_cast<const double2*>(A + r0 + (int64_t)b * lda);
+            const double* yb = Y + (int64_t)b * ldy;
+            double xk0 = cb2.x, xk1 = cb2.y;
+#pragma unroll
+            for (int s = 0; s < P - 1; ++s) {
+                const double yv = yb[s];
+                xk0 = __dsub_rn(xk0, __dmul_rn(x0[s], yv));
+                xk1 = __dsub_rn(xk1, __dmul_rn(x1[s], yv));
+            }
+            if (leftorth) {
+                xk0 = xk0 / piv;
+                xk1 = xk1 / piv;
+            }
+            x0[P - 1] = xk0;
+            x1[P - 1] = xk1;
+            if (tc == 0) {
+                if (in0) {
+                    X[(int64_t)r0 * ldx + P - 1] = xk0;
+                    Lp[r0 + (int64_t)k * ldl] = xk0;
+                }
+                if (in1) {
+                    X[(int64_t)(r0 + 1) * ldx + P - 1] = xk1;
+                    Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
+                }
+            }
+        }
+        // one column: apply the P pending updates in order (rows outside the block keep their
+        // value), write back if FLUSH, fold both rows into the running candidate
+        auto column = [&](double2 v, int c, double2* pa) {
+            const int cp = cpos_s[c];
+            if (cp <= k) return;  // column already pivoted: not in the trailing block
+            double u0 = v.x, u1 = v.y;
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const double y = ys[c * PP + s];
+                u0 = __dsub_rn(u0, __dmul_rn(x0[s], y));
+                u1 = __dsub_rn(u1, __dmul_rn(x1[s], y));
+            }
+            v.x = in0 ? u0 : v.x;
+            v.y = in1 ? u1 : v.y;
+            if (FLUSH) *pa = v;
+            // the full (value, column, row) comparison only matters when v >= best.v, which is
+            // rare once a large value has been seen: test that first (NaN fails it, as it should)
+            const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
+            if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                const int j = j0 + c;
+                if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
+                if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
+            }
+        };
+        double* base = A + r0;
+        int c = 0;
+        for (; c + U <= j1 - j0; c += U) {
+            double2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = *reinterpret_cast<const double2*>(base + (int64_t)(j0 + c + u) * lda);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                column(v[u], c + u, reinterpret_cast<double2*>(base + (int64_t)(j0 + c + u) * lda));
+        }
+        for (; c < j1 - j0; ++c) {
+            double2* pa = reinterpret_cast<double2*>(base + (int64_t)(j0 + c) * lda);
+            column(*pa, c, pa);
+        }
+    }
+    block_reduce_cand<kUpdThreads>(best);
+    if (threadIdx.x == 0)
+        cand[blockIdx.x] = Cand{best.v, best.val, best.cpos, best.rpos, best.pc, best.pr};
+}
+
+int argmax_grid(int m, int n, int k, int cb, int max_grid) {
+    (void)k;
+    const long long tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const long long tiles_c = (n + cb - 1) / cb;
+    long long nt = tiles_r * tiles_c;
+    if (nt < 1) nt = 1;
+    return (int)(nt < max_grid ? nt : max_grid);
+}
+
+template <int P>
+static void launch_pass_p(hipStream_t s, bool flush, const PassArgs& g, int grid) {
+    if (flush)
+        hipLaunchKernelGGL((k_pass<P, true>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m, g.n,
+                           g.k, g.X, g.ldx, g.Y, g.ldy, g.rowpos, g.colpos, g.st, g.Lp, g.ldl, g.Up,
+                           g.ldu, g.leftorth, g.cand, g.cb);
+    else
+        hipLaunchKernelGGL((k_pass<P, false>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m,
+                           g.n, g.k, g.X, g.ldx, g.Y, g.ldy, g.rowpos, g.colpos, g.st, g.Lp, g.ldl,
+                           g.Up, g.ldu, g.leftorth, g.cand, g.cb);
+}
+
+void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid) {
+    switch (P) {
+#define TCI_PASS_CASE(p) \
+    case p: launch_pass_p<p>(s, flush, g, grid); break;
+        TCI_PASS_CASE(0) TCI_PASS_CASE(1) TCI_PASS_CASE(2) TCI_PASS_CASE(3) TCI_PASS_CASE(4)
+        TCI_PASS_CASE(5) TCI_PASS_CASE(6) TCI_PASS_CASE(7) TCI_PASS_CASE(8) TCI_PASS_CASE(9)
+        TCI_PASS_CASE(10) TCI_PASS_CASE(11) TCI_PASS_CASE(12) TCI_PASS_CASE(13) TCI_PASS_CASE(14)
+        TCI_PASS_CASE(15) TCI_PASS_CASE(16)
+#undef TCI_PASS_CASE
+    default: break;
+    }
+}
+
+// ---------------------------------------------------------------- select
+// Pivot k: winner over the candidates (its value is the current, pending-updated one), the stop
+// test of _optimizerrlu! (matrixlu.jl:359-368), and on acceptance addpivot!'s swaps as map
+// updates: the rows at positions k and p exchange positions (swaprow!, :254-262), likewise the
+// columns at k and q (swapcol!, :269-275).
+__global__ __launch_bounds__(kSelThreads) void k_select(int k, const Cand* __restrict__ cand, int ncand,
+                                                        RrluState* st, double reltol, double abstol,
+                                                        int32_t* rowpos, int32_t* colpos,
+                                                        int64_t* rowphys, int64_t* colphys,
+                                                        double* pivvals) {
+    if (st->done) return;
+    CandR best = cand_none();
+    for (int i = threadIdx.x; i < ncand; i += kSelThreads) {
+        const Cand c = cand[i];
+        cand_take(best, CandR{c.v, c.val, c.cpos, c.rpos, c.pcol, c.prow});
+    }
+    block_reduce_cand<kSelThreads>(best);
+    if (threadIdx.x != 0) return;
+    int pr = best.pr, pc = best.pc, rp = best.rpos, cp = best.cpos;
+    double val = best.val;
+    if (!(best.v >= 0.0)) {
+        // every trailing value is NaN: Julia keeps (first(rows), first(cols)) = positions (k, k),
+        // whose current value is one of those NaNs
+        rp = k;
+        cp = k;
+        pr = (int)rowphys[k];
+        pc = (int)colphys[k];
+        val = __longlong_as_double(0x7ff8000000000000LL);
+    }
+    const double err = fabs(val);
+    st->error = err;
+    if (((fabs(err) < reltol * st->maxerror) || (fabs(err) < abstol)) && k > 0) {
+        st->done = 1;
+        return;
+    }
+    st->maxerror = jl_max(st->maxerror, err);
+    st->p = pr;
+    st->q = pc;
+    st->pval = val;
+    st->np = k + 1;
+    pivvals[k] = val;
+    // swaprow!(k, rp): the physical row at position k moves to position rp
+    const int64_t rk = rowphys[k];
+    rowphys[k] = pr;
+    rowphys[rp] = rk;
+    rowpos[pr] = k;
+    rowpos[rk] = rp;
+    // swapcol!(k, cp)
+    const int64_t ck = colphys[k];
+    colphys[k] = pc;
+    colphys[cp] = ck;
+    colpos[pc] = k;
+    colpos[ck] = cp;
+}
+
+void launch_select(hipStream_t s, int k, const Cand* cand, int ncand, RrluState* st, double reltol,
+                   double abstol, int32_t* rowpos, int32_t* colpos, int64_t* rowphys,
+                   int64_t* colphys, double* pivvals) {
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s, k, cand, ncand, st, reltol, abstol,
+                       rowpos, colpos, rowphys, colphys, pivvals);
+}
+
+__global__ void k_init_state(RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
+                             int32_t* colpos, int64_t* colphys, int n) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int stride = gridDim.x * blockDim.x;
+    if (gid == 0) {
+        st->np = 0;
+        st->done = 0;
+        st->maxerror = 0.0;
+        st->error = __longlong_as_double(0x7ff8000000000000LL);  // rrLU{T}(...): error = NaN
+        st->p = st->q = 0;
+        st->pval = 0.0;
+    }
+    for (int i = gid; i < m; i += stride) {
+        rowpos[i] = i;
+        rowphys[i] = i;
+    }
+    for (int j = gid; j < n; j += stride) {
+        colpos[j] = j;
+        colphys[j] = j;
+    }
+}
+
+void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
+                       int32_t* colpos, int64_t* colphys, int n) {
+    int work = m > n ? m : n;
+    int grid = (work + 255) / 256;
+    if (grid > 256) grid = 256;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_init_state, dim3(grid), dim3(256), 0, s, st, rowpos, rowphys, m, colpos,
+                       colphys, n);
+}
+
+// ------------------------------------------------------------ extraction
+// L (m x np, position order) and U (np x n) as _optimizerrlu! leaves them (matrixlu.jl:372-388):
+//   L[pos, t] = 0 (pos < t), diag (pos == t), Lp[rowphys[pos], t] (pos > t)
+//   U[t, pos] = 0 (pos < t), diag (pos == t), Up[t, colphys[pos]] (pos > t)
+// with the pivot value on U's diagonal and 1 on L's when leftorth, the reverse otherwise.
+// NaN check on the way (flag bit 0: L, bit 1: U).
+__global__ void k_extract(const double* __restrict__ Lp, int64_t ldlp, const double* __restrict__ Up,
+                          int64_t ldup, const double* __restrict__ pivvals,
+                          const int64_t* __restrict__ rowphys, const int64_t* __restrict__ colphys,
+                          int m, int n, int np, int leftorth, double* __restrict__ L, int64_t ldl,
+                          double* __restrict__ U, int64_t ldu, int* flag) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int f = 0;
+    for (int64_t e = gid; e < (int64_t)m * np; e += stride) {
+        const int pos = (int)(e % m), t = (int)(e / m);
+        double v;
+        if (pos < t) v = 0.0;
+        else if (pos == t) v = leftorth ? 1.0 : pivvals[t];
+        else v = Lp[rowphys[pos] + (int64_t)t * ldlp];
+        if (pos >= t && isnan(pos == t ? pivvals[t] : v)) f |= 1;
+        if (L) L[pos + (int64_t)t * ldl] = v;
+    }
+    for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
+        const int t = (int)(e % np), pos = (int)(e / np);
+        double v;
+        if (pos < t) v = 0.0;
+        else if (pos == t) v = leftorth ? pivvals[t] : 1.0;
+        else v = Up[t + colphys[pos] * ldup];
+        if (pos >= t && isnan(pos == t ? pivvals[t] : v)) f |= 2;
+        if (U) U[t + (int64_t)pos * ldu] = v;
+    }
+    if (f) atomicOr(flag, f);
+}
+
+void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double* Up, int64_t ldup,
+                    const double* pivvals, const int64_t* rowphys, const int64_t* colphys, int m,
+                    int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
+                    int* flag) {
+    long long work = (long long)m * np + (long long)np * n;
+    long long g = (work + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_extract, dim3((int)g), dim3(256), 0, s, Lp, ldlp, Up, ldup, pivvals, rowphys,
+                       colphys, m, n, np, leftorth, L, ldl, U, ldu, flag);
+}
+
+}  // namespace tci

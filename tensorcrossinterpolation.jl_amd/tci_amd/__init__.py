@@ -11,7 +11,7 @@ from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFind
 from .matrixlu import (DeviceMatrix, colindices, diag, lastpivoterror, ldiv, left, npivots, pivoterrors,
                        right, rowindices, rrLU, rrlu, rrlu_inplace_device)
 from .matrixluci import MatrixLUCI
-from .tensorci2 import (TensorCI2, convergencecriterion, crossinterpolate2, forwardsweep, kronecker_left,
+from .tensorci2 import (TensorCI2, convergencecriterion, crossinterpolate2, forwardsweep, kronecker_left, optfirstpivot,
                         kronecker_right, union_sets)
 
 __all__ = [name for name in dir() if not name.startswith("_")]

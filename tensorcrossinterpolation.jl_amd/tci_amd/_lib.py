@@ -50,6 +50,7 @@ SIGNATURES = {
     "tci_ctx_synchronize": ([vp], C.c_int),
     "tci_last_kernel_stats": ([vp, C.c_int, pdbl, pi64], C.c_int),
     "tci_set_timing": ([vp, C.c_int], C.c_int),
+    "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
@@ -63,6 +64,7 @@ SIGNATURES = {
                              vp, vp, pi64, pdbl, vp, vp], C.c_int),
     "tci_sitetensor_h": ([vp, vp, vp, i64, i32, vp, i64, i32, vp, i64, vp, pdbl], C.c_int),
     "tci_fill_uniform_d": ([vp, vp, i64, i64, i64, C.c_uint64], C.c_int),
+    "tci_diag_stream_d": ([vp, vp, vp, i64, C.c_int, C.c_int, pdbl, pdbl], C.c_int),
     "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
     "tci_free_d": ([vp, vp], C.c_int),
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),

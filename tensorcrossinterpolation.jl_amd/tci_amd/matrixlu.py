@@ -58,7 +58,7 @@ def rrlu(A, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True, ct
     rowperm = np.zeros(max(m, 1), np.int64)
     colperm = np.zeros(max(n, 1), np.int64)
     L = np.zeros(max(m * mr, 1))
-    U = np.zeros(max(mr * n, 1))
+    U = np.zeros(max(mr, 1) * max(n, 1))
     npv = C.c_int64()
     err = C.c_double()
     ctx.check(ctx.lib.tci_rrlu_h(ctx.h, _lib.ptr(Af), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
@@ -68,7 +68,7 @@ def rrlu(A, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True, ct
     k = npv.value
     Lm = L[: m * k].reshape((m, k), order="F").copy()
     # U was written with leading dimension max(mr, 1)
-    Um = U[: max(mr, 1) * n].reshape((max(mr, 1), n), order="F")[:k, :].copy() if n else np.zeros((k, 0))
+    Um = U[: max(mr, 1) * n].reshape((max(mr, 1), n), order="F")[:k, :].copy()
     return rrLU(rowperm[:m].copy(), colperm[:n].copy(), Lm, Um, leftorthogonal, k, err.value)
 
 

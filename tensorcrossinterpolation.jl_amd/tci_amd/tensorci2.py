@@ -525,3 +525,25 @@ def crossinterpolate2(f, localdims=None, initialpivots=None, **kwargs):
     tci = TensorCI2.from_function(f, localdims, initialpivots)
     ranks, errors = tci.optimize(f, **kwargs)
     return tci, ranks, errors
+
+
+def optfirstpivot(f, localdims, firstpivot=None, maxsweep=1000):
+    """optfirstpivot (util.jl:260-298). Within one leg only that leg changes, so the d candidate
+    values of a leg are evaluated in one device call and then scanned in the reference's order
+    (strict '>' against the running best, which is exactly the sequential loop)."""
+    L = len(localdims)
+    pivot = list(firstpivot) if firstpivot is not None else [1] * L
+    valf = abs(f.points([pivot])[0])
+    for _ in range(maxsweep):
+        valf_prev = valf
+        for i in range(L):
+            cand = np.tile(np.asarray(pivot, np.int32), (localdims[i], 1))
+            cand[:, i] = np.arange(1, localdims[i] + 1)
+            vals = np.abs(f.points(cand))
+            for d in range(localdims[i]):
+                if vals[d] > valf:
+                    valf = vals[d]
+                    pivot[i] = d + 1
+        if valf_prev == valf:
+            break
+    return [int(x) for x in pivot]
