@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-pivots", type=int, default=256)
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events in the timed region (no roofline line)")
     ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "8")),
                     help="deferred-update depth of the rrLU (results are identical for every nb)")
     args = ap.parse_args()
@@ -94,17 +96,19 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    ctx.set_timing(True)
+    # per-kernel device times: HIP events recorded on the context's stream around every pass
+    # launch inside the timed region (--no-kernel-timing: diagnostic run without them)
+    ctx.set_timing(not args.no_kernel_timing)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         np_, err, _, _, _ = step()
     barrier()
     dt = time.perf_counter() - t0
+    assert np_ == min(r, m, n), np_
     wb_ms, wb_launches = ctx.kernel_stats(0)
     ro_ms, ro_launches = ctx.kernel_stats(2)
     ctx.set_timing(False)
-    assert np_ == min(r, m, n), np_
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -118,16 +122,18 @@ def main():
     (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
+        dom_key = "rrlu_read_only_pass"
         dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,false> (read-only: pending updates "
                                                        "applied on the fly + abs2 argmax)", ro_ms,
                                                        ro_launches, ro_b, ro_n)
     else:
+        dom_key = "rrlu_write_back_pass"
         dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,true> (pending updates applied and "
                                                        "written back + abs2 argmax)", wb_ms, wb_launches,
                                                        wb_b, wb_n)
     avg_launch_ms = dom_ms / max(dom_launches, 1)
     bytes_per_launch = dom_bytes / max(dom_n, 1)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     other = {"write_back_pass": {"launches": wb_launches, "avg_ms": round(wb_ms / max(wb_launches, 1), 5),
                                  "GBps": round(wb_b / max(wb_n, 1) / (wb_ms / max(wb_launches, 1) * 1e-3) / 1e9, 1)
                                  if wb_launches else None},
@@ -156,13 +162,20 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
                      "deferred_depth_nb": nb},
     }
-    # roofline calibration on the same buffers: 16-B stream read and stream copy
+    # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
+    # WRITE_SIZE, scripts/profile_round.sh); null when none matches
+    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb))
+    # roofline calibration on the same buffers: 16-B stream read and stream copy, best grid
     import ctypes as C
-    ms_r, ms_c = C.c_double(), C.c_double()
     nel = A.ld * n
-    ctx.check(ctx.lib.tci_diag_stream_d(ctx.h, A.ptr, W.ptr, nel, 5, 0, C.byref(ms_r), C.byref(ms_c)))
-    out["roofline"]["measured_stream_read_GBps"] = round(8.0 * nel / (ms_r.value * 1e-3) / 1e9, 1)
-    out["roofline"]["measured_stream_copy_GBps"] = round(16.0 * nel / (ms_c.value * 1e-3) / 1e9, 1)
+    best_r = best_c = 0.0
+    for grid in (256, 512, 1024, 2048):
+        ms_r, ms_c = C.c_double(), C.c_double()
+        ctx.check(ctx.lib.tci_diag_stream_d(ctx.h, A.ptr, W.ptr, nel, 5, grid, C.byref(ms_r), C.byref(ms_c)))
+        best_r = max(best_r, 8.0 * nel / (ms_r.value * 1e-3) / 1e9)
+        best_c = max(best_c, 16.0 * nel / (ms_c.value * 1e-3) / 1e9)
+    out["roofline"]["measured_stream_read_GBps"] = round(best_r, 1)
+    out["roofline"]["measured_stream_copy_GBps"] = round(best_c, 1)
     A.free()
     W.free()
 
@@ -174,6 +187,23 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 8}  # the bench command profiled there
+
+
+def pmc_traffic(fam, m, n, r, nb):
+    """HBM bytes per launch of kernel family `fam` from the committed rocprofv3 PMC summary."""
+    if {"m": m, "n": n, "r": r, "nb": nb} != PMC_CONFIG or not os.path.exists(PMC_SUMMARY):
+        return {"traffic": None}
+    with open(PMC_SUMMARY) as fh:
+        rec = json.load(fh).get(fam, {})
+    if "hbm_bytes_per_launch" not in rec:
+        return {"traffic": None}
+    return {"traffic": rec["hbm_bytes_per_launch"],
+            "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE, "
+                              f"{rec['dispatches_profiled']} dispatches)"}
 
 
 def extras(T, ctx):

@@ -1,26 +1,62 @@
-"""Summarise rocprofv3 PMC csv passes per kernel family (mean per dispatch)."""
+"""Summarise rocprofv3 PMC passes (scripts/profile_round.sh) per kernel family.
+
+Usage: python scripts/pmc_summary.py PMC_DIR [OUT_JSON]
+
+Every pmc*/ directory under PMC_DIR holds one counter group's run_counter_collection.csv. Values
+are averaged per dispatch. FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half
+the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md "HBM"), so read bytes =
+2 x FETCH_SIZE x 1024. The stream-read kernel of the same run (k_stream_read, a known byte count)
+is kept in the summary as the calibration check of that factor.
+"""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
 
-root = sys.argv[1]
-agg = defaultdict(lambda: defaultdict(list))
-durs = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "pmc*", "run_counter_collection.csv"))):
-    for row in csv.DictReader(open(f)):
-        name = row["Kernel_Name"]
-        short = name.split("(")[0].replace("void ", "")
-        if "k_pass" in short:
-            short = short + ("" if "true" not in short else "")
-        agg[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
-        agg[short]["_vgpr"].append(float(row["VGPR_Count"]))
-        durs[short].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-3)
-for k in sorted(agg, key=lambda k: -sum(durs[k])):
-    d = agg[k]
-    line = f"{k[:60]:60s} n={len(durs[k]) // max(1, len([c for c in d if c != '_vgpr'])):4d} us={sum(durs[k]) / len(durs[k]):8.1f}"
-    for c in sorted(d):
-        v = sum(d[c]) / len(d[c])
-        line += f" {c}={v:.4g}"
-    print(line)
+
+def family(name):
+    short = name.split("(")[0].replace("void ", "").strip()
+    if short.startswith("tci::k_pass<"):
+        return "rrlu_write_back_pass" if "true>" in short else "rrlu_read_only_pass"
+    return short
+
+
+def summarise(root):
+    vals = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(root, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
+        seen = set()
+        for row in csv.DictReader(open(f)):
+            fam = family(row["Kernel_Name"])
+            vals[fam][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            key = (f, row["Dispatch_Id"])
+            if key not in seen:
+                seen.add(key)
+                durs[fam].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-3)
+    out = {}
+    for fam, d in vals.items():
+        rec = {"dispatches_profiled": len(durs[fam]),
+               "avg_us_under_pmc": round(sum(durs[fam]) / max(len(durs[fam]), 1), 2)}
+        for c, v in sorted(d.items()):
+            rec[c] = sum(v) / len(v)
+        if "FETCH_SIZE" in rec:
+            rec["read_bytes_per_launch"] = 2.0 * rec["FETCH_SIZE"] * 1024.0
+        if "WRITE_SIZE" in rec:
+            rec["write_bytes_per_launch"] = rec["WRITE_SIZE"] * 1024.0
+        if "read_bytes_per_launch" in rec and "write_bytes_per_launch" in rec:
+            rec["hbm_bytes_per_launch"] = rec["read_bytes_per_launch"] + rec["write_bytes_per_launch"]
+        out[fam] = rec
+    return out
+
+
+if __name__ == "__main__":
+    res = summarise(sys.argv[1])
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w") as fh:
+            json.dump(res, fh, indent=1, sort_keys=True)
+    for fam, rec in sorted(res.items(), key=lambda kv: -kv[1]["avg_us_under_pmc"] * kv[1]["dispatches_profiled"]):
+        print(f"{fam[:48]:48s} n={rec['dispatches_profiled']:5d} us={rec['avg_us_under_pmc']:9.2f} "
+              f"read={rec.get('read_bytes_per_launch', float('nan')) / 1e6:9.2f}MB "
+              f"write={rec.get('write_bytes_per_launch', float('nan')) / 1e6:9.2f}MB")

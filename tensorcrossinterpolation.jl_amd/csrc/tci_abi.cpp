@@ -38,8 +38,10 @@ struct tci_ctx {
     double* ybuf = nullptr;
     size_t capY = 0;
     int flush_every = 8;  // deferred-update depth nb (1 = write back every pivot)
-    int pass_grid = 2048;  // workgroups of an rrLU pass (env TCI_PASS_GRID)
+    int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
+    int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int* flag = nullptr;
+    unsigned* ticket = nullptr;  // rrLU pass tail hand-off counter (zero between passes)
     int* hflag = nullptr;  // pinned
     unsigned long long* maxbits = nullptr;
     unsigned long long* hmaxbits = nullptr;  // pinned
@@ -180,7 +182,7 @@ void ev_collect(tci_ctx* c) {
     c->evused = 0;
 }
 
-constexpr int kMaxGrid = 2048;  // 8 workgroups per CU x 256 CUs
+constexpr int kMaxGrid = tci::kMaxPassGrid;
 
 // columns per rrLU tile (multiple of the kernel's 8-column batch): wide tiles when the matrix
 // is large, narrower ones so that small matrices still spread over every CU
@@ -244,21 +246,30 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     g.leftorth = leftorth;
     g.cand = c->cand;
     g.cb = pick_cb(m, n);
+    if (const char* e = getenv("TCI_RRLU_CB")) g.cb = std::max(8, std::min(atoi(e) / 8 * 8, tci::kMaxCB));
+    g.rev = 0;
+    g.rowphys = c->rowperm;
+    g.colphys = c->colperm;
+    g.pivvals = c->pivv;
+    g.reltol = reltol;
+    g.abstol = abstol;
+    g.ticket = c->ticket;
+    g.selk = 0;
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb, std::min(c->pass_grid, kMaxGrid));
-    tci::launch_pass(c->stream, 0, false, g, grid);
+    tci::launch_pass(c->stream, 0, false, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
     while (k < mr && !stopped) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
-            tci::launch_select(c->stream, (int)kk, c->cand, grid, c->st, reltol, abstol, c->rowpos,
-                               c->colpos, c->rowperm, c->colperm, c->pivv);
             // pass k: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
-            // finds the argmax for pivot k+1. After the last pivot only x_k / y_k are needed;
-            // that pass's argmax is discarded.
+            // selects pivot k+1 from the updated block. After the last pivot only x_k / y_k are
+            // needed: no selection.
             const int P = (int)(kk - t0) + 1;
             const bool flush = (P >= nb) && (kk + 1 < mr);
             g.k = (int)kk;
+            g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
+            g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             ev_begin(c, flush ? 0 : 2);
             tci::launch_pass(c->stream, P, flush, g, grid);
             ev_end(c);
@@ -396,6 +407,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     c->device = device;
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
+    if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -404,6 +416,8 @@ int tci_ctx_create(int device, tci_ctx** out) {
     bool ok = hipMalloc((void**)&c->st, sizeof(RrluState)) == hipSuccess &&
               hipHostMalloc((void**)&c->hst, sizeof(RrluState), 0) == hipSuccess &&
               hipMalloc((void**)&c->flag, sizeof(int)) == hipSuccess &&
+              hipMalloc((void**)&c->ticket, sizeof(unsigned)) == hipSuccess &&
+              hipMemset(c->ticket, 0, sizeof(unsigned)) == hipSuccess &&
               hipHostMalloc((void**)&c->hflag, sizeof(int), 0) == hipSuccess &&
               hipMalloc((void**)&c->maxbits, sizeof(unsigned long long)) == hipSuccess &&
               hipHostMalloc((void**)&c->hmaxbits, sizeof(unsigned long long), 0) == hipSuccess;
@@ -420,6 +434,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     auto fr = [](void* p) { if (p) hipFree(p); };
     fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
+    fr(c->ticket);
     fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
     fr(c->dU);

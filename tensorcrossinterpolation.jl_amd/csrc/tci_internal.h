@@ -9,8 +9,8 @@ namespace tci {
 constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at most
 constexpr int kUpdThreads = 256;   // rrLU pass: 4 waves
 constexpr int kRowsPerTile = 512;  // 256 lanes x double2
-constexpr int kSelThreads = 1024;
 constexpr int kMaxCB = 32;         // rrLU pass: at most this many columns per tile
+constexpr int kMaxPassGrid = 2048; // rrLU pass: at most this many workgroups (8 per CU)
 
 // Argmax candidate: abs2 value, the (current, pending-updated) value itself, its column and row
 // *positions* (the reference's permuted coordinates: the tie-break keys) and its physical column
@@ -25,7 +25,7 @@ struct Cand {
 };
 
 // Device-resident rrLU state (mirrors rrLU.npivot / rrLU.error and the loop-local maxerror of
-// _optimizerrlu!, matrixlu.jl:353-369). Written only by the single-block select kernel.
+// _optimizerrlu!, matrixlu.jl:353-369). Written only by the selecting workgroup of a pass.
 struct RrluState {
     int64_t np;      // pivots accepted so far
     int32_t done;    // stop test fired (matrixlu.jl:363-365)
@@ -45,9 +45,9 @@ struct PassArgs {
     int64_t ldx;
     double* Y;  // pending y's, [physical column][ldy]
     int64_t ldy;
-    const int32_t* rowpos;
-    const int32_t* colpos;
-    const RrluState* st;
+    int32_t* rowpos;
+    int32_t* colpos;
+    RrluState* st;
     double* Lp;  // L columns in physical row order (m x maxrank, ld ldl)
     int64_t ldl;
     double* Up;  // U rows in physical column order (maxrank x n, ld ldu)
@@ -55,6 +55,28 @@ struct PassArgs {
     int leftorth;
     Cand* cand;
     int cb;
+    int rev;  // walk the tiles in descending memory order (alternated pass to pass, see k_pass)
+    // pivot selection fused into the pass's tail (the last workgroup to finish): pivot selk
+    // (< 0: none, e.g. after the last pivot)
+    int selk;
+    int64_t* rowphys;
+    int64_t* colphys;
+    double* pivvals;
+    double reltol, abstol;
+    unsigned* ticket;  // zero between passes
+};
+
+// Selection fields of PassArgs as seen by the device.
+struct SelArgs {
+    int32_t* rowpos;
+    int32_t* colpos;
+    int64_t* rowphys;
+    int64_t* colphys;
+    double* pivvals;
+    RrluState* st;
+    unsigned* ticket;
+    double reltol, abstol;
+    int selk;
 };
 
 // Device view of an integrand (tci_func).
@@ -69,11 +91,9 @@ struct FuncDev {
 
 // ---- rrLU (tci_rrlu.hip)
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
-// pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k)
+// pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
+// last workgroup selects pivot g.selk
 void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid);
-void launch_select(hipStream_t s, int k, const Cand* cand, int ncand, RrluState* st, double reltol,
-                   double abstol, int32_t* rowpos, int32_t* colpos, int64_t* rowphys,
-                   int64_t* colphys, double* pivvals);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // L (m x np, ld ldl) / U (np x n, ld ldu) in position order from the physical-order factors;

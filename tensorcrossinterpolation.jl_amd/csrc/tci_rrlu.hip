@@ -94,13 +94,47 @@ __device__ __forceinline__ void block_reduce_cand(CandR& c) {
 //   y_k[j] = (stale[a,j] - sum_{s<P-1} x_s[a] y_s[j]) (/ piv otherwise)
 // with (a, b) the pivot's physical row/column. Workgroups of column tile 0 store x_k (pending
 // slot P-1 and L column k), those of row tile 0 store y_k (slot and U row k).
+//
+// Tail: the workgroups publish their candidates (sc1 stores, then one agent-scope atomic add each;
+// MI355X_MICROARCH.md hand-off table, first row) and the one whose add comes last reduces them and
+// commits pivot sel.selk -- the selection needs no launch of its own. rowpos / colpos / st change
+// only there, after every other workgroup has finished reading them.
+__device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
+                             int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
+                             double* pivvals);
+
+__device__ __forceinline__ void store_cand_sc1(Cand* dst, const CandR& c) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+    const uint64_t w0 = (uint64_t)__double_as_longlong(c.v);
+    const uint64_t w1 = (uint64_t)__double_as_longlong(c.val);
+    const uint64_t w2 = (uint64_t)(uint32_t)c.cpos | ((uint64_t)(uint32_t)c.rpos << 32);
+    const uint64_t w3 = (uint64_t)(uint32_t)c.pc | ((uint64_t)(uint32_t)c.pr << 32);
+    __hip_atomic_store(d + 0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 2, w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 3, w3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ CandR load_cand_sc1(const Cand* src) {
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(src);
+    const uint64_t w0 = __hip_atomic_load(s + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t w1 = __hip_atomic_load(s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t w2 = __hip_atomic_load(s + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t w3 = __hip_atomic_load(s + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return CandR{__longlong_as_double((long long)w0), __longlong_as_double((long long)w1),
+                 (int)(uint32_t)w2, (int)(uint32_t)(w2 >> 32), (int)(uint32_t)w3,
+                 (int)(uint32_t)(w3 >> 32)};
+}
+
 template <int P, bool FLUSH>
 __global__ __launch_bounds__(kUpdThreads) void k_pass(
     double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
-    double* __restrict__ Y, int64_t ldy, const int32_t* __restrict__ rowpos,
-    const int32_t* __restrict__ colpos, const RrluState* __restrict__ st, double* __restrict__ Lp,
-    int64_t ldl, double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand,
-    int cb) {
+    double* __restrict__ Y, int64_t ldy, double* __restrict__ Lp, int64_t ldl,
+    double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand, int cb, int rev,
+    SelArgs sel) {
+    RrluState* st = sel.st;
+    const int32_t* rowpos = sel.rowpos;
+    const int32_t* colpos = sel.colpos;
     if (st->done) return;
     constexpr int U = 8;  // columns whose loads are in flight together
     constexpr int PP = P > 0 ? P : 1;
@@ -117,7 +151,10 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         piv = st->pval;
     }
     CandR best = cand_none();
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform tile sequence
+    for (int tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {  // block-uniform tile sequence
+        // serpentine: a reversed pass starts on the tiles the previous pass touched last, which
+        // are still in the 256 MiB Infinity Cache
+        const int t = rev ? ntiles - 1 - tt : tt;
         const int tr = t % tiles_r, tc = t / tiles_r;
         const int j0 = tc * cb;
         const int j1 = min(j0 + cb, n);
@@ -236,8 +273,35 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         }
     }
     block_reduce_cand<kUpdThreads>(best);
-    if (threadIdx.x == 0)
-        cand[blockIdx.x] = Cand{best.v, best.val, best.cpos, best.rpos, best.pc, best.pr};
+    if (sel.selk < 0) return;
+    __shared__ int last_s;
+    if (threadIdx.x == 0) {
+        store_cand_sc1(cand + blockIdx.x, best);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old =
+            __hip_atomic_fetch_add(sel.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = (old == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
+    constexpr int CPT = kMaxPassGrid / kUpdThreads;
+    CandR cs[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int i = threadIdx.x + u * kUpdThreads;
+        cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
+    }
+    CandR w = cs[0];
+#pragma unroll
+    for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
+    __syncthreads();  // block_reduce_cand's LDS slots are reused
+    block_reduce_cand<kUpdThreads>(w);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
+                     sel.colphys, sel.pivvals);
+    }
 }
 
 int argmax_grid(int m, int n, int k, int cb, int max_grid) {
@@ -251,14 +315,16 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 
 template <int P>
 static void launch_pass_p(hipStream_t s, bool flush, const PassArgs& g, int grid) {
+    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals,
+                      g.st,     g.ticket, g.reltol,  g.abstol,  g.selk};
     if (flush)
         hipLaunchKernelGGL((k_pass<P, true>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m, g.n,
-                           g.k, g.X, g.ldx, g.Y, g.ldy, g.rowpos, g.colpos, g.st, g.Lp, g.ldl, g.Up,
-                           g.ldu, g.leftorth, g.cand, g.cb);
+                           g.k, g.X, g.ldx, g.Y, g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand,
+                           g.cb, g.rev, sel);
     else
         hipLaunchKernelGGL((k_pass<P, false>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m,
-                           g.n, g.k, g.X, g.ldx, g.Y, g.ldy, g.rowpos, g.colpos, g.st, g.Lp, g.ldl,
-                           g.Up, g.ldu, g.leftorth, g.cand, g.cb);
+                           g.n, g.k, g.X, g.ldx, g.Y, g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth,
+                           g.cand, g.cb, g.rev, sel);
 }
 
 void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid) {
@@ -275,23 +341,13 @@ void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid) 
 }
 
 // ---------------------------------------------------------------- select
-// Pivot k: winner over the candidates (its value is the current, pending-updated one), the stop
-// test of _optimizerrlu! (matrixlu.jl:359-368), and on acceptance addpivot!'s swaps as map
-// updates: the rows at positions k and p exchange positions (swaprow!, :254-262), likewise the
-// columns at k and q (swapcol!, :269-275).
-__global__ __launch_bounds__(kSelThreads) void k_select(int k, const Cand* __restrict__ cand, int ncand,
-                                                        RrluState* st, double reltol, double abstol,
-                                                        int32_t* rowpos, int32_t* colpos,
-                                                        int64_t* rowphys, int64_t* colphys,
-                                                        double* pivvals) {
-    if (st->done) return;
-    CandR best = cand_none();
-    for (int i = threadIdx.x; i < ncand; i += kSelThreads) {
-        const Cand c = cand[i];
-        cand_take(best, CandR{c.v, c.val, c.cpos, c.rpos, c.pcol, c.prow});
-    }
-    block_reduce_cand<kSelThreads>(best);
-    if (threadIdx.x != 0) return;
+// Pivot k: given the winner over all candidates (its value is the current, pending-updated one),
+// the stop test of _optimizerrlu! (matrixlu.jl:359-368), and on acceptance addpivot!'s swaps as
+// map updates: the rows at positions k and p exchange positions (swaprow!, :254-262), likewise
+// the columns at k and q (swapcol!, :269-275). One thread.
+__device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
+                             int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
+                             double* pivvals) {
     int pr = best.pr, pc = best.pc, rp = best.rpos, cp = best.cpos;
     double val = best.val;
     if (!(best.v >= 0.0)) {
@@ -327,13 +383,6 @@ __global__ __launch_bounds__(kSelThreads) void k_select(int k, const Cand* __res
     colphys[cp] = ck;
     colpos[pc] = k;
     colpos[ck] = cp;
-}
-
-void launch_select(hipStream_t s, int k, const Cand* cand, int ncand, RrluState* st, double reltol,
-                   double abstol, int32_t* rowpos, int32_t* colpos, int64_t* rowphys,
-                   int64_t* colphys, double* pivvals) {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s, k, cand, ncand, st, reltol, abstol,
-                       rowpos, colpos, rowphys, colphys, pivvals);
 }
 
 __global__ void k_init_state(RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
