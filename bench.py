@@ -29,21 +29,25 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def pass_bytes(m, n, r, nb):
-    """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-2, each over the
-    (m-k-1) x (n-k-1) trailing block: a read-only pass reads 8 B/element, every nb-th pass
-    (pending count reaches nb) also writes 8 B/element back. Returns (read_only, write_back)
-    as (bytes, launches)."""
+def pass_bytes(m, n, r, nb, stride=1):
+    """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-1 with k % stride == 0
+    (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block: a read-only pass
+    reads 8 B/element, every nb-th pass (pending count reaches nb; never the last) also writes
+    8 B/element back. Returns (read_only, write_back) as (bytes, launches)."""
     ro_b = wb_b = 0.0
     ro_n = wb_n = 0
     pend = 0
-    for k in range(r - 1):
+    for k in range(r):
         pend += 1
         elems = float(m - k - 1) * float(n - k - 1)
-        if pend >= nb:
+        flush = pend >= nb and k + 1 < r
+        if flush:
+            pend = 0
+        if k % stride:
+            continue
+        if flush:
             wb_b += 16.0 * elems
             wb_n += 1
-            pend = 0
         else:
             ro_b += 8.0 * elems
             ro_n += 1
@@ -63,6 +67,8 @@ def main():
     ap.add_argument("--cpu-pivots", type=int, default=256)
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP events in the timed region (no roofline line)")
+    ap.add_argument("--timing-stride", type=int, default=5,
+                    help="time the rrLU pass of every s-th pivot with HIP events")
     ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "8")),
                     help="deferred-update depth of the rrLU (results are identical for every nb)")
     args = ap.parse_args()
@@ -96,9 +102,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # per-kernel device times: HIP events recorded on the context's stream around every pass
-    # launch inside the timed region (--no-kernel-timing: diagnostic run without them)
-    ctx.set_timing(not args.no_kernel_timing)
+    # per-kernel device times: HIP events recorded on the context's stream around the passes of
+    # every 5th pivot inside the timed region (5 is prime to nb = 8, so both pass kinds and every
+    # pending depth are sampled; an event pair costs ~8 us of stream time, recording all 256 passes
+    # would cost ~6 % of a step). --no-kernel-timing: diagnostic run without them.
+    ctx.set_timing(not args.no_kernel_timing, stride=args.timing_stride)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -119,7 +127,7 @@ def main():
     flops = rrlu_flops(m, n, r)
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
-    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb)
+    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, args.timing_stride)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"

@@ -61,6 +61,8 @@ int tci_ctx_synchronize(tci_ctx* ctx);
  * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
  * 1 = batch evaluation. */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
+/* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
+ * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
 /* Deferred-update depth of the rrLU (1..16; default 8, env TCI_RRLU_NB): up to nb rank-1
  * updates are applied on the fly by read-only passes and written back every nb-th pivot.

@@ -79,6 +79,7 @@ struct tci_ctx {
     // kernel timing (family 0: rrLU pass with write-back, 1: batch evaluation,
     //                2: rrLU read-only pass)
     bool timing = false;
+    int timing_stride = 1;  // rrLU passes: only every timing_stride-th pivot's pass is timed
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
     std::vector<std::pair<int, size_t>> evpairs;  // (family, index of start event)
@@ -143,8 +144,8 @@ int ensure(tci_ctx* c, T** p, size_t* cap, size_t n) {
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
-void ev_begin(tci_ctx* c, int fam) {
-    if (!c->timing) return;
+void ev_begin(tci_ctx* c, int fam, bool sampled = true) {
+    if (!c->timing || !sampled) return;
     if (c->evused + 2 > c->evpool.size()) {
         size_t add = std::max<size_t>(64, c->evpool.size());
         for (size_t i = 0; i < add; ++i) {
@@ -157,8 +158,8 @@ void ev_begin(tci_ctx* c, int fam) {
     hipEventRecord(c->evpool[c->evused], c->stream);
     c->evused += 2;
 }
-void ev_end(tci_ctx* c) {
-    if (!c->timing) return;
+void ev_end(tci_ctx* c, bool sampled = true) {
+    if (!c->timing || !sampled) return;
     hipEventRecord(c->evpool[c->evpairs.back().second + 1], c->stream);
 }
 void ev_reset(tci_ctx* c) {
@@ -270,9 +271,10 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             g.k = (int)kk;
             g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
-            ev_begin(c, flush ? 0 : 2);
+            const bool sampled = kk % c->timing_stride == 0;
+            ev_begin(c, flush ? 0 : 2, sampled);
             tci::launch_pass(c->stream, P, flush, g, grid);
-            ev_end(c);
+            ev_end(c, sampled);
             if (flush) t0 = kk + 1;
         }
         k = kend;
@@ -461,7 +463,8 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
 }
 
 int tci_set_timing(tci_ctx* c, int enabled) {
-    c->timing = enabled != 0;
+    c->timing = enabled > 0;
+    c->timing_stride = enabled > 0 ? enabled : 1;
     ev_reset(c);
     return TCI_OK;
 }

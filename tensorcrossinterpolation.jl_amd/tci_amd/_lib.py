@@ -136,8 +136,9 @@ class Context:
         except Exception:
             pass
 
-    def set_timing(self, on):
-        self.check(self.lib.tci_set_timing(self.h, int(bool(on))))
+    def set_timing(self, on, stride=1):
+        """HIP-event kernel timing on/off; rrLU passes are sampled every `stride`-th pivot."""
+        self.check(self.lib.tci_set_timing(self.h, max(1, int(stride)) if on else 0))
 
     def kernel_stats(self, family):
         ms = C.c_double()
