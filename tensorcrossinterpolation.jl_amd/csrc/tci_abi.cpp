@@ -221,12 +221,16 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
     if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
     if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * n)))) return st;
-    // pending rank-1 updates: X[i * ldx + s] (physical row i, slot s), Y[j * ldy + s]; one extra
-    // row so the 16-B loads of a tile's last odd row stay in bounds
+    // pending rank-1 updates, slot-major: X[s * ldx + i] (slot s, physical row i), Y[s * ldy + j];
+    // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
     const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
-    const int64_t ldx = tci::kMaxPend, ldy = tci::kMaxPend;
-    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)((m + 2) * ldx)))) return st;
-    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)((n + 2) * ldy)))) return st;
+    const int64_t ldx = round_up(m + 2, 16), ldy = round_up(n + 2, 16);
+    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPend * ldx)))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPend * ldy)))) return st;
+    if ((m + tci::kRowsPerTile - 1) / tci::kRowsPerTile > kMaxGrid)
+        return set_err(c, TCI_ERR_ARG, "rrlu: more than " +
+                                           std::to_string((long long)tci::kRowsPerTile * kMaxGrid) +
+                                           " rows is not supported");
     tci::PassArgs g;
     g.A = dA;
     g.lda = lda;

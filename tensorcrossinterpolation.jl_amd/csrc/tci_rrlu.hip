@@ -86,14 +86,20 @@ __device__ __forceinline__ void block_reduce_cand(CandR& c) {
 }
 
 // ------------------------------------------------------------------ pass
-// Runs after pivot k has been selected (k = -1: the initial argmax, no pending update). Tiles
-// cover the physical matrix: 512 rows (256 lanes x double2, 16-B accesses; lda even) x cb
-// columns; elements outside the trailing block are skipped (columns: uniformly; rows: masked).
-// P = pending updates including pivot k's own, which the workgroup derives for its tile:
+// Runs after pivot k has been selected (k = -1: the initial argmax, no pending update). The
+// physical matrix is cut into row tiles of 512 rows (256 lanes x double2, 16-B accesses; lda
+// even) and column tiles of cb columns. Workgroup w owns row tile w % tiles_r and the column
+// tiles q, q + nq, ... (q = w / tiles_r): its rows' pending x's -- and pivot k's x_k, which it derives --
+// stay in registers while it walks the chunk, one column tile (and its y's, staged in LDS) at a
+// time. Elements outside the trailing block are skipped (columns: uniformly; rows: masked).
+// P = pending updates including pivot k's own:
 //   x_k[i] = (stale[i,b] - sum_{s<P-1} x_s[i] y_s[b]) (/ piv if leftorth)
 //   y_k[j] = (stale[a,j] - sum_{s<P-1} x_s[a] y_s[j]) (/ piv otherwise)
-// with (a, b) the pivot's physical row/column. Workgroups of column tile 0 store x_k (pending
-// slot P-1 and L column k), those of row tile 0 store y_k (slot and U row k).
+// with (a, b) the pivot's physical row/column. Pending vectors are slot-major, X[s*ldx + i] and
+// Y[s*ldy + j], so every access to them is coalesced. Workgroups with q = 0 store x_k (slot P-1
+// and L column k), those of row tile 0 store y_k (slot P-1 and U row k).
+// Serpentine: with rev set the bands are walked backwards, so a pass starts on the bytes the
+// previous pass touched last (still in the 256 MiB Infinity Cache).
 //
 // Tail: the workgroups publish their candidates (sc1 stores, then one agent-scope atomic add each;
 // MI355X_MICROARCH.md hand-off table, first row) and the one whose add comes last reduces them and
@@ -142,7 +148,12 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     __shared__ int cpos_s[kMaxCB];
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
-    const int ntiles = tiles_r * tiles_c;
+    const int nq = gridDim.x / tiles_r;  // chunks per row tile (host: gridDim.x = tiles_r * nq)
+    const int tr = blockIdx.x % tiles_r;
+    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    // column tiles q, q + nq, q + 2 nq, ...: at any moment the grid streams one contiguous band
+    // of nq column tiles (spread over every HBM channel), band after band
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
     int a = 0, b = 0;
     double piv = 1.0;
     if (P > 0) {
@@ -150,12 +161,50 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         b = (int)st->q;
         piv = st->pval;
     }
+    // this thread's two rows, their pending x's and x_k
+    const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;
+    const int rp0 = r0 < m ? rowpos[r0] : -1;
+    const int rp1 = r0 + 1 < m ? rowpos[r0 + 1] : -1;
+    const bool in0 = rp0 > k, in1 = rp1 > k;
+    const bool active = in0 || in1;
+    double x0[PP], x1[PP];
+    if (P > 0 && active) {
+        // x's of rows r0, r0 + 1 (ldx >= m + 1, so r0 + 1 is in bounds even past the last row)
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) {
+            const double2 u = *reinterpret_cast<const double2*>(X + (int64_t)s * ldx + r0);
+            x0[s] = u.x;
+            x1[s] = u.y;
+        }
+        const double2 cb2 = *reinterpret_cast<const double2*>(A + r0 + (int64_t)b * lda);
+        double xk0 = cb2.x, xk1 = cb2.y;
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) {
+            const double yv = Y[(int64_t)s * ldy + b];
+            xk0 = __dsub_rn(xk0, __dmul_rn(x0[s], yv));
+            xk1 = __dsub_rn(xk1, __dmul_rn(x1[s], yv));
+        }
+        if (leftorth) {
+            xk0 = xk0 / piv;
+            xk1 = xk1 / piv;
+        }
+        x0[P - 1] = xk0;
+        x1[P - 1] = xk1;
+        if (q == 0) {
+            double* xs = X + (int64_t)(P - 1) * ldx;
+            if (in0) {
+                xs[r0] = xk0;
+                Lp[r0 + (int64_t)k * ldl] = xk0;
+            }
+            if (in1) {
+                xs[r0 + 1] = xk1;
+                Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
+            }
+        }
+    }
     CandR best = cand_none();
-    for (int tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {  // block-uniform tile sequence
-        // serpentine: a reversed pass starts on the tiles the previous pass touched last, which
-        // are still in the 256 MiB Infinity Cache
-        const int t = rev ? ntiles - 1 - tt : tt;
-        const int tr = t % tiles_r, tc = t / tiles_r;
+    for (int it = 0; it < ntc; ++it) {
+        const int tc = q + (rev ? ntc - 1 - it : it) * nq;
         const int j0 = tc * cb;
         const int j1 = min(j0 + cb, n);
         __syncthreads();  // previous tile's readers are done with ys / cpos_s
@@ -164,74 +213,22 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
             const int cp = colpos[j];
             cpos_s[c] = cp;
             if (P > 0 && cp > k) {
-                const double* yj = Y + (int64_t)j * ldy;
-                const double* xa = X + (int64_t)a * ldx;
                 double yk = A[a + (int64_t)j * lda];
                 for (int s = 0; s < P - 1; ++s) {
-                    const double ysv = yj[s];
+                    const double ysv = Y[(int64_t)s * ldy + j];
                     ys[c * PP + s] = ysv;
-                    yk = __dsub_rn(yk, __dmul_rn(xa[s], ysv));
+                    yk = __dsub_rn(yk, __dmul_rn(X[(int64_t)s * ldx + a], ysv));
                 }
                 if (!leftorth) yk = yk / piv;
                 ys[c * PP + P - 1] = yk;
                 if (tr == 0) {
-                    Y[(int64_t)j * ldy + P - 1] = yk;
+                    Y[(int64_t)(P - 1) * ldy + j] = yk;
                     Up[k + (int64_t)j * ldu] = yk;
                 }
             }
         }
         __syncthreads();
-        const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;
-        if (r0 >= m) continue;
-        const bool has1 = r0 + 1 < m;
-        const int rp0 = rowpos[r0];
-        const int rp1 = has1 ? rowpos[r0 + 1] : -1;
-        const bool in0 = rp0 > k, in1 = rp1 > k;
-        if (!(in0 || in1)) continue;
-        double x0[PP], x1[PP];
-        if (P > 0) {
-            const double* xr = X + (int64_t)r0 * ldx;
-#pragma unroll
-            for (int s = 0; s < P - 1; s += 2) {
-                if (s + 1 < P - 1) {
-                    const double2 u = *reinterpret_cast<const double2*>(xr + s);
-                    const double2 w = *reinterpret_cast<const double2*>(xr + ldx + s);
-                    x0[s] = u.x;
-                    x0[s + 1] = u.y;
-                    x1[s] = w.x;
-                    x1[s + 1] = w.y;
-                } else {
-                    x0[s] = xr[s];
-                    x1[s] = xr[ldx + s];
-                }
-            }
-            // x_k for this thread's two rows
-            const double2 cb2 = *reinterpret_cast<const double2*>(A + r0 + (int64_t)b * lda);
-            const double* yb = Y + (int64_t)b * ldy;
-            double xk0 = cb2.x, xk1 = cb2.y;
-#pragma unroll
-            for (int s = 0; s < P - 1; ++s) {
-                const double yv = yb[s];
-                xk0 = __dsub_rn(xk0, __dmul_rn(x0[s], yv));
-                xk1 = __dsub_rn(xk1, __dmul_rn(x1[s], yv));
-            }
-            if (leftorth) {
-                xk0 = xk0 / piv;
-                xk1 = xk1 / piv;
-            }
-            x0[P - 1] = xk0;
-            x1[P - 1] = xk1;
-            if (tc == 0) {
-                if (in0) {
-                    X[(int64_t)r0 * ldx + P - 1] = xk0;
-                    Lp[r0 + (int64_t)k * ldl] = xk0;
-                }
-                if (in1) {
-                    X[(int64_t)(r0 + 1) * ldx + P - 1] = xk1;
-                    Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
-                }
-            }
-        }
+        if (!active) continue;
         // one column: apply the P pending updates in order (rows outside the block keep their
         // value), write back if FLUSH, fold both rows into the running candidate
         auto column = [&](double2 v, int c, double2* pa) {
@@ -304,13 +301,16 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     }
 }
 
+// tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
+// column tiles (at least one; the host rejects tiles_r > kMaxPassGrid).
 int argmax_grid(int m, int n, int k, int cb, int max_grid) {
     (void)k;
-    const long long tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
-    const long long tiles_c = (n + cb - 1) / cb;
-    long long nt = tiles_r * tiles_c;
-    if (nt < 1) nt = 1;
-    return (int)(nt < max_grid ? nt : max_grid);
+    const long long tiles_r = m > 0 ? (m + kRowsPerTile - 1) / kRowsPerTile : 1;
+    const long long tiles_c = n > 0 ? (n + cb - 1) / cb : 1;
+    long long nq = max_grid / tiles_r;
+    if (nq > tiles_c) nq = tiles_c;
+    if (nq < 1) nq = 1;
+    return (int)(tiles_r * nq);
 }
 
 template <int P>
