@@ -69,7 +69,7 @@ def main():
                     help="diagnostic: no HIP events in the timed region (no roofline line)")
     ap.add_argument("--timing-stride", type=int, default=5,
                     help="time the rrLU pass of every s-th pivot with HIP events")
-    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "8")),
+    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "10")),
                     help="deferred-update depth of the rrLU (results are identical for every nb)")
     args = ap.parse_args()
 
@@ -103,10 +103,14 @@ def main():
             dist.barrier()
 
     # per-kernel device times: HIP events recorded on the context's stream around the passes of
-    # every 5th pivot inside the timed region (5 is prime to nb = 8, so both pass kinds and every
+    # every s-th pivot inside the timed region (s >= 5 prime to nb, so both pass kinds and every
     # pending depth are sampled; an event pair costs ~8 us of stream time, recording all 256 passes
     # would cost ~6 % of a step). --no-kernel-timing: diagnostic run without them.
-    ctx.set_timing(not args.no_kernel_timing, stride=args.timing_stride)
+    import math
+    stride = args.timing_stride
+    while math.gcd(stride, args.nb) != 1:  # sample every pending depth, both pass kinds
+        stride += 1
+    ctx.set_timing(not args.no_kernel_timing, stride=stride)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -127,7 +131,7 @@ def main():
     flops = rrlu_flops(m, n, r)
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
-    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, args.timing_stride)
+    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"

@@ -64,7 +64,7 @@ int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* l
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
-/* Deferred-update depth of the rrLU (1..16; default 8, env TCI_RRLU_NB): up to nb rank-1
+/* Deferred-update depth of the rrLU (1..16; default 10, env TCI_RRLU_NB): up to nb rank-1
  * updates are applied on the fly by read-only passes and written back every nb-th pivot.
  * Results are bitwise identical for every nb. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
@@ -90,8 +90,10 @@ int tci_batcheval_d(tci_ctx* ctx, const tci_func* f, const int32_t* I, int64_t m
 
 /* ------------------------------------------------------------------ rrLU
  * Replaces rrlu / rrlu! / _optimizerrlu! (matrixlu.jl:346-463) with identical arithmetic: full
- * pivoting by abs2 argmax (ties -> smallest column, then row; matrixlu.jl:46-87), physical row and
- * column swaps, true-division normalisation and separate multiply/subtract rank-1 updates.
+ * pivoting by abs2 argmax (ties -> smallest column, then row; matrixlu.jl:46-87), the row and
+ * column swaps of addpivot! (kept as position maps: the matrix itself never moves),
+ * true-division normalisation and separate multiply/subtract rank-1 updates (deferred up to nb
+ * pivots, applied on the fly in the reference's order: bitwise the same values).
  * Outputs mirror the rrLU struct (matrixlu.jl:200-207):
  *   rowperm[m], colperm[n]  (1-based),  L: m x maxrank (ld m), U: maxrank x n (ld ldu >= maxrank),
  *   only the first *npivot columns of L / rows of U are meaningful; *lasterror = lu.error.
@@ -99,9 +101,10 @@ int tci_batcheval_d(tci_ctx* ctx, const tci_func* f, const int32_t* I, int64_t m
 int tci_rrlu_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
                double reltol, double abstol, int leftorth, int64_t* rowperm, int64_t* colperm,
                double* L, double* U, int64_t ldu, int64_t* npivot, double* lasterror);
-/* rrlu! on a device matrix: factorises d_A (column-major, ld lda; lda even) IN PLACE and leaves
- * the packed factors there (L below the diagonal, U on/above it, like the reference's A after
- * _optimizerrlu!). Permutations are returned to the host. */
+/* rrlu! on a device matrix: factorises d_A (column-major, ld lda; lda even) using it as the work
+ * matrix -- its contents are clobbered (stale trailing values), as the reference's A is after
+ * _optimizerrlu! -- and returns to the host the permutations (NULL to skip), npivot, lu.error and
+ * the np + 1 pivot errors (matrixlu.jl:799; NULL to skip). L and U stay in the context. */
 int tci_rrlu_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
                        int64_t maxrank, double reltol, double abstol, int leftorth,
                        int64_t* rowperm, int64_t* colperm, int64_t* npivot, double* lasterror,

@@ -10,6 +10,7 @@ constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at mo
 constexpr int kUpdThreads = 256;   // rrLU pass: 4 waves
 constexpr int kRowsPerTile = 512;  // 256 lanes x double2
 constexpr int kMaxCB = 16;         // rrLU pass: at most this many columns per tile (measured best)
+constexpr int kStageCols = 256;    // rrLU pass: columns whose y's a workgroup stages at once
 constexpr int kMaxPassGrid = 2048; // rrLU pass: at most this many workgroups (8 per CU)
 
 // Argmax candidate: abs2 value, the (current, pending-updated) value itself, its column and row

@@ -30,6 +30,13 @@
 
 #include "tci_internal.h"
 
+#ifndef TCI_PASS_U
+#define TCI_PASS_U 4  // columns per lane whose 16-B loads are in flight together (measured)
+#endif
+#ifndef TCI_FLUSH_NT
+#define TCI_FLUSH_NT 0  // write-back pass stores non-temporal
+#endif
+
 namespace tci {
 
 static constexpr int32_t kBig = 0x7fffffff;
@@ -142,10 +149,11 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
     if (st->done) return;
-    constexpr int U = 8;  // columns whose loads are in flight together
+    constexpr int U = TCI_PASS_U;  // columns whose loads are in flight together
     constexpr int PP = P > 0 ? P : 1;
-    __shared__ double ys[kMaxCB * PP];  // the tile's y_s, [column][slot]; slot P-1 = y_k
-    __shared__ int cpos_s[kMaxCB];
+    // y_s of up to kStageCols of the workgroup's columns, [local column][slot]; slot P-1 = y_k
+    __shared__ double ys[kStageCols * PP];
+    __shared__ int cpos_s[kStageCols];
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
     const int nq = gridDim.x / tiles_r;  // chunks per row tile (host: gridDim.x = tiles_r * nq)
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     const bool in0 = rp0 > k, in1 = rp1 > k;
     const bool active = in0 || in1;
     double x0[PP], x1[PP];
-    if (P > 0 && active) {
+    if constexpr (P > 0) if (active) {
         // x's of rows r0, r0 + 1 (ldx >= m + 1, so r0 + 1 is in bounds even past the last row)
 #pragma unroll
         for (int s = 0; s < P - 1; ++s) {
@@ -203,24 +211,30 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         }
     }
     CandR best = cand_none();
-    for (int it = 0; it < ntc; ++it) {
-        const int tc = q + (rev ? ntc - 1 - it : it) * nq;
-        const int j0 = tc * cb;
-        const int j1 = min(j0 + cb, n);
-        __syncthreads();  // previous tile's readers are done with ys / cpos_s
-        for (int c = threadIdx.x; c < j1 - j0; c += kUpdThreads) {
-            const int j = j0 + c;
+    // staging groups: the y's of G column tiles are staged at once (one barrier pair per group,
+    // usually one group per pass), then the group's tiles stream without barriers
+    const int G = kStageCols / cb;
+    for (int g0 = 0; g0 < ntc; g0 += G) {
+        const int gn = min(G, ntc - g0);
+        __syncthreads();  // previous group's readers are done with ys / cpos_s
+        for (int lc = threadIdx.x; lc < gn * cb; lc += kUpdThreads) {
+            const int it = g0 + lc / cb;
+            const int j = (q + (rev ? ntc - 1 - it : it) * nq) * cb + lc % cb;
+            if (j >= n) {
+                cpos_s[lc] = -1;  // past the last column: skipped like a pivoted one
+                continue;
+            }
             const int cp = colpos[j];
-            cpos_s[c] = cp;
+            cpos_s[lc] = cp;
             if (P > 0 && cp > k) {
                 double yk = A[a + (int64_t)j * lda];
                 for (int s = 0; s < P - 1; ++s) {
                     const double ysv = Y[(int64_t)s * ldy + j];
-                    ys[c * PP + s] = ysv;
+                    ys[lc * PP + s] = ysv;
                     yk = __dsub_rn(yk, __dmul_rn(X[(int64_t)s * ldx + a], ysv));
                 }
                 if (!leftorth) yk = yk / piv;
-                ys[c * PP + P - 1] = yk;
+                ys[lc * PP + P - 1] = yk;
                 if (tr == 0) {
                     Y[(int64_t)(P - 1) * ldy + j] = yk;
                     Up[k + (int64_t)j * ldu] = yk;
@@ -229,44 +243,58 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         }
         __syncthreads();
         if (!active) continue;
-        // one column: apply the P pending updates in order (rows outside the block keep their
-        // value), write back if FLUSH, fold both rows into the running candidate
-        auto column = [&](double2 v, int c, double2* pa) {
-            const int cp = cpos_s[c];
-            if (cp <= k) return;  // column already pivoted: not in the trailing block
-            double u0 = v.x, u1 = v.y;
+        for (int it = g0; it < g0 + gn; ++it) {
+            const int tc = q + (rev ? ntc - 1 - it : it) * nq;
+            const int j0 = tc * cb;
+            const int j1 = min(j0 + cb, n);
+            const int l0 = (it - g0) * cb;  // local column index of j0
+            // one column: apply the P pending updates in order (rows outside the block keep their
+            // value), write back if FLUSH, fold both rows into the running candidate
+            auto column = [&](double2 v, int c, double2* pa) {
+                const int cp = cpos_s[l0 + c];
+                if (cp <= k) return;  // column already pivoted: not in the trailing block
+                double u0 = v.x, u1 = v.y;
 #pragma unroll
-            for (int s = 0; s < P; ++s) {
-                const double y = ys[c * PP + s];
-                u0 = __dsub_rn(u0, __dmul_rn(x0[s], y));
-                u1 = __dsub_rn(u1, __dmul_rn(x1[s], y));
+                for (int s = 0; s < P; ++s) {
+                    const double y = ys[(l0 + c) * PP + s];
+                    u0 = __dsub_rn(u0, __dmul_rn(x0[s], y));
+                    u1 = __dsub_rn(u1, __dmul_rn(x1[s], y));
+                }
+                v.x = in0 ? u0 : v.x;
+                v.y = in1 ? u1 : v.y;
+                if (FLUSH) {
+                    if (TCI_FLUSH_NT) {
+                        typedef double dv2 __attribute__((ext_vector_type(2)));
+                        dv2 w = {v.x, v.y};
+                        __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
+                    } else {
+                        *pa = v;
+                    }
+                }
+                // the full (value, column, row) comparison only matters when v >= best.v, which is
+                // rare once a large value has been seen: test that first (NaN fails it, as it should)
+                const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
+                if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                    const int j = j0 + c;
+                    if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
+                    if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
+                }
+            };
+            double* base = A + r0;
+            int c = 0;
+            for (; c + U <= j1 - j0; c += U) {
+                double2 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    v[u] = *reinterpret_cast<const double2*>(base + (int64_t)(j0 + c + u) * lda);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    column(v[u], c + u, reinterpret_cast<double2*>(base + (int64_t)(j0 + c + u) * lda));
             }
-            v.x = in0 ? u0 : v.x;
-            v.y = in1 ? u1 : v.y;
-            if (FLUSH) *pa = v;
-            // the full (value, column, row) comparison only matters when v >= best.v, which is
-            // rare once a large value has been seen: test that first (NaN fails it, as it should)
-            const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
-            if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
-                const int j = j0 + c;
-                if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
-                if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
+            for (; c < j1 - j0; ++c) {
+                double2* pa = reinterpret_cast<double2*>(base + (int64_t)(j0 + c) * lda);
+                column(*pa, c, pa);
             }
-        };
-        double* base = A + r0;
-        int c = 0;
-        for (; c + U <= j1 - j0; c += U) {
-            double2 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                v[u] = *reinterpret_cast<const double2*>(base + (int64_t)(j0 + c + u) * lda);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                column(v[u], c + u, reinterpret_cast<double2*>(base + (int64_t)(j0 + c + u) * lda));
-        }
-        for (; c < j1 - j0; ++c) {
-            double2* pa = reinterpret_cast<double2*>(base + (int64_t)(j0 + c) * lda);
-            column(*pa, c, pa);
         }
     }
     block_reduce_cand<kUpdThreads>(best);
