@@ -68,6 +68,10 @@ int tci_set_timing(tci_ctx* ctx, int enabled);
  * updates are applied on the fly by read-only passes and written back every nb-th pivot.
  * Results are bitwise identical for every nb. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
+/* Matrices with m*n <= 16384 and m + n <= 4096 are factorised by one workgroup holding the whole
+ * matrix in LDS (one launch instead of one per pivot); enabled = 0 forces the pass pipeline.
+ * Both paths give bitwise identical results. Default on (env TCI_RRLU_SMALL=0: off). */
+int tci_set_rrlu_small(tci_ctx* ctx, int enabled);
 
 /* ------------------------------------------------------------ integrands */
 /* Uploads an integrand's parameters to the device once; localdims has L entries. */

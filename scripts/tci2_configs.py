@@ -1,0 +1,64 @@
+"""TCI2 sweeps of the BASELINE configs on the GPU path: wall time, ranks, errors.
+
+  python scripts/tci2_configs.py [names...]     (default: all)
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tensorcrossinterpolation.jl_amd"))
+
+import numpy as np  # noqa: E402
+
+import tci_amd as T  # noqa: E402
+
+
+def run(name, f, localdims, initialpivots=None, **kw):
+    T.crossinterpolate2(f, localdims, initialpivots, **dict(kw, maxiter=1))  # warm the kernels
+    t0 = time.perf_counter()
+    tci, ranks, errors = T.crossinterpolate2(f, localdims, initialpivots, **kw)
+    wall = time.perf_counter() - t0
+    return {"config": name, "wall_s": round(wall, 4), "iterations": len(ranks),
+            "ranks": ranks, "final_error": errors[-1], "linkdims": tci.linkdims(),
+            "kwargs": {k: v for k, v in kw.items() if k != "rng"}}
+
+
+def configs():
+    out = {}
+    out["C1_lorentz8d_parity"] = lambda: run("C1 8d Lorentzian d=10 tol=1e-8 (nsearchglobalpivot=0)",
+                                             T.lorentz([10] * 8), [10] * 8, tolerance=1e-8,
+                                             nsearchglobalpivot=0)
+    out["C1_lorentz8d_default"] = lambda: run("C1 8d Lorentzian d=10 tol=1e-8 (default global search)",
+                                              T.lorentz([10] * 8), [10] * 8, tolerance=1e-8,
+                                              rng=np.random.default_rng(0))
+    out["C3_gauss20d"] = lambda: run("C3 20d separable Gaussian d=16 tol=1e-10 maxbonddim=512",
+                                     T.gauss([16] * 20, 0.05, 8.5), [16] * 20, [[8] * 20],
+                                     tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0)
+
+    def gaussmix():
+        rng = np.random.default_rng(3)
+        K = 64
+        centres = rng.uniform(1, 16, (K, 20))
+        f = T.gaussmix([16] * 20, 0.05, centres, np.ones(K))
+        p0 = T.optfirstpivot(f, [16] * 20, [int(round(c)) for c in centres[0]])
+        return run("C3' 20d sum of 64 Gaussians d=16 tol=1e-10 maxbonddim=512", f, [16] * 20, [p0],
+                   tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0)
+    out["C3_gaussmix20d"] = gaussmix
+
+    def qosc():
+        f = T.quantics_osc(40)
+        p0 = T.optfirstpivot(f, [2] * 40)
+        return run("C4 quantics exp(-10x) sin(2pi 100 x^1.1), 40 legs d=2 tol=1e-8", f, [2] * 40, [p0],
+                   tolerance=1e-8, nsearchglobalpivot=0)
+    out["C4_qosc40"] = qosc
+    return out
+
+
+if __name__ == "__main__":
+    cs = configs()
+    names = sys.argv[1:] or list(cs)
+    for nm in names:
+        res = cs[nm]()
+        print(json.dumps(res), flush=True)

@@ -40,8 +40,16 @@ struct tci_ctx {
     int flush_every = 10;  // deferred-update depth nb (1 = write back every pivot; 10 measured best)
     int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
+    int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int* flag = nullptr;
     unsigned* ticket = nullptr;  // rrLU pass tail hand-off counter (zero between passes)
+    char* hin = nullptr;         // pinned staging for uploads / downloads of the small path
+    size_t capHin = 0;
+    char* hout = nullptr;
+    size_t capHout = 0;
+    char* zbuf = nullptr;  // mapped pinned host memory the small path's kernels write into
+    char* zdev = nullptr;  // its device address
+    size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     unsigned long long* maxbits = nullptr;
     unsigned long long* hmaxbits = nullptr;  // pinned
@@ -51,6 +59,8 @@ struct tci_ctx {
     size_t capI = 0;
     int32_t* dJ = nullptr;
     size_t capJ = 0;
+    int32_t* dI2 = nullptr;
+    size_t capI2 = 0;
     double* dF1 = nullptr;  // factor / auxiliary buffers
     size_t capF1 = 0;
     double* dF2 = nullptr;
@@ -144,6 +154,46 @@ int ensure(tci_ctx* c, T** p, size_t* cap, size_t n) {
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+// mapped pinned host buffer (zero-copy results of the small path; the stream is idle whenever it
+// is reallocated)
+int ensure_mapped(tci_ctx* c, size_t bytes) {
+    if (bytes <= c->capZ && c->zbuf) return TCI_OK;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    if (c->zbuf) {
+        hipStreamSynchronize(c->stream);
+        hipHostFree(c->zbuf);
+        c->zbuf = c->zdev = nullptr;
+        c->capZ = 0;
+    }
+    if (hipHostMalloc((void**)&c->zbuf, want, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->zdev, c->zbuf, 0) != hipSuccess) {
+        c->zbuf = c->zdev = nullptr;
+        return set_err(c, TCI_ERR_NOMEM, "mapped host allocation of " + std::to_string(want) +
+                                             " bytes failed");
+    }
+    c->capZ = want;
+    return TCI_OK;
+}
+
+// pinned host staging buffer (grown on demand; the stream is idle whenever it is reallocated)
+int ensure_pinned(tci_ctx* c, char** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap && *p) return TCI_OK;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    if (*p) {
+        hipStreamSynchronize(c->stream);
+        hipHostFree(*p);
+        *p = nullptr;
+        *cap = 0;
+    }
+    if (hipHostMalloc((void**)p, want, 0) != hipSuccess) {
+        *p = nullptr;
+        return set_err(c, TCI_ERR_NOMEM, "pinned host allocation of " + std::to_string(want) +
+                                             " bytes failed");
+    }
+    *cap = want;
+    return TCI_OK;
+}
+
 void ev_begin(tci_ctx* c, int fam, bool sampled = true) {
     if (!c->timing || !sampled) return;
     if (c->evused + 2 > c->evpool.size()) {
@@ -221,6 +271,17 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
     if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
     if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * n)))) return st;
+    if (c->small_path && tci::rrlu_small_fits(m, n)) {
+        // the whole factorisation in one workgroup's LDS: one launch instead of one per pivot
+        HIPCHK(c, tci::launch_rrlu_small(c->stream, dA, lda, mi, ni, (int)mr, reltol, abstol,
+                                         leftorth, c->st, c->rowperm, c->colperm, c->pivv, c->Lp, m,
+                                         c->Up, c->ldUp, tci::SmallOut{nullptr, nullptr, nullptr}));
+        HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *np_out = c->hst->np;
+        *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;  // matrixlu.jl:391-393
+        return TCI_OK;
+    }
     // pending rank-1 updates, slot-major: X[s * ldx + i] (slot s, physical row i), Y[s * ldy + j];
     // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
     const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
@@ -367,9 +428,9 @@ int upload_index(tci_ctx* c, int32_t** d, size_t* cap, const int32_t* h, int64_t
 }
 
 // batch evaluation into a device buffer (column-major, ld ldo). *maxabs = max|out|.
-int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
-                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo,
-                     double* maxabs) {
+// batch evaluation launches only (no synchronisation); c->maxbits receives max|out| bits
+int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
+                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo) {
     if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
     if (M < 0 || M > 1) return set_err(c, TCI_ERR_ARG, "only M = 0 or M = 1 centre legs are supported");
     const int D = M ? f->localdims[nl] : 1;
@@ -386,6 +447,14 @@ int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
         ev_end(c);
         HIPCHK(c, hipGetLastError());
     }
+    return TCI_OK;
+}
+
+int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
+                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo,
+                     double* maxabs) {
+    int st;
+    if ((st = batcheval_launch(c, f, dI, m, nl, dJ, n, nr, M, dout, ldo))) return st;
     HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -414,6 +483,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -441,12 +511,15 @@ int tci_ctx_destroy(tci_ctx* c) {
     auto fr = [](void* p) { if (p) hipFree(p); };
     fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
     fr(c->ticket);
-    fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
+    fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
     fr(c->dU);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
+    if (c->hin) hipHostFree(c->hin);
+    if (c->hout) hipHostFree(c->hout);
+    if (c->zbuf) hipHostFree(c->zbuf);
     for (auto e : c->evpool) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -463,6 +536,11 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
     if (nb < 1 || nb > tci::kMaxPend)
         return set_err(c, TCI_ERR_ARG, "flush interval must be in 1.." + std::to_string(tci::kMaxPend));
     c->flush_every = nb;
+    return TCI_OK;
+}
+
+int tci_set_rrlu_small(tci_ctx* c, int enabled) {
+    c->small_path = enabled != 0;
     return TCI_OK;
 }
 
@@ -626,6 +704,77 @@ int tci_luci_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
     return luci_outputs(c, m, n, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
 }
 
+// The 2-site update of a small Pi (rrlu_small_fits) with one host synchronisation and no
+// device-to-host copies: index tables up by one copy from mapped host memory, Pi + maxabs, then
+// one workgroup doing rrLU, NaN checks and the MatrixLUCI factors from LDS and writing every
+// result straight into the mapped host buffer.
+static int update_pivots_small(tci_ctx* c, const tci_func* f, const int32_t* rows, int64_t m,
+                               int32_t nl, const int32_t* cols, int64_t n, int32_t nr,
+                               int64_t maxrank, double reltol, double abstol, int leftorth,
+                               int want_factors, int64_t* rowidx, int64_t* colidx,
+                               double* pivoterrs, int64_t* npivot, double* maxabs, double* left,
+                               double* right) {
+    const int64_t mr = std::min<int64_t>(maxrank, std::min(m, n));
+    const int64_t ld = round_up(m, 16);
+    const bool wl = want_factors && left, wr = want_factors && right;
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(ld * n)))) return st;
+    if ((st = ensure(c, &c->dI, &c->capI, (size_t)(m * nl + n * nr + 8)))) return st;
+    // mapped host buffer: rows | cols (uploaded by one copy) | state | flag | maxbits |
+    // rowphys[m] | colphys[n] | pivv[mr] | left[m * mr] | right[mr * n] (written by the kernel)
+    size_t off[10];
+    off[0] = 0;
+    off[1] = off[0] + (size_t)round_up((m * nl + n * nr) * 4, 16);
+    off[2] = off[1] + (size_t)round_up(sizeof(RrluState), 16);
+    off[3] = off[2] + 16;
+    off[4] = off[3] + 16;
+    off[5] = off[4] + (size_t)round_up(m * 8, 16);
+    off[6] = off[5] + (size_t)round_up(n * 8, 16);
+    off[7] = off[6] + (size_t)round_up(mr * 8, 16);
+    off[8] = off[7] + (wl ? (size_t)(m * mr * 8) : 0);
+    off[9] = off[8] + (wr ? (size_t)(mr * n * 8) : 0);
+    if ((st = ensure_mapped(c, off[9]))) return st;
+    char* h = c->zbuf;
+    char* d = c->zdev;
+    const size_t bi = (size_t)(m * nl) * 4, bj = (size_t)(n * nr) * 4;
+    if (bi) memcpy(h, rows, bi);
+    if (bj) memcpy(h + bi, cols, bj);
+    if (bi + bj) HIPCHK(c, hipMemcpyAsync(c->dI, d, bi + bj, hipMemcpyHostToDevice, c->stream));
+    if ((st = batcheval_launch(c, f, c->dI, m, nl, c->dI + m * nl, n, nr, 0, c->dA, ld))) return st;
+    c->ldUp = std::max<int64_t>(mr, 1);
+    tci::SmallOut out{wl ? reinterpret_cast<double*>(d + off[7]) : nullptr,
+                      wr ? reinterpret_cast<double*>(d + off[8]) : nullptr,
+                      reinterpret_cast<int*>(d + off[2]), c->maxbits,
+                      reinterpret_cast<unsigned long long*>(d + off[3])};
+    HIPCHK(c, tci::launch_rrlu_small(c->stream, c->dA, ld, (int)m, (int)n, (int)mr, reltol, abstol,
+                                     leftorth, reinterpret_cast<RrluState*>(d + off[1]),
+                                     reinterpret_cast<int64_t*>(d + off[4]),
+                                     reinterpret_cast<int64_t*>(d + off[5]),
+                                     reinterpret_cast<double*>(d + off[6]), nullptr, m, nullptr,
+                                     c->ldUp, out));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const RrluState* hs = reinterpret_cast<const RrluState*>(h + off[1]);
+    const int64_t np = hs->np;
+    const double err = np >= std::min(m, n) ? 0.0 : hs->error;  // matrixlu.jl:391-393
+    if (maxabs) memcpy(maxabs, h + off[3], sizeof(double));
+    *npivot = np;
+    const int fl = *reinterpret_cast<const int*>(h + off[2]);
+    if (fl & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+    if (fl & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    const int64_t* rp = reinterpret_cast<const int64_t*>(h + off[4]);
+    const int64_t* cp = reinterpret_cast<const int64_t*>(h + off[5]);
+    const double* pv = reinterpret_cast<const double*>(h + off[6]);
+    for (int64_t t = 0; t < np; ++t) {
+        if (rowidx) rowidx[t] = rp[t] + 1;
+        if (colidx) colidx[t] = cp[t] + 1;
+        if (pivoterrs) pivoterrs[t] = std::fabs(pv[t]);
+    }
+    if (pivoterrs) pivoterrs[np] = err;
+    if (wl && np > 0) memcpy(left, h + off[7], (size_t)(m * np * 8));
+    if (wr && np > 0) memcpy(right, h + off[8], (size_t)(np * n * 8));
+    return TCI_OK;
+}
+
 int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int64_t m, int32_t nl,
                         const int32_t* cols, int64_t n, int32_t nr, int64_t maxrank, double reltol,
                         double abstol, int leftorth, int want_factors, int64_t* rowidx,
@@ -633,6 +782,10 @@ int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int6
                         double* left, double* right) {
     if (!c || !f || !npivot) return TCI_ERR_ARG;
     if (nl + nr != f->L) return set_err(c, TCI_ERR_ARG, "rows/cols widths must add up to L");
+    if (c->small_path && tci::rrlu_small_fits(m, n) && maxrank > 0)
+        return update_pivots_small(c, f, rows, m, nl, cols, n, nr, maxrank, reltol, abstol, leftorth,
+                                   want_factors, rowidx, colidx, pivoterrs, npivot, maxabs, left,
+                                   right);
     const int64_t ld = round_up(std::max<int64_t>(m, 1), 16);
     int st;
     if ((st = ensure(c, &c->dA, &c->capA, (size_t)(ld * std::max<int64_t>(n, 1))))) return st;
@@ -656,33 +809,50 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
     const int64_t d = f->localdims[wI];
     const int64_t R = nIb * d;
     const int64_t ldR = std::max<int64_t>(R, 1);
+    if (Inext && nInext != nJb) return set_err(c, TCI_ERR_NONSQ, "Pivot matrix is not square!");
+    const int64_t r = nJb;
     int st;
     if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(ldR * std::max<int64_t>(nJb, 1))))) return st;
-    if ((st = upload_index(c, &c->dI, &c->capI, Ib, nIb, wI))) return st;
-    if ((st = upload_index(c, &c->dJ, &c->capJ, Jb, nJb, wJ))) return st;
-    if ((st = batcheval_device(c, f, c->dI, nIb, wI, c->dJ, nJb, wJ, 1, c->dF1, ldR, maxabs)))
-        return st;
-    if (!Inext) {
-        if (R * nJb > 0)
-            HIPCHK(c, hipMemcpyAsync(T, c->dF1, R * nJb * sizeof(double), hipMemcpyDeviceToHost,
-                                     c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        return TCI_OK;
+    if ((st = ensure(c, &c->dI, &c->capI, (size_t)std::max<int64_t>(nIb * wI, 1)))) return st;
+    if ((st = ensure(c, &c->dJ, &c->capJ, (size_t)std::max<int64_t>(nJb * wJ, 1)))) return st;
+    // index tables up through one pinned stage: Ib | Jb | Inext
+    const size_t bi = (size_t)(nIb * wI) * 4, bj = (size_t)(nJb * wJ) * 4;
+    const size_t bn = Inext ? (size_t)(nInext * (wI + 1)) * 4 : 0;
+    if ((st = ensure_pinned(c, &c->hin, &c->capHin, bi + bj + bn + 16))) return st;
+    if (bi) memcpy(c->hin, Ib, bi);
+    if (bj) memcpy(c->hin + bi, Jb, bj);
+    if (bn) memcpy(c->hin + bi + bj, Inext, bn);
+    if (bi) HIPCHK(c, hipMemcpyAsync(c->dI, c->hin, bi, hipMemcpyHostToDevice, c->stream));
+    if (bj) HIPCHK(c, hipMemcpyAsync(c->dJ, c->hin + bi, bj, hipMemcpyHostToDevice, c->stream));
+    const bool solve = Inext && r > 0 && R > 0;
+    if (solve) {
+        // P = f(Inext x Jb) (r x r) into dF2 first: maxabs is Pi1's alone (updatemaxsample!(tci,
+        // Pi1), tensorci2.jl:609), and each evaluation resets c->maxbits
+        if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
+        if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
+        if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+        if ((st = ensure(c, &c->dI2, &c->capI2, (size_t)std::max<int64_t>(nInext * (wI + 1), 1))))
+            return st;
+        if (bn)
+            HIPCHK(c, hipMemcpyAsync(c->dI2, c->hin + bi + bj, bn, hipMemcpyHostToDevice, c->stream));
+        if ((st = batcheval_launch(c, f, c->dI2, nInext, wI + 1, c->dJ, nJb, wJ, 0, c->dF2, r)))
+            return st;
     }
-    if (nInext != nJb) return set_err(c, TCI_ERR_NONSQ, "Pivot matrix is not square!");
-    const int64_t r = nJb;
-    if (r == 0 || R == 0) return TCI_OK;
-    // P = f(Inext x Jb) (r x r) into dF2; T into dA
-    if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
-    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
-    if ((st = upload_index(c, &c->dI, &c->capI, Inext, nInext, wI + 1))) return st;
-    if ((st = batcheval_device(c, f, c->dI, nInext, wI + 1, c->dJ, nJb, wJ, 0, c->dF2, r, nullptr)))
-        return st;
-    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if ((st = batcheval_launch(c, f, c->dI, nIb, wI, c->dJ, nJb, wJ, 1, c->dF1, ldR))) return st;
+    if (solve) {
+        tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
+        HIPCHK(c, hipGetLastError());
+    }
+    // T (and maxabs) down through one pinned stage
+    const size_t bt = (size_t)(R * nJb) * 8;
+    if ((st = ensure_pinned(c, &c->hout, &c->capHout, bt + 16))) return st;
+    HIPCHK(c, hipMemcpyAsync(c->hout, c->maxbits, 8, hipMemcpyDeviceToHost, c->stream));
+    if (bt && (solve || !Inext))
+        HIPCHK(c, hipMemcpyAsync(c->hout + 16, solve ? c->dA : c->dF1, bt, hipMemcpyDeviceToHost,
+                                 c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (maxabs) memcpy(maxabs, c->hout, 8);
+    if (bt && (solve || !Inext)) memcpy(T, c->hout + 16, bt);
     return TCI_OK;
 }
 

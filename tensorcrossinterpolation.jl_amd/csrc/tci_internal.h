@@ -97,6 +97,23 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid);
 void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
+// small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:
+// st, rowphys/colphys, pivvals, Lp (ld ldl, physical rows), Up (ld ldu, physical columns))
+// Optionally also the NaN flags (*flag = 1: L, 2: U), the MatrixLUCI factors in their final
+// layouts (left m x np, ld m; right np x n, ld np) and a copy of *maxin in *maxout. Null = skip.
+// Any of them (and st, rowphys, colphys, pivvals) may point into mapped pinned host memory.
+struct SmallOut {
+    double* left;
+    double* right;
+    int* flag;
+    const unsigned long long* maxin;
+    unsigned long long* maxout;
+};
+bool rrlu_small_fits(int64_t m, int64_t n);
+hipError_t launch_rrlu_small(hipStream_t s, const double* A, int64_t lda, int m, int n, int mr,
+                             double reltol, double abstol, int leftorth, RrluState* st,
+                             int64_t* rowphys, int64_t* colphys, double* pivvals, double* Lp,
+                             int64_t ldl, double* Up, int64_t ldu, SmallOut out);
 // L (m x np, ld ldl) / U (np x n, ld ldu) in position order from the physical-order factors;
 // either output may be null (NaN check only). flag |= 1 (NaN in L), 2 (NaN in U).
 void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double* Up, int64_t ldup,

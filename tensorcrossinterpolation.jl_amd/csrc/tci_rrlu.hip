@@ -445,6 +445,240 @@ void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* r
                        colphys, n);
 }
 
+// ------------------------------------------------------------ small rrLU
+// Pi matrices of a TCI2 sweep at low rank are small (C1: ~120 x 120); there the per-pivot launch
+// latency of the pass pipeline dominates. One 1024-thread workgroup holds the whole matrix in
+// LDS and runs _optimizerrlu! (matrixlu.jl:346-369) as written: argmax over the trailing block
+// (column-major scan order as the tie-break), stop test, swaprow!/swapcol! (physical, in LDS),
+// true-division normalisation and the rank-1 update with separate multiply and subtract.
+constexpr int kSmallThreads = 1024;
+constexpr int64_t kSmallElems = 16384;  // 128 KiB of fp64 in LDS
+constexpr int64_t kSmallPerm = 2048;    // m + n
+
+bool rrlu_small_fits(int64_t m, int64_t n) {
+    return m > 0 && n > 0 && m * n <= kSmallElems && m + n <= kSmallPerm;
+}
+
+static size_t small_lds_bytes(int m, int n) {
+    const size_t a = ((size_t)m * n * sizeof(double) + 15) / 16 * 16;
+    const size_t p = ((size_t)(m + n) * sizeof(int) + 15) / 16 * 16;
+    return a + p + (kSmallThreads / 64) * sizeof(CandR) + 32 + (size_t)(m + n) * sizeof(double);
+}
+
+__global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
+    const double* __restrict__ A, int64_t lda, int m, int n, int mr, double reltol, double abstol,
+    int leftorth, RrluState* st, int64_t* rowphys, int64_t* colphys, double* pivvals,
+    double* Lp, int64_t ldl, double* Up, int64_t ldu, SmallOut out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* S = reinterpret_cast<double*>(smem);  // m x n, ld m
+    int* rp = reinterpret_cast<int*>(smem + ((size_t)m * n * sizeof(double) + 15) / 16 * 16);
+    int* cp = rp + m;
+    CandR* red = reinterpret_cast<CandR*>(reinterpret_cast<char*>(rp) +
+                                          ((size_t)(m + n) * sizeof(int) + 15) / 16 * 16);
+    int* ctl = reinterpret_cast<int*>(red + kSmallThreads / 64);  // [3] np, [4] NaN flags
+    double* xv = reinterpret_cast<double*>(ctl + 8);  // column k (normalised if leftorth)
+    double* yv = xv + m;                             // row k (normalised otherwise)
+    // thread (w, l) owns rows l, l + 64, ... of columns w, w + 16, ...: no index division
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    constexpr int NW = kSmallThreads / 64;
+    for (int j = w; j < n; j += NW)
+        for (int i = l; i < m; i += 64) S[i + j * m] = A[i + (int64_t)j * lda];
+    for (int i = tid; i < m; i += kSmallThreads) rp[i] = i;
+    for (int j = tid; j < n; j += kSmallThreads) cp[j] = j;
+    // every thread tracks the loop state (identical everywhere); thread 0 publishes it
+    double maxerror = 0.0, error = __longlong_as_double(0x7ff8000000000000LL);
+    int np = 0;
+    __syncthreads();
+    // argmax of abs2 over the trailing block (submatrixargmax, matrixlu.jl:46-87): the candidate
+    // order (value, column, row) is the reference's column-major scan with strict '>'
+    CandR best = cand_none();
+    for (int j = w; j < n; j += NW)
+        for (int i = l; i < m; i += 64) {
+            const double v = S[i + j * m];
+            const double a2 = __dmul_rn(v, v);
+            if (cand_better(a2, j, i, best.v, best.cpos, best.rpos)) best = CandR{a2, v, j, i, j, i};
+        }
+    for (int k = 0; k < mr; ++k) {
+        wave_reduce_cand(best);
+        if (l == 0) red[w] = best;
+        __syncthreads();
+        CandR b = red[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) cand_take(b, red[i]);
+        int p = b.rpos, q = b.cpos;
+        double val = b.val;  // the candidate carries A[p, q] (read before any thread swaps)
+        if (!(b.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
+            p = q = k;
+            val = S[k + k * m];
+        }
+        error = fabs(val);
+        if (((fabs(error) < reltol * maxerror) || (fabs(error) < abstol)) && k > 0) break;
+        maxerror = jl_max(maxerror, error);
+        np = k + 1;
+        if (tid == 0) pivvals[k] = val;
+        // swaprow!(k, p) then swapcol!(k, q) (matrixlu.jl:254-275)
+        if (p != k) {
+            for (int j = tid; j < n; j += kSmallThreads) {
+                const double t = S[k + j * m];
+                S[k + j * m] = S[p + j * m];
+                S[p + j * m] = t;
+            }
+            if (tid == 0) {
+                const int t = rp[k];
+                rp[k] = rp[p];
+                rp[p] = t;
+            }
+            __syncthreads();
+        }
+        if (q != k) {
+            for (int i = tid; i < m; i += kSmallThreads) {
+                const double t = S[i + k * m];
+                S[i + k * m] = S[i + q * m];
+                S[i + q * m] = t;
+            }
+            if (tid == 0) {
+                const int t = cp[k];
+                cp[k] = cp[q];
+                cp[q] = t;
+            }
+            __syncthreads();
+        }
+        // normalisation by the pivot (true division; matrixlu.jl:300-305) into S and xv / yv
+        const double piv = S[k + k * m];
+        for (int i = k + 1 + tid; i < m; i += kSmallThreads) {
+            const double x = leftorth ? S[i + k * m] / piv : S[i + k * m];
+            xv[i] = x;
+            S[i + k * m] = x;
+        }
+        for (int j = k + 1 + tid; j < n; j += kSmallThreads) {
+            const double y = leftorth ? S[k + j * m] : S[k + j * m] / piv;
+            yv[j] = y;
+            S[k + j * m] = y;
+        }
+        __syncthreads();
+        // rank-1 update (mul then sub, matrixlu.jl:314-320) fused with the next pivot's argmax
+        best = cand_none();
+        for (int j = w; j < n; j += NW) {
+            if (j <= k) continue;
+            const double y = yv[j];
+            for (int i = l; i < m; i += 64) {
+                if (i <= k) continue;
+                const double v = __dsub_rn(S[i + j * m], __dmul_rn(xv[i], y));
+                S[i + j * m] = v;
+                const double a2 = __dmul_rn(v, v);
+                if (cand_better(a2, j, i, best.v, best.cpos, best.rpos)) best = CandR{a2, v, j, i, j, i};
+            }
+        }
+    }
+    if (tid == 0) {
+        st->np = np;
+        st->done = 1;
+        st->maxerror = maxerror;
+        st->error = error;
+        ctl[3] = np;
+        ctl[4] = 0;
+        if (out.maxout) *out.maxout = *out.maxin;
+    }
+    __syncthreads();
+    np = ctl[3];  // thread 0's count, for every thread
+    // outputs in the pass pipeline's conventions (physical-order L columns / U rows)
+    for (int i = tid; i < m; i += kSmallThreads) rowphys[i] = rp[i];
+    for (int j = tid; j < n; j += kSmallThreads) colphys[j] = cp[j];
+    if (Lp)
+        for (int e = tid; e < m * np; e += kSmallThreads) {
+            const int pos = e % m, t = e / m;
+            if (pos > t) Lp[rp[pos] + (int64_t)t * ldl] = S[pos + t * m];
+        }
+    if (Up)
+        for (int e = tid; e < np * n; e += kSmallThreads) {
+            const int t = e % np, pos = e / np;
+            if (pos > t) Up[t + (int64_t)cp[pos] * ldu] = S[t + pos * m];
+        }
+    if (!out.flag) return;
+    // NaN checks of tril(A[:, 1:np]) / triu(A[1:np, :]) before the unit diagonal is set
+    // (matrixlu.jl:376-381); the pivot values sit on S's diagonal
+    {
+        int fl = 0;
+        for (int e = tid; e < m * np; e += kSmallThreads) {
+            const int pos = e % m, t = e / m;
+            if (pos >= t && isnan(S[pos + t * m])) fl |= 1;
+        }
+        for (int e = tid; e < np * n; e += kSmallThreads) {
+            const int t = e % np, pos = e / np;
+            if (pos >= t && isnan(S[t + pos * m])) fl |= 2;
+        }
+        if (fl) atomicOr(&ctl[4], fl);
+        __syncthreads();
+        if (tid == 0) *out.flag = ctl[4];
+    }
+    if (np == 0) return;
+    // MatrixLUCI factors (matrixluci.jl:161-283) straight from LDS, in the same operation order
+    // as the pass pipeline's factor kernels (tci_device.hip). Position-order L / U are
+    //   leftorth:  L[a,t] = (t == a ? 1 : S[a,t]),  U[t,j] = S[t,j]          (t <= a, t <= j)
+    //   otherwise: L[i,t] = S[i,t],                 U[t,j] = (t == j ? 1 : S[t,j])
+    if (leftorth) {
+        if (out.right)  // rowmatrix = L11 * U, column-scattered
+            for (int e = tid; e < np * n; e += kSmallThreads) {
+                const int a = e % np, j = e / np;
+                double s = 0.0;
+                for (int t = 0; t <= min(a, j); ++t)
+                    s = __dadd_rn(s, __dmul_rn(t == a ? 1.0 : S[a + t * m], S[t + j * m]));
+                out.right[a + (int64_t)cp[j] * np] = s;
+            }
+        if (out.left) {  // colstimespivotinv: rows >= np solve X L11 = L21 in place
+            __syncthreads();
+            for (int i = np + tid; i < m; i += kSmallThreads)
+                for (int j = np - 1; j >= 0; --j) {
+                    double s = S[i + j * m];
+                    for (int t = j + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[i + t * m], S[t + j * m]));
+                    S[i + j * m] = s;
+                }
+            __syncthreads();
+            for (int e = tid; e < m * np; e += kSmallThreads) {
+                const int i = e % m, j = e / m;
+                out.left[rp[i] + (int64_t)j * m] = i < np ? (i == j ? 1.0 : 0.0) : S[i + j * m];
+            }
+        }
+    } else {
+        if (out.left)  // colmatrix = L * U11, row-scattered
+            for (int e = tid; e < m * np; e += kSmallThreads) {
+                const int i = e % m, j = e / m;
+                double s = 0.0;
+                for (int t = 0; t <= min(i, j); ++t)
+                    s = __dadd_rn(s, __dmul_rn(S[i + t * m], t == j ? 1.0 : S[t + j * m]));
+                out.left[rp[i] + (int64_t)j * m] = s;
+            }
+        if (out.right) {  // pivotinvtimesrows: columns >= np solve U11 x = U[:, c] in place
+            __syncthreads();
+            for (int c = np + tid; c < n; c += kSmallThreads)
+                for (int a = np - 1; a >= 0; --a) {
+                    double s = S[a + c * m];
+                    for (int t = a + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[a + t * m], S[t + c * m]));
+                    S[a + c * m] = s;
+                }
+            __syncthreads();
+            for (int e = tid; e < np * n; e += kSmallThreads) {
+                const int a = e % np, j = e / np;
+                out.right[a + (int64_t)cp[j] * np] = j < np ? (a == j ? 1.0 : 0.0) : S[a + j * m];
+            }
+        }
+    }
+}
+
+hipError_t launch_rrlu_small(hipStream_t s, const double* A, int64_t lda, int m, int n, int mr,
+                             double reltol, double abstol, int leftorth, RrluState* st,
+                             int64_t* rowphys, int64_t* colphys, double* pivvals, double* Lp,
+                             int64_t ldl, double* Up, int64_t ldu, SmallOut out) {
+    const size_t bytes = small_lds_bytes(m, n);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rrlu_small),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rrlu_small, dim3(1), dim3(kSmallThreads), bytes, s, A, lda, m, n, mr,
+                       reltol, abstol, leftorth, st, rowphys, colphys, pivvals, Lp, ldl, Up, ldu,
+                       out);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ extraction
 // L (m x np, position order) and U (np x n) as _optimizerrlu! leaves them (matrixlu.jl:372-388):
 //   L[pos, t] = 0 (pos < t), diag (pos == t), Lp[rowphys[pos], t] (pos > t)

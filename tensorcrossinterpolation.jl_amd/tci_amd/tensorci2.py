@@ -58,8 +58,17 @@ def union_sets(a, b):
         return np.ascontiguousarray(cat, np.int32)
     if cat.shape[1] == 0:
         return np.zeros((1, 0), np.int32)
-    _, first = np.unique(cat, axis=0, return_index=True)
-    return np.ascontiguousarray(cat[np.sort(first)], np.int32)
+    cat = np.ascontiguousarray(cat, np.int32)
+    keys = cat.view(np.dtype((np.void, 4 * cat.shape[1]))).ravel()
+    if len(keys) <= 4096:  # small sets (every TCI2 bond at low rank): one dict pass
+        seen = {}
+        for i, k in enumerate(keys.tolist()):
+            seen.setdefault(k, i)
+        if len(seen) == len(keys):
+            return cat
+        return cat[np.fromiter(seen.values(), np.int64, len(seen))]
+    _, first = np.unique(keys, return_index=True)
+    return cat[np.sort(first)]
 
 
 def pushunique(s, e):

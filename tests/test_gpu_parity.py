@@ -16,9 +16,14 @@ pytestmark = pytest.mark.gpu
 T = pytest.importorskip("tci_amd")
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    return T.context(0)
+@pytest.fixture(scope="module", params=["small", "pipeline"])
+def ctx(request):
+    """Every test runs twice: with the single-workgroup LDS rrLU for small matrices (the default)
+    and with the pass pipeline forced for every size."""
+    c = T.Context(0)
+    c.check(c.lib.tci_set_rrlu_small(c.h, int(request.param == "small")))
+    yield c
+    c.close()
 
 
 def assert_lu_bitwise(lu, ref):
@@ -62,6 +67,15 @@ def test_rrlu_random_bitwise(ctx, m, n, maxrank, leftorth):
     A = O.fill_uniform(m * n, seed=m * 7 + n).reshape((m, n), order="F")
     lu = T.rrlu(A, maxrank=maxrank, leftorthogonal=leftorth, ctx=ctx)
     assert_lu_bitwise(lu, O.OracleLU(A, maxrank=maxrank, leftorthogonal=leftorth))
+
+
+@pytest.mark.parametrize("m,n", [(128, 128), (64, 256), (1, 4000), (4000, 1), (129, 127), (2, 2048)])
+def test_rrlu_small_path_limits_bitwise(ctx, m, n):
+    # around the single-workgroup limits (m*n <= 16384, m + n <= 4096)
+    A = O.fill_uniform(m * n, seed=m + 3 * n).reshape((m, n), order="F")
+    for leftorth in (True, False):
+        lu = T.rrlu(A, maxrank=min(m, n), leftorthogonal=leftorth, ctx=ctx)
+        assert_lu_bitwise(lu, O.OracleLU(A, maxrank=min(m, n), leftorthogonal=leftorth))
 
 
 def test_rrlu_ties_lorentzian_bitwise(ctx):
