@@ -44,6 +44,10 @@ extern "C" {
 #define TCI_F_QOSC 5     /* quantics x: exp(-p0 x) sin(p1 x^p2)         (test_tensorci2.jl:437) */
 #define TCI_F_QEXP 6     /* quantics x: p0 exp(-p1 x) + p2 exp(-p3 x)   (test_tensorci2.jl:65)  */
 #define TCI_F_TT 7       /* tensor-train evaluation (test_tensorci2.jl:477-502, TTCache as f)   */
+#define TCI_F_CP 8       /* f(x) = sum_k prod_t g[k][t][x_t]: CP-rank-K synthetic */
+/* GAUSSMIX and CP are sums of K separable terms: Pi is assembled as a rank-K fp64 MFMA GEMM.
+ * params: GAUSSMIX [K, a, centres (K x L, row-major), weights (K)];
+ *         CP       [K, dmax, g (K x L x dmax, dmax fastest)] with dmax >= max(localdims). */
 
 typedef struct tci_ctx tci_ctx;
 typedef struct tci_func tci_func;

@@ -76,7 +76,7 @@ void orc_fill_uniform(double* a, i64 n, uint64_t seed, i64 offset) {
  * _batchevaluate_dispatch does (batcheval.jl:157-171). x is 1-based, length L. */
 enum {
     F_SUM = 0, F_LORENTZ = 1, F_TABLE = 2, F_GAUSS = 3, F_GAUSSMIX = 4,
-    F_QOSC = 5, F_QEXP = 6, F_TT = 7
+    F_QOSC = 5, F_QEXP = 6, F_TT = 7, F_CP = 8
 };
 typedef struct {
     int kind;
@@ -172,6 +172,19 @@ static double feval(const orc_func* f, const i32* x) {
             core += (i64)ra * d * rb;
         }
         return v[0];
+    }
+    case F_CP: {
+        /* CP-rank-K synthetic of SURVEY.md 8(d) (config 5): sum_k prod_t g[k][t][x_t];
+         * p = [K, dmax, g (K x L x dmax, dmax fastest)] */
+        int K = (int)p[0], dmax = (int)p[1];
+        const double* g = p + 2;
+        double acc = 0.0;
+        for (int k = 0; k < K; ++k) {
+            double prod = 1.0;
+            for (int t = 0; t < L; ++t) prod = prod * g[((i64)k * L + t) * dmax + (x[t] - 1)];
+            acc = acc + prod;
+        }
+        return acc;
     }
     }
     return NAN;

@@ -53,6 +53,16 @@ def configs():
         return run("C4 quantics exp(-10x) sin(2pi 100 x^1.1), 40 legs d=2 tol=1e-8", f, [2] * 40, [p0],
                    tolerance=1e-8, nsearchglobalpivot=0)
     out["C4_qosc40"] = qosc
+
+    def cp12():
+        # config 5 scaled: CP-rank-256 synthetic, 12 legs of d = 32 (the full config: K = 1024)
+        rng = np.random.default_rng(2)
+        K, L, d = 256, 12, 32
+        f = T.cp_function(0.5 + rng.random((K, L, d)))
+        p0 = T.optfirstpivot(f, [d] * L)
+        return run("C5 scaled: 12d CP-rank-256 synthetic d=32 tol=1e-10 maxbonddim=256", f, [d] * L,
+                   [p0], tolerance=1e-10, maxbonddim=256, maxiter=3, nsearchglobalpivot=0)
+    out["C5_cp12d_K256"] = cp12
     return out
 
 

@@ -106,8 +106,10 @@ struct tci_func {
     int32_t* dld = nullptr;
     int64_t* dstrides = nullptr;
     int64_t nparams = 0;
+    int32_t cpK = 0;
     FuncDev view() const {
         FuncDev f;
+        f.cpK = cpK;
         f.kind = kind;
         f.L = L;
         f.localdims = dld;
@@ -561,13 +563,32 @@ int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* lau
 int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
                     const int32_t* localdims, int32_t L, tci_func** out) {
     if (!c || !out) return TCI_ERR_ARG;
-    if (kind < TCI_F_SUM || kind > TCI_F_TT) return set_err(c, TCI_ERR_ARG, "unknown integrand kind");
+    if (kind < TCI_F_SUM || kind > TCI_F_CP) return set_err(c, TCI_ERR_ARG, "unknown integrand kind");
     if (L < 1) return set_err(c, TCI_ERR_ARG, "L must be >= 1");
     if (L > 62 && (kind == TCI_F_QOSC || kind == TCI_F_QEXP))
         return set_err(c, TCI_ERR_ARG, "quantics integrands support at most 62 legs");
+    int32_t cpK = 0;
+    if (kind == TCI_F_GAUSSMIX || kind == TCI_F_CP) {
+        if (nparams < 2 || !params || params[0] < 0) return set_err(c, TCI_ERR_ARG, "params too short");
+        cpK = (int32_t)params[0];
+        int64_t need = 2 + (int64_t)cpK * L + cpK;  // GAUSSMIX: K, a, centres, weights
+        if (kind == TCI_F_CP) {
+            const int64_t dmax = (int64_t)params[1];
+            for (int t = 0; t < L; ++t)
+                if (localdims[t] > dmax) return set_err(c, TCI_ERR_ARG, "CP: localdims exceed dmax");
+            need = 2 + (int64_t)cpK * L * dmax;
+        }
+        if (nparams < need) return set_err(c, TCI_ERR_ARG, "params too short for K terms");
+    }
+    if (kind == TCI_F_TABLE) {
+        int64_t cnt = 1;
+        for (int t = 0; t < L; ++t) cnt *= localdims[t];
+        if (nparams < cnt) return set_err(c, TCI_ERR_ARG, "table smaller than prod(localdims)");
+    }
     tci_func* f = new tci_func();
     f->ctx = c;
     f->kind = kind;
+    f->cpK = cpK;
     f->L = L;
     f->localdims.assign(localdims, localdims + L);
     f->nparams = nparams;

@@ -212,7 +212,11 @@ void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t
 // per-row and per-column "state" (O((m+n)L)), then one pass that combines and writes
 // Pi[R + ldo*j] -- an HBM-write-bound stream. Other kinds evaluate directly per element.
 enum { F_SUM = 0, F_LORENTZ = 1, F_TABLE = 2, F_GAUSS = 3, F_GAUSSMIX = 4, F_QOSC = 5, F_QEXP = 6,
-       F_TT = 7 };
+       F_TT = 7, F_CP = 8 };
+
+// Kinds that are a sum of K separable terms, f = sum_k rowfactor_k(I, c) * colfactor_k(J): Pi is
+// a rank-K product EL * ER^T, assembled by an fp64 MFMA GEMM (k_gemm_cp).
+__host__ __device__ __forceinline__ bool cp_kind(int kind) { return kind == F_GAUSSMIX || kind == F_CP; }
 
 __host__ __device__ __forceinline__ bool staged_kind(int kind) {
     return kind == F_SUM || kind == F_LORENTZ || kind == F_TABLE || kind == F_GAUSS ||
@@ -448,7 +452,115 @@ __global__ __launch_bounds__(256) void k_assemble_direct(FuncDev f, const int32_
     block_maxabs(mx, maxbits);
 }
 
+// ------------------------------------------------ separable kinds: GEMM
+// GAUSSMIX: f = sum_k w_k exp(-(a * sum_t (x_t - c_kt)^2)) = sum_k EL[R,k] ER[j,k] with
+//   EL = exp(-(a * S_left)), ER = w_k exp(-(a * S_right)) (S: partial sums over the legs of I
+//   (+ centre) / J). Splitting the exponential changes the rounding against per-element
+//   evaluation by ~|a S| ulps (tests: rtol 1e-12).
+// CP: f = sum_k prod_t g[k][t][x_t]: EL / ER = partial products.
+// Factors are stored k-major (EL[k * ldR + R], ER[k * ldC + j]) and zero-padded to K4 = 4 |K.
+
+__device__ double cp_factor(const FuncDev& f, int k, const int32_t* e, int t0, int cnt, int cval,
+                            bool right) {
+    // legs t0 .. t0 + cnt - 1 take values e[0 .. cnt-1]; if cval > 0 one more leg (the centre,
+    // position t0 + cnt) takes cval
+    const int L = f.L;
+    const double* p = f.params;
+    const int K = (int)p[0];
+    if (f.kind == F_GAUSSMIX) {
+        const double a = p[1];
+        const double* cc = p + 2 + (int64_t)k * L;
+        double s = 0.0;
+        for (int q = 0; q < cnt; ++q) {
+            const double u = (double)e[q] - cc[t0 + q];
+            s = __dadd_rn(s, __dmul_rn(u, u));
+        }
+        if (cval > 0) {
+            const double u = (double)cval - cc[t0 + cnt];
+            s = __dadd_rn(s, __dmul_rn(u, u));
+        }
+        const double v = exp(-(a * s));
+        return right ? __dmul_rn(p[2 + (int64_t)K * L + k], v) : v;
+    }
+    // F_CP
+    const int dmax = (int)p[1];
+    const double* g = p + 2 + (int64_t)k * L * dmax;
+    double prod = 1.0;
+    for (int q = 0; q < cnt; ++q) prod = __dmul_rn(prod, g[(int64_t)(t0 + q) * dmax + (e[q] - 1)]);
+    if (cval > 0) prod = __dmul_rn(prod, g[(int64_t)(t0 + cnt) * dmax + (cval - 1)]);
+    return prod;
+}
+
+// rows: R in [0, m*D) (i = R % m, centre c = R / m); cols: j in [0, n) (legs L - nr ..)
+__global__ void k_cp_factors(FuncDev f, const int32_t* __restrict__ T, int cnt, int nrows, int D,
+                             int M, int K, int K4, int64_t ld, int t0, bool right,
+                             double* __restrict__ out) {
+    const int64_t tot = (int64_t)ld * K4;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int R = (int)(e % ld), k = (int)(e / ld);
+        double v = 0.0;
+        if (R < (int64_t)nrows * D && k < K) {
+            const int i = R % nrows, c = R / nrows;
+            v = cp_factor(f, k, T + (int64_t)i * cnt, t0, cnt, M ? c + 1 : 0, right);
+        }
+        out[e] = v;
+    }
+}
+
+// Pi[R, j] = sum_k EL[k, R] * ER[k, j] on v_mfma_f64_16x16x4_f64: a wave owns a 32 x 32 tile
+// (2 x 2 MFMA blocks), a workgroup 4 waves (64 x 64). Operand lanes: A[row l&15][k l>>4],
+// B[k l>>4][col l&15]; result: col = l & 15, row = (l >> 4) + 4 * reg (cdna_hip_programming.md).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_gemm_cp(const double* __restrict__ EL, int64_t ldR,
+                                                 const double* __restrict__ ER, int64_t ldC, int K4,
+                                                 int64_t mR, int n, double* __restrict__ out,
+                                                 int64_t ldo, unsigned long long* maxbits) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t R0 = (int64_t)blockIdx.x * 64 + (wv & 1) * 32;
+    const int64_t j0 = (int64_t)blockIdx.y * 64 + (wv >> 1) * 32;
+    const int r = lane & 15, kk = lane >> 4;
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
+    // factors are padded to whole 32-row / 32-column tiles (ldR, ldC multiples of 64): no guards
+    for (int k0 = 0; k0 < K4; k0 += 4) {
+        const double* el = EL + (int64_t)(k0 + kk) * ldR + R0 + r;
+        const double* er = ER + (int64_t)(k0 + kk) * ldC + j0 + r;
+        const double a0 = el[0], a1 = el[16], b0 = er[0], b1 = er[16];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    double mx = 0.0;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t R = R0 + 16 * x + (lane >> 4) + 4 * g;
+                const int64_t j = j0 + 16 * y + (lane & 15);
+                if (R < mR && j < n) {
+                    const double v = acc[x][y][g];
+                    out[R + ldo * j] = v;
+                    const double av = fabs(v);
+                    mx = (isnan(av) || av > mx) ? av : mx;
+                }
+            }
+    block_maxabs(mx, maxbits);
+}
+
+static int64_t cp_ld(int64_t rows) { return (rows + 63) / 64 * 64; }
+
 int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n) {
+    if (cp_kind(f.kind)) {
+        const int64_t K4 = (f.cpK + 3) / 4 * 4;
+        return 8 * K4 * (cp_ld((int64_t)m * D) + cp_ld(n));
+    }
     if (!staged_kind(f.kind)) return 0;
     return 8 * ((int64_t)m * D + n);
 }
@@ -457,6 +569,19 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
                       const int32_t* J, int n, int nr, int M, int D, double* out, int64_t ldo,
                       unsigned long long* maxbits, void* scratch) {
     const int64_t mR = (int64_t)m * D;
+    if (cp_kind(f.kind)) {
+        const int K = f.cpK, K4 = (K + 3) / 4 * 4;
+        const int64_t ldR = cp_ld(mR), ldC = cp_ld(n);
+        double* EL = reinterpret_cast<double*>(scratch);
+        double* ER = EL + (int64_t)K4 * ldR;
+        hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldR * K4, 4096)), dim3(256), 0, s, f, I, nl, m,
+                           D, M, K, K4, ldR, 0, false, EL);
+        hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldC * K4, 4096)), dim3(256), 0, s, f, J, nr, n,
+                           1, 0, K, K4, ldC, f.L - nr, true, ER);
+        hipLaunchKernelGGL(k_gemm_cp, dim3((unsigned)(ldR / 64), (unsigned)(ldC / 64)), dim3(256), 0,
+                           s, EL, ldR, ER, ldC, K4, mR, n, out, ldo, maxbits);
+        return;
+    }
     if (staged_kind(f.kind)) {
         St* rs = reinterpret_cast<St*>(scratch);
         St* cs = rs + mR;

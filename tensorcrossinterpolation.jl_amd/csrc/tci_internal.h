@@ -88,6 +88,7 @@ struct FuncDev {
     const double* params;      // device
     int64_t nparams;
     const int64_t* strides;    // device, column-major strides for TCI_F_TABLE
+    int32_t cpK;               // number of separable terms (TCI_F_GAUSSMIX, TCI_F_CP), host copy
 };
 
 // ---- rrLU (tci_rrlu.hip)

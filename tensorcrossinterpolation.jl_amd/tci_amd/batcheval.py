@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _lib
 
-F_SUM, F_LORENTZ, F_TABLE, F_GAUSS, F_GAUSSMIX, F_QOSC, F_QEXP, F_TT = range(8)
+F_SUM, F_LORENTZ, F_TABLE, F_GAUSS, F_GAUSSMIX, F_QOSC, F_QEXP, F_TT, F_CP = range(9)
 
 
 def _as_index_table(sets, width):
@@ -144,6 +144,16 @@ def tensortrain_function(cores, **kw):
     bd = [cores[0].shape[0]] + [c.shape[2] for c in cores]
     p = np.concatenate([np.asarray(bd, np.float64)] + [np.asarray(c, np.float64).ravel(order="F") for c in cores])
     return GPUBatchEvaluator(F_TT, p, [c.shape[1] for c in cores], name="tt", **kw)
+
+
+def cp_function(g, **kw):
+    """f(x) = sum_k prod_t g[k][t][x_t - 1]: the CP-rank-K synthetic of BASELINE config 5
+    (SURVEY.md 8(d)). g: array (K, L, dmax); leg t uses g[:, t, :localdims[t]]."""
+    g = np.asarray(g, np.float64)
+    K, L, dmax = g.shape
+    localdims = kw.pop("localdims", [dmax] * L)
+    p = np.concatenate([[K, dmax], g.ravel(order="C")])
+    return GPUBatchEvaluator(F_CP, p, localdims, name="cp", **kw)
 
 
 def quantics_bits(x, R):

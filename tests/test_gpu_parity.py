@@ -138,15 +138,29 @@ KINDS = [
     (3, [1.0 / 64, 8.5], [16] * 6),
     (5, [10.0, 2 * np.pi * 100, 1.1], [2] * 20),
     (6, [1.0, 1.0, 1e-4, 2.0], [2] * 12),
+    (4, None, [6] * 8),           # GAUSSMIX: rank-K MFMA GEMM path
+    (8, None, [5, 3, 4, 5, 2, 5]),  # CP-rank-K synthetic: rank-K MFMA GEMM path
 ]
+
+
+def _random_params(kind, ld, rng, K=37):
+    L = len(ld)
+    if kind == 2:
+        return rng.random(int(np.prod(ld))).tolist()
+    if kind == 4:  # K Gaussians, mixed-sign weights
+        return np.concatenate([[K, 0.07], rng.random(K * L) * max(ld), rng.random(K) - 0.3]).tolist()
+    if kind == 8:
+        dmax = max(ld)
+        return np.concatenate([[K, dmax], rng.random(K * L * dmax) * 1.5]).tolist()
+    return None
 
 
 @pytest.mark.parametrize("kind,params,ld", KINDS)
 @pytest.mark.parametrize("M", [0, 1])
 def test_batcheval_vs_oracle(ctx, kind, params, ld, M):
     rng = np.random.default_rng(kind * 10 + M)
-    if kind == 2:
-        params = rng.random(int(np.prod(ld))).tolist()
+    if params is None:
+        params = _random_params(kind, ld, rng)
     L = len(ld)
     nl = L // 2 - (1 if M else 0)
     nr = L - nl - M
@@ -161,7 +175,8 @@ def test_batcheval_vs_oracle(ctx, kind, params, ld, M):
         _, gmx = f.pi(I, J, M)
         assert gmx == rmx
     else:
-        # ocml vs glibc exp/sin/pow: a few ulp of the largest intermediate
+        # ocml vs glibc exp/sin/pow: a few ulp of the largest intermediate; separable kinds (4, 8)
+        # also split the exponential / product and sum the K terms in MFMA order
         np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-13 * np.abs(ref).max())
         _, gmx = f.pi(I, J, M)
         assert gmx == pytest.approx(rmx, rel=1e-13)
@@ -182,7 +197,25 @@ def test_batcheval_tt_and_gaussmix(ctx):
     g = T.gaussmix([6] * 5, 0.1, cen, [1.0, -0.5, 0.25, 2.0], ctx=ctx)
     p2 = np.concatenate([[4, 0.1], cen.ravel(), [1.0, -0.5, 0.25, 2.0]])
     X = rng.integers(1, 7, (50, 5)).astype(np.int32)
-    np.testing.assert_allclose(g.points(X), [O.feval(4, p2, [6] * 5, x) for x in X], rtol=1e-13)
+    ref = np.array([O.feval(4, p2, [6] * 5, x) for x in X])
+    np.testing.assert_allclose(g.points(X), ref, rtol=1e-12, atol=1e-13 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (130, 70, 5), (200, 257, 64), (64, 64, 1024)])
+def test_cp_gemm_sizes(ctx, shape):
+    # rank-K GEMM assembly across tile edges (R, n not multiples of 64; K not a multiple of 4)
+    m, n, K = shape
+    rng = np.random.default_rng(m + n + K)
+    ld = [4, 3, 5, 4]
+    params = np.concatenate([[K, 5], rng.random(K * 4 * 5) - 0.5])
+    I = np.stack([rng.integers(1, ld[t] + 1, m) for t in range(2)], axis=1).astype(np.int32)
+    J = np.stack([rng.integers(1, ld[2 + t] + 1, n) for t in range(2)], axis=1).astype(np.int32)
+    ref, rmx = O.batcheval(8, params, ld, I, J, 0)
+    f = T.GPUBatchEvaluator(8, params, ld, ctx=ctx)
+    got, gmx = f.pi(I, J, 0)
+    ref = ref.reshape(got.shape, order="F")
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-13 * np.abs(ref).max())
+    assert gmx == pytest.approx(rmx, rel=1e-12)
 
 
 def test_sitetensor_solve(ctx):
