@@ -202,7 +202,7 @@ def main():
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 8}  # the bench command profiled there
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10}  # the bench command profiled there
 
 
 def pmc_traffic(fam, m, n, r, nb):
