@@ -83,7 +83,9 @@ def main():
 
     import tci_amd as T
 
-    ctx = T.context(local_rank)
+    # one process per GPU (LOCAL_RANK); TCI_BENCH_DEVICE pins every rank to one device, only to
+    # rehearse the multi-rank control flow on a one-GPU machine
+    ctx = T.context(int(os.environ.get("TCI_BENCH_DEVICE", local_rank)))
     ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, args.nb))
     m, n, r = args.m, args.n, args.r
     A = T.DeviceMatrix(m, n, ctx=ctx)
@@ -191,8 +193,11 @@ def main():
     A.free()
     W.free()
 
-    if rank == 0 and not args.no_extras:
-        out["extras"] = extras(T, ctx)
+    if not args.no_extras:
+        sh = sharded_pi(T, ctx, dist, world, rank)
+        if rank == 0:
+            out["extras"] = extras(T, ctx)
+            out["extras"]["pi_lorentz_sharded"] = sh
     if rank == 0 and not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(m, n, r, args.cpu_pivots)
     if rank == 0:
@@ -216,6 +221,51 @@ def pmc_traffic(fam, m, n, r, nb):
     return {"traffic": rec["hbm_bytes_per_launch"],
             "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE, "
                               f"{rec['dispatches_profiled']} dispatches)"}
+
+
+def sharded_pi(T, ctx, dist, world, rank):
+    """Pi assembly of one 8192 x 8192 Lorentzian Pi (L = 20) split by column blocks over the
+    ranks: each rank evaluates its block on its own GPU, maxsample is all-reduced.
+    Strong scaling: Pi-rows/s = m / (max over ranks of the block time)."""
+    import ctypes as C
+
+    import torch
+
+    m = n = 8192
+    rng = np.random.default_rng(1)
+    I = rng.integers(1, 11, (m, 10)).astype(np.int32)
+    J = rng.integers(1, 11, (n, 10)).astype(np.int32)
+    j0, j1 = T.column_blocks(n, world)[rank]
+    Jb = np.ascontiguousarray(J[j0:j1])
+    f = T.lorentz([10] * 20, ctx=ctx)
+    dm = T.DeviceMatrix(m, max(j1 - j0, 1), ctx=ctx)
+    mx = C.c_double()
+
+    def run():
+        if j1 > j0:
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(I), m, 10, T._lib.ptr(Jb), j1 - j0, 10,
+                                              0, dm.ptr, dm.ld, C.byref(mx)))
+        else:
+            mx.value = 0.0
+
+    run()
+    reps = 5
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    gmx = mx.value
+    if dist is not None:
+        t = torch.tensor([dt, gmx], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, gmx = float(t[0]), float(t[1])
+    dm.free()
+    return {"m": m, "n": n, "L": 20, "ranks": world, "pi_rows_per_s": round(m / dt, 1),
+            "ms_per_pi": round(dt * 1e3, 4), "maxsample": gmx,
+            "note": "column blocks per rank, allreduce(max) of maxsample, no gather (strong scaling)"}
 
 
 def extras(T, ctx):

@@ -149,6 +149,12 @@ int tci_sitetensor_h(tci_ctx* ctx, const tci_func* f, const int32_t* Ib, int64_t
                      const int32_t* Jb, int64_t nJb, int32_t wJ, const int32_t* Inext,
                      int64_t nInext, double* T, double* maxabs);
 
+/* The solve of setsitetensor! alone (tensorci2.jl:620-627) on host matrices: T = Pi1 * P^-1,
+ * P: r x r, Pi1 and T: R x r, column-major (ld r / R). Used when Pi1 and P come from an
+ * evaluator other than a tci_func (e.g. the multi-GPU sharded evaluation). */
+int tci_sitetensor_solve_h(tci_ctx* ctx, const double* P, int64_t r, const double* Pi1, int64_t R,
+                           double* T);
+
 /* ----------------------------------------------------- synthetic inputs
  * Fills d_A (m x n, ld lda) with U[0,1): splitmix64(seed * 0xD1B54A32D192ED03 + (i + m*j)) >> 11
  * times 2^-53 -- the same stream as the oracle's orc_fill_uniform. */

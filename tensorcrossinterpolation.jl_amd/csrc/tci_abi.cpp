@@ -877,6 +877,26 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
     return TCI_OK;
 }
 
+int tci_sitetensor_solve_h(tci_ctx* c, const double* P, int64_t r, const double* Pi1, int64_t R,
+                           double* T) {
+    if (!c || (r > 0 && (!P || !T)) || (R > 0 && r > 0 && !Pi1) || r < 0 || R < 0)
+        return TCI_ERR_ARG;
+    if (r == 0 || R == 0) return TCI_OK;
+    if (r > INT32_MAX / 2 || R > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int st;
+    if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
+    if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(R * r)))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+    HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
 int tci_fill_uniform_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda, uint64_t seed) {
     if (!c || lda < m) return TCI_ERR_ARG;
     tci::launch_fill_uniform(c->stream, d_A, m, n, lda, seed);

@@ -7,6 +7,7 @@ from ._lib import Context, TCIArgumentError, TCIDeviceError, TCIError, context, 
 from .batcheval import (F_CP, F_GAUSS, F_GAUSSMIX, F_LORENTZ, F_QEXP, F_QOSC, F_SUM, F_TABLE, F_TT,
                         GPUBatchEvaluator, cp_function, gauss, gaussmix, lorentz, quantics_bits,
                         quantics_exp, quantics_osc, sum_, table, tensortrain_function)
+from .distributed import Comm, ShardedBatchEvaluator, column_blocks
 from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder
 from .matrixlu import (DeviceMatrix, colindices, diag, lastpivoterror, ldiv, left, npivots, pivoterrors,
                        right, rowindices, rrLU, rrlu, rrlu_inplace_device)

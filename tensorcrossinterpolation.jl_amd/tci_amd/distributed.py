@@ -1,0 +1,137 @@
+"""Multi-GPU sharding of the batch evaluation.
+
+One process per GPU (torch.distributed: "nccl" is RCCL over xGMI on ROCm, "gloo" for host
+buffers and CPU tests). Pi assembly is embarrassingly parallel over elements, so the columns of
+Jcomb are split into contiguous blocks, one per rank: each rank evaluates Pi[:, j0:j1] on its own
+GPU (column-major, so a block is contiguous), maxsample is all-reduced with Julia's
+NaN-propagating max (updatemaxsample!, tensorci2.jl:636-638 / util.jl:34-43), and the blocks are
+all-gathered only where a replicated Pi is needed (the replicated rrLU that follows in
+updatepivots!, tensorci2.jl:842-868). Every rank then holds bitwise the same Pi, so the
+replicated factorisations agree exactly and all ranks keep identical TCI2 state.
+
+`ShardedBatchEvaluator` wraps any evaluator with the `pi(I, J, M) -> (matrix, maxabs)` method of
+`GPUBatchEvaluator` and is itself such an evaluator, so `crossinterpolate2` takes it unchanged.
+"""
+import math
+
+import numpy as np
+
+
+def column_blocks(n, world):
+    """Balanced contiguous blocks [(j0, j1)] of n columns over `world` ranks (rank order)."""
+    base, rem = divmod(int(n), int(world))
+    out, j = [], 0
+    for r in range(world):
+        w = base + (1 if r < rem else 0)
+        out.append((j, j + w))
+        j += w
+    return out
+
+
+class Comm:
+    """torch.distributed facade for the two collectives the sharded path needs.
+
+    device: the torch device of the collective buffers ("cpu" for gloo; "cuda:<local rank>" for
+    nccl, i.e. RCCL on ROCm). Data is exchanged as float64 tensors.
+    """
+
+    def __init__(self, group=None, device="cpu"):
+        import torch
+        import torch.distributed as dist
+
+        self.torch = torch
+        self.dist = dist
+        self.group = group
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def allreduce_maxabs(self, x):
+        """max over ranks with Julia's NaN propagation (any NaN -> NaN)."""
+        torch = self.torch
+        isn = math.isnan(x)
+        t = torch.tensor([-math.inf if isn else float(x), 1.0 if isn else 0.0], dtype=torch.float64,
+                         device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return math.nan if t[1].item() > 0 else float(t[0].item())
+
+    def allgather_columns(self, block, blocks, rows):
+        """Concatenate the ranks' column blocks (rows x (j1 - j0), Fortran order) into the full
+        rows x n matrix, identical on every rank."""
+        torch = self.torch
+        wmax = max(j1 - j0 for j0, j1 in blocks)
+        n = blocks[-1][1]
+        buf = torch.zeros(rows * max(wmax, 1), dtype=torch.float64, device=self.device)
+        if block.size:
+            buf[: block.size] = torch.from_numpy(np.asarray(block, np.float64).ravel(order="F")).to(self.device)
+        out = torch.empty(self.world * buf.numel(), dtype=torch.float64, device=self.device)
+        self.dist.all_gather_into_tensor(out, buf, group=self.group)
+        out = out.cpu().numpy().reshape(self.world, -1)
+        full = np.empty((rows, n), order="F")
+        for r, (j0, j1) in enumerate(blocks):
+            if j1 > j0:
+                full[:, j0:j1] = out[r, : rows * (j1 - j0)].reshape((rows, j1 - j0), order="F")
+        return full
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+
+class ShardedBatchEvaluator:
+    """A BatchEvaluator{Float64} whose batch evaluation is split over the ranks of `comm` by
+    column blocks of Jset; each rank's block runs on its own GPU through `local` (a
+    GPUBatchEvaluator on that rank's device)."""
+
+    def __init__(self, local, comm):
+        self.local = local
+        self.comm = comm
+        self.localdims = list(local.localdims)
+        self.L = len(self.localdims)
+        self.name = f"sharded({getattr(local, 'name', 'f')})"
+
+    def block(self, n):
+        """This rank's column range of an n-column Pi."""
+        return column_blocks(n, self.comm.world)[self.comm.rank]
+
+    def pi_local(self, I, J, M=0):
+        """This rank's block Pi[:, j0:j1] and the global max|Pi| (no gather)."""
+        I = np.ascontiguousarray(np.asarray(I, np.int32))
+        J = np.ascontiguousarray(np.asarray(J, np.int32))
+        D = self.localdims[I.shape[1]] if M == 1 else 1
+        j0, j1 = self.block(len(J))
+        if j1 > j0:
+            blk, mx = self.local.pi(I, J[j0:j1], M)
+        else:
+            blk, mx = np.zeros((I.shape[0] * D, 0), order="F"), 0.0
+        return (j0, j1), blk, self.comm.allreduce_maxabs(mx)
+
+    def pi(self, I, J, M=0):
+        """Full (|I| * D) x |J| Pi on every rank, and max|Pi|."""
+        I = np.asarray(I, np.int32)
+        J = np.asarray(J, np.int32)
+        D = self.localdims[I.shape[1]] if M == 1 else 1
+        _, blk, gmx = self.pi_local(I, J, M)
+        full = self.comm.allgather_columns(blk, column_blocks(len(J), self.comm.world), I.shape[0] * D)
+        return full, gmx
+
+    def points(self, X):
+        X = np.asarray(X, np.int32).reshape(-1, self.L)
+        out, _ = self.pi(np.zeros((1, 0), np.int32), X)  # the points become the columns
+        return out[0, :].copy()
+
+    def __call__(self, x, Jset=None, M=None):
+        if Jset is not None:
+            return self.batch(x, Jset, M)
+        return float(self.points(np.asarray(x).reshape(1, -1))[0])
+
+    def batch(self, Iset, Jset, M):
+        M = int(M)
+        if len(Iset) * len(Jset) == 0:
+            return np.zeros((0,) * (M + 2))
+        nl, nr = len(Iset[0]), len(Jset[0])
+        if nl + M + nr != self.L:
+            raise ValueError("Invalid number of central indices")
+        I = np.asarray(Iset, np.int32).reshape(len(Iset), nl)
+        J = np.asarray(Jset, np.int32).reshape(len(Jset), nr)
+        out, _ = self.pi(I, J, M)
+        return out.reshape((len(Iset),) + tuple(self.localdims[nl:nl + M]) + (len(Jset),), order="F")

@@ -437,9 +437,19 @@ def reconstractglobalpivotsfromijset(localdims, Isets, Jsets):
 
 
 # --------------------------------------------------------------- device calls
+def _ctx_of(f):
+    ctx = getattr(f, "ctx", None) or getattr(getattr(f, "local", None), "ctx", None)
+    return ctx or _lib.context()
+
+
 def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                          want_left=True, want_right=True):
-    """One fused device call: Pi = f(rows x cols), maxabs, rrLU, pivots, MatrixLUCI factors."""
+    """One fused device call: Pi = f(rows x cols), maxabs, rrLU, pivots, MatrixLUCI factors.
+    An evaluator that is not a GPUBatchEvaluator (e.g. a ShardedBatchEvaluator) supplies Pi
+    through its pi() method; the factorisation then runs on this process's GPU."""
+    if not hasattr(f, "h"):
+        return _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                                      want_left, want_right)
     ctx = f.ctx
     rows = np.ascontiguousarray(rows, np.int32)
     cols = np.ascontiguousarray(cols, np.int32)
@@ -468,8 +478,55 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
     return res
 
 
+def _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                           want_left, want_right):
+    ctx = _ctx_of(f)
+    Pi, mx = f.pi(np.asarray(rows, np.int32), np.asarray(cols, np.int32), 0)
+    Pi = np.asfortranarray(Pi, np.float64)
+    m, n = Pi.shape
+    mr = int(max(min(int(maxrank), m, n), 0))
+    rowidx = np.zeros(max(mr, 1), np.int64)
+    colidx = np.zeros(max(mr, 1), np.int64)
+    pe = np.zeros(mr + 1)
+    npv = C.c_int64()
+    left = np.zeros(max(m * mr, 1)) if (want_factors and want_left) else None
+    right = np.zeros(max(mr * n, 1)) if (want_factors and want_right) else None
+    ctx.check(ctx.lib.tci_luci_h(ctx.h, _lib.ptr(Pi), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
+                                 float(reltol), float(abstol), int(bool(leftorth)), _lib.ptr(rowidx),
+                                 _lib.ptr(colidx), _lib.ptr(pe), _lib.ptr(left), _lib.ptr(right),
+                                 C.byref(npv)))
+    k = npv.value
+    res = {"rowidx": rowidx[:k].copy(), "colidx": colidx[:k].copy(), "pivoterrors": pe[: k + 1].copy(),
+           "maxabs": mx, "npivot": k}
+    if left is not None:
+        res["left"] = left[: m * k].reshape((m, k), order="F")
+    if right is not None:
+        res["right"] = right[: k * n].reshape((k, n), order="F")
+    return res
+
+
+def _sitetensor_generic(f, Ib, Jb, Inext, solve):
+    Pi1, mx = f.pi(np.asarray(Ib, np.int32), np.asarray(Jb, np.int32), 1)
+    if not solve:
+        return None, mx
+    if Inext is None:
+        return np.asfortranarray(Pi1), mx
+    P, _ = f.pi(np.asarray(Inext, np.int32), np.asarray(Jb, np.int32), 0)
+    r = P.shape[0]
+    if P.shape[0] != P.shape[1]:
+        raise RuntimeError("Pivot matrix is not square!")
+    R = Pi1.shape[0]
+    T = np.zeros(max(R * r, 1))
+    ctx = _ctx_of(f)
+    ctx.check(ctx.lib.tci_sitetensor_solve_h(ctx.h, _lib.ptr(np.asfortranarray(P, np.float64)), r,
+                                             _lib.ptr(np.asfortranarray(Pi1, np.float64)), R, _lib.ptr(T)))
+    return T[: R * r].reshape((R, r), order="F"), mx
+
+
 def sitetensor_device(f, Ib, Jb, Inext, solve=True):
     """T = Pi1 * P^-1 (tensorci2.jl:599-629) on the device; returns (T or None, max|Pi1|)."""
+    if not hasattr(f, "h"):
+        return _sitetensor_generic(f, Ib, Jb, Inext, solve)
     ctx = f.ctx
     Ib = np.ascontiguousarray(Ib, np.int32)
     Jb = np.ascontiguousarray(Jb, np.int32)
@@ -498,6 +555,8 @@ def sitetensor_device(f, Ib, Jb, Inext, solve=True):
 
 
 def _batch_maxabs(f, I, J, M):
+    if not hasattr(f, "h"):
+        return f.pi(I, J, M)[1]
     ctx = f.ctx
     m, nl = I.shape
     n, nr = J.shape

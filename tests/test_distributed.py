@@ -1,0 +1,146 @@
+"""Multi-process tests of the sharded batch evaluation (tci_amd/distributed.py).
+
+CPU tests: world_size 2 (and 3) over gloo, with a test-only evaluator backed by the oracle, so
+the product's sharding, NaN-propagating maxsample reduction and column all-gather are checked
+against the single-process evaluation. GPU test: two ranks sharing cuda:0 (gloo for the
+exchange) run crossinterpolate2 through ShardedBatchEvaluator and must reproduce the
+single-process run bitwise. The parent process never touches the GPU (children are spawned).
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "tensorcrossinterpolation.jl_amd"))
+
+from tci_amd.distributed import Comm, ShardedBatchEvaluator, column_blocks  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_column_blocks():
+    for n in (0, 1, 5, 8, 37, 1000):
+        for world in (1, 2, 3, 8):
+            b = column_blocks(n, world)
+            assert len(b) == world and b[0][0] == 0 and b[-1][1] == n
+            assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
+            w = [j1 - j0 for j0, j1 in b]
+            assert max(w) - min(w) <= 1
+
+
+class OracleEvaluator:
+    """Test-only stand-in for a rank's GPUBatchEvaluator: the oracle's batch evaluation."""
+
+    def __init__(self, kind, params, localdims):
+        import oracle_lib as O
+
+        self.O, self.kind, self.params, self.localdims = O, kind, params, list(localdims)
+
+    def pi(self, I, J, M=0):
+        out, mx = self.O.batcheval(self.kind, self.params, self.localdims, I, J, M)
+        return out.reshape((-1, len(J)), order="F"), mx
+
+
+def _cpu_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        res = {}
+        # Lorentzian (integer-exact) and a table with a NaN in the last column block
+        ld = [6] * 6
+        table = rng.random(int(np.prod(ld)))
+        for name, kind, params in (("lorentz", 1, [1.0]), ("table", 2, table.tolist())):
+            for M in (0, 1):
+                nl = 2
+                nr = 6 - nl - M
+                I = rng.integers(1, 7, (23, nl)).astype(np.int32)
+                J = rng.integers(1, 7, (31, nr)).astype(np.int32)
+                f = ShardedBatchEvaluator(OracleEvaluator(kind, params, ld), Comm(device="cpu"))
+                full, mx = f.pi(I, J, M)
+                ref, rmx = OracleEvaluator(kind, params, ld).pi(I, J, M)
+                res[f"{name}{M}"] = bool(np.array_equal(full, ref)) and (mx == rmx)
+        # NaN in a column only the last rank evaluates: every rank must see maxabs = NaN
+        t2 = table.copy()
+        J = np.array([[1, 1, 1, 1]] * 9 + [[6, 6, 6, 6]], np.int32)
+        I = np.array([[1, 1]] * 4, np.int32)
+        t2[np.ravel_multi_index((0, 0, 5, 5, 5, 5), ld, order="F")] = np.nan
+        f = ShardedBatchEvaluator(OracleEvaluator(2, t2.tolist(), ld), Comm(device="cpu"))
+        _, mx = f.pi(I, J, 0)
+        res["nan"] = bool(np.isnan(mx))
+        # more ranks than columns: empty blocks
+        f = ShardedBatchEvaluator(OracleEvaluator(1, [1.0], ld), Comm(device="cpu"))
+        full, mx = f.pi(I, J[:1], 0)
+        ref, rmx = OracleEvaluator(1, [1.0], ld).pi(I, J[:1], 0)
+        res["empty_blocks"] = bool(np.array_equal(full, ref)) and mx == rmx
+        pts = rng.integers(1, 7, (13, 6)).astype(np.int32)
+        got = f.points(pts)
+        ref = OracleEvaluator(1, [1.0], ld).pi(np.zeros((1, 0), np.int32), pts, 0)[0][0]
+        res["points"] = bool(np.array_equal(got, ref))
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batcheval_gloo(tmp_path, world):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_cpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        assert all(res.values()), (r, res)
+
+
+def _gpu_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import tci_amd as T
+
+        ctx = T.context(0)
+        local = T.lorentz([8] * 6, ctx=ctx)
+        fs = ShardedBatchEvaluator(local, Comm(device="cpu"))
+        kw = dict(tolerance=1e-10, maxiter=8, nsearchglobalpivot=0)
+        tci, ranks, errors = T.crossinterpolate2(fs, [8] * 6, **kw)
+        ref, rranks, rerrors = T.crossinterpolate2(local, [8] * 6, **kw)
+        q = T.quantics_osc(16, ctx=ctx)
+        p0 = T.optfirstpivot(q, [2] * 16)
+        qs = ShardedBatchEvaluator(q, Comm(device="cpu"))
+        t2, r2, e2 = T.crossinterpolate2(qs, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
+        t2r, r2r, e2r = T.crossinterpolate2(q, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
+        res = {
+            "ranks": ranks == rranks, "errors": list(errors) == list(rerrors),
+            "isets": all(np.array_equal(a, b) for a, b in zip(tci.Iset, ref.Iset)),
+            "jsets": all(np.array_equal(a, b) for a, b in zip(tci.Jset, ref.Jset)),
+            "qosc": r2 == r2r and list(e2) == list(e2r),
+            "linkdims": tci.linkdims(),
+        }
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_tci2_two_ranks_one_gpu(tmp_path):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_gpu_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    for r in res:
+        assert r["ranks"] and r["errors"] and r["isets"] and r["jsets"] and r["qosc"], r
+    assert res[0]["linkdims"] == res[1]["linkdims"]
