@@ -48,6 +48,81 @@ __global__ void k_trsm_cols_upper(double* __restrict__ U, int64_t ldu, int n, in
     }
 }
 
+// Blocked form of both triangular solves for np <= kTrsmMaxNp: a workgroup keeps kTrsmRhs
+// right-hand sides (rows of L21 / columns of U12) x np in LDS and walks 16-column blocks from the
+// right: solve the block's unit-triangular diagonal part per right-hand side, then subtract the
+// block's contribution from every column to its left in parallel (right-looking). Same
+// recurrence X[., j] = B[., j] - sum_{t > j} X[., t] coef(t, j) as the one-thread-per-row
+// kernels, in block order.
+//   LOWER (leftorth): X(r, j) = L[r + j ld], coef(t, j) = L[t + j ld]
+//   upper (!leftorth): X(c, j) = U[j + c ld], coef(t, j) = U[j + t ld]
+constexpr int kTrsmRhs = 32;
+constexpr int kTrsmBlk = 16;
+constexpr int kTrsmMaxNp = 512;
+
+template <bool LOWER>
+__global__ __launch_bounds__(256) void k_trsm_blocked(double* __restrict__ Mx, int64_t ld, int rhs0,
+                                                      int rhs1, int np) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* Xs = reinterpret_cast<double*>(smem);  // [j][r], r fastest
+    const int r0 = rhs0 + blockIdx.x * kTrsmRhs;
+    const int nr = min(kTrsmRhs, rhs1 - r0);
+    auto X = [&](int r, int j) -> double& {
+        return LOWER ? Mx[(int64_t)(r0 + r) + (int64_t)j * ld] : Mx[(int64_t)j + (int64_t)(r0 + r) * ld];
+    };
+    auto coef = [&](int t, int j) -> double {
+        return LOWER ? Mx[(int64_t)t + (int64_t)j * ld] : Mx[(int64_t)j + (int64_t)t * ld];
+    };
+    for (int e = threadIdx.x; e < kTrsmRhs * np; e += blockDim.x) {
+        const int r = e % kTrsmRhs, j = e / kTrsmRhs;
+        Xs[e] = r < nr ? X(r, j) : 0.0;
+    }
+    __syncthreads();
+    for (int jb = ((np - 1) / kTrsmBlk) * kTrsmBlk; jb >= 0; jb -= kTrsmBlk) {
+        const int je = min(jb + kTrsmBlk, np);
+        if (threadIdx.x < kTrsmRhs) {
+            const int r = threadIdx.x;
+            for (int j = je - 1; j >= jb; --j) {
+                double s = Xs[j * kTrsmRhs + r];
+                for (int t = j + 1; t < je; ++t)
+                    s = __dsub_rn(s, __dmul_rn(Xs[t * kTrsmRhs + r], coef(t, j)));
+                Xs[j * kTrsmRhs + r] = s;
+            }
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < kTrsmRhs * jb; e += blockDim.x) {
+            const int r = e % kTrsmRhs, j = e / kTrsmRhs;
+            double s = Xs[e];
+            for (int t = jb; t < je; ++t) s = __dsub_rn(s, __dmul_rn(Xs[t * kTrsmRhs + r], coef(t, j)));
+            Xs[e] = s;
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < kTrsmRhs * np; e += blockDim.x) {
+        const int r = e % kTrsmRhs, j = e / kTrsmRhs;
+        if (r < nr) X(r, j) = Xs[e];
+    }
+}
+
+template <bool LOWER>
+static void launch_trsm(hipStream_t s, double* Mx, int64_t ld, int rhs0, int rhs1, int np) {
+    if (rhs1 <= rhs0) return;
+    if (np > kTrsmMaxNp) {
+        if (LOWER)
+            hipLaunchKernelGGL(k_trsm_rows_lower, dim3((rhs1 - rhs0 + 127) / 128), dim3(128), 0, s, Mx, ld,
+                               rhs1, np);
+        else
+            hipLaunchKernelGGL(k_trsm_cols_upper, dim3((rhs1 - rhs0 + 127) / 128), dim3(128), 0, s, Mx, ld,
+                               rhs1, np);
+        return;
+    }
+    const size_t bytes = (size_t)kTrsmRhs * np * sizeof(double);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm_blocked<LOWER>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    hipLaunchKernelGGL(k_trsm_blocked<LOWER>, dim3((rhs1 - rhs0 + kTrsmRhs - 1) / kTrsmRhs), dim3(256),
+                       bytes, s, Mx, ld, rhs0, rhs1, np);
+}
+
 // left (m x np, ld m) scatter for leftorth: out[rowperm[i], j] = i < np ? (i==j) : X[i,j]
 __global__ void k_left_scatter_lo(const double* __restrict__ L, int64_t ldl, int m, int np,
                                   const int64_t* __restrict__ rowperm, double* __restrict__ out) {
@@ -115,9 +190,7 @@ void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64
             hipLaunchKernelGGL(k_right_gemm_lo, dim3(grid_for((long long)np * n, 8192)), dim3(256),
                                0, s, L, ldl, U, ldu, n, np, colperm, right);
         if (left) {
-            if (m > np)
-                hipLaunchKernelGGL(k_trsm_rows_lower, dim3((m - np + 127) / 128), dim3(128), 0, s, L,
-                                   ldl, m, np);
+            launch_trsm<true>(s, L, ldl, np, m, np);
             hipLaunchKernelGGL(k_left_scatter_lo, dim3(grid_for((long long)m * np, 8192)), dim3(256),
                                0, s, L, ldl, m, np, rowperm, left);
         }
@@ -126,9 +199,7 @@ void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64
             hipLaunchKernelGGL(k_left_gemm_ro, dim3(grid_for((long long)m * np, 8192)), dim3(256), 0,
                                s, L, ldl, U, ldu, m, np, rowperm, left);
         if (right) {
-            if (n > np)
-                hipLaunchKernelGGL(k_trsm_cols_upper, dim3((n - np + 127) / 128), dim3(128), 0, s, U,
-                                   ldu, n, np);
+            launch_trsm<false>(s, U, ldu, np, n, np);
             hipLaunchKernelGGL(k_right_scatter_ro, dim3(grid_for((long long)np * n, 8192)),
                                dim3(256), 0, s, U, ldu, n, np, colperm, right);
         }
