@@ -41,6 +41,12 @@ struct tci_ctx {
     int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
+    int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
+    int ncu = 0;           // compute units of the device
+    double* colbuf = nullptr;  // mid path: published candidate columns
+    size_t capColbuf = 0;
+    unsigned* bar = nullptr;   // mid path: grid-barrier counter
+    int* fault = nullptr;      // mid path: barrier timeout flag
     int* flag = nullptr;
     unsigned* ticket = nullptr;  // rrLU pass tail hand-off counter (zero between passes)
     char* hin = nullptr;         // pinned staging for uploads / downloads of the small path
@@ -284,6 +290,21 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;  // matrixlu.jl:391-393
         return TCI_OK;
     }
+    if (c->mid_path && c->ncu > 0 && tci::rrlu_mid_fits(m, n, c->ncu)) {
+        // the matrix resident in the LDS of a persistent grid: one launch, one barrier per pivot
+        const int64_t G = std::min<int64_t>(std::min(c->ncu, 256), n);
+        if ((st = ensure(c, &c->colbuf, &c->capColbuf, (size_t)(G * m)))) return st;
+        HIPCHK(c, tci::launch_rrlu_mid(c->stream, c->ncu, dA, lda, mi, ni, (int)mr, reltol, abstol,
+                                       leftorth, c->st, c->rowperm, c->colperm, c->pivv, c->Lp, m, c->Up,
+                                       c->ldUp, c->cand, c->colbuf, c->bar, c->fault));
+        HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->hflag, c->fault, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (*c->hflag) return set_err(c, TCI_ERR_DEVICE, "rrlu: grid barrier timed out (mid-size path)");
+        *np_out = c->hst->np;
+        *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;
+        return TCI_OK;
+    }
     // pending rank-1 updates, slot-major: X[s * ldx + i] (slot s, physical row i), Y[s * ldy + j];
     // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
     const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
@@ -486,6 +507,14 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->ncu = prop.multiProcessorCount;
+        int coop = 0;
+        if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop)
+            c->mid_path = 0;
+    }
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -495,6 +524,8 @@ int tci_ctx_create(int device, tci_ctx** out) {
               hipHostMalloc((void**)&c->hst, sizeof(RrluState), 0) == hipSuccess &&
               hipMalloc((void**)&c->flag, sizeof(int)) == hipSuccess &&
               hipMalloc((void**)&c->ticket, sizeof(unsigned)) == hipSuccess &&
+              hipMalloc((void**)&c->bar, sizeof(unsigned)) == hipSuccess &&
+              hipMalloc((void**)&c->fault, sizeof(int)) == hipSuccess &&
               hipMemset(c->ticket, 0, sizeof(unsigned)) == hipSuccess &&
               hipHostMalloc((void**)&c->hflag, sizeof(int), 0) == hipSuccess &&
               hipMalloc((void**)&c->maxbits, sizeof(unsigned long long)) == hipSuccess &&
@@ -512,7 +543,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     auto fr = [](void* p) { if (p) hipFree(p); };
     fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
-    fr(c->ticket);
+    fr(c->ticket); fr(c->bar); fr(c->fault); fr(c->colbuf);
     fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
     fr(c->dU);
@@ -543,6 +574,13 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
 
 int tci_set_rrlu_small(tci_ctx* c, int enabled) {
     c->small_path = enabled != 0;
+    return TCI_OK;
+}
+
+int tci_set_rrlu_mid(tci_ctx* c, int enabled) {
+    int coop = 0;
+    hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device);
+    c->mid_path = enabled != 0 && coop;
     return TCI_OK;
 }
 

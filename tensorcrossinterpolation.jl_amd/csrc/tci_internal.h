@@ -111,6 +111,13 @@ struct SmallOut {
     unsigned long long* maxout;
 };
 bool rrlu_small_fits(int64_t m, int64_t n);
+// mid-size matrices: persistent cooperative grid (one workgroup per CU, matrix in LDS), one grid
+// barrier per pivot. colbuf: min(ncu, 256) x m doubles; count / fault: device words.
+bool rrlu_mid_fits(int64_t m, int64_t n, int ncu);
+hipError_t launch_rrlu_mid(hipStream_t s, int ncu, const double* A, int64_t lda, int m, int n, int mr,
+                           double reltol, double abstol, int leftorth, RrluState* st, int64_t* rowphys,
+                           int64_t* colphys, double* pivvals, double* Lp, int64_t ldl, double* Up,
+                           int64_t ldu, Cand* cand, double* colbuf, unsigned* count, int* fault);
 hipError_t launch_rrlu_small(hipStream_t s, const double* A, int64_t lda, int m, int n, int mr,
                              double reltol, double abstol, int leftorth, RrluState* st,
                              int64_t* rowphys, int64_t* colphys, double* pivvals, double* Lp,

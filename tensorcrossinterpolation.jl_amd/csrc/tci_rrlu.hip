@@ -451,7 +451,16 @@ void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* r
 // LDS and runs _optimizerrlu! (matrixlu.jl:346-369) as written: argmax over the trailing block
 // (column-major scan order as the tie-break), stop test, swaprow!/swapcol! (physical, in LDS),
 // true-division normalisation and the rank-1 update with separate multiply and subtract.
-constexpr int kSmallThreads = 1024;
+#ifndef TCI_SMALL_THREADS
+#define TCI_SMALL_THREADS 1024
+#endif
+constexpr int kSmallThreads = TCI_SMALL_THREADS;
+struct SmallCand {
+    double v;
+    unsigned key;
+    unsigned pad;
+    double val;
+};
 constexpr int64_t kSmallElems = 16384;  // 128 KiB of fp64 in LDS
 constexpr int64_t kSmallPerm = 2048;    // m + n
 
@@ -491,22 +500,38 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     __syncthreads();
     // argmax of abs2 over the trailing block (submatrixargmax, matrixlu.jl:46-87): the candidate
     // order (value, column, row) is the reference's column-major scan with strict '>'
-    CandR best = cand_none();
+    // a candidate is (abs2, key = column << 16 | row): larger abs2 wins, then the smaller key
+    double bv = -1.0;
+    unsigned bk = 0xffffffffu;
+    auto take = [&](double a2, unsigned key) {
+        const bool better = (a2 > bv) || (a2 == bv && key < bk);  // NaN never wins
+        bv = better ? a2 : bv;
+        bk = better ? key : bk;
+    };
     for (int j = w; j < n; j += NW)
         for (int i = l; i < m; i += 64) {
             const double v = S[i + j * m];
-            const double a2 = __dmul_rn(v, v);
-            if (cand_better(a2, j, i, best.v, best.cpos, best.rpos)) best = CandR{a2, v, j, i, j, i};
+            take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
         }
+    SmallCand* red2 = reinterpret_cast<SmallCand*>(red);
     for (int k = 0; k < mr; ++k) {
-        wave_reduce_cand(best);
-        if (l == 0) red[w] = best;
-        __syncthreads();
-        CandR b = red[0];
 #pragma unroll
-        for (int i = 1; i < NW; ++i) cand_take(b, red[i]);
-        int p = b.rpos, q = b.cpos;
-        double val = b.val;  // the candidate carries A[p, q] (read before any thread swaps)
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ov = __shfl_xor(bv, off);
+            const unsigned ok = __shfl_xor(bk, off);
+            take(ov, ok);
+        }
+        if (l == 0)  // the wave's winner and its value (no swap can be under way here)
+            red2[w] = SmallCand{bv, bk, 0u, bv >= 0.0 ? S[(bk & 0xffffu) + (bk >> 16) * m] : 0.0};
+        __syncthreads();
+        SmallCand b = red2[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            const SmallCand o = red2[i];
+            if ((o.v > b.v) || (o.v == b.v && o.key < b.key)) b = o;
+        }
+        int p = (int)(b.key & 0xffffu), q = (int)(b.key >> 16);
+        double val = b.val;
         if (!(b.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
             p = q = k;
             val = S[k + k * m];
@@ -557,7 +582,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
         }
         __syncthreads();
         // rank-1 update (mul then sub, matrixlu.jl:314-320) fused with the next pivot's argmax
-        best = cand_none();
+        bv = -1.0;
+        bk = 0xffffffffu;
         for (int j = w; j < n; j += NW) {
             if (j <= k) continue;
             const double y = yv[j];
@@ -565,8 +591,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
                 if (i <= k) continue;
                 const double v = __dsub_rn(S[i + j * m], __dmul_rn(xv[i], y));
                 S[i + j * m] = v;
-                const double a2 = __dmul_rn(v, v);
-                if (cand_better(a2, j, i, best.v, best.cpos, best.rpos)) best = CandR{a2, v, j, i, j, i};
+                take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
             }
         }
     }
@@ -677,6 +702,260 @@ hipError_t launch_rrlu_small(hipStream_t s, const double* A, int64_t lda, int m,
                        reltol, abstol, leftorth, st, rowphys, colphys, pivvals, Lp, ldl, Up, ldu,
                        out);
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------ mid-size rrLU
+// Pi matrices of a few MiB (C3': 1024^2 at rank 64) are too big for one workgroup's LDS and too
+// small for the pass pipeline, whose ~16 us per pivot is a chain of dependent memory round trips
+// plus a launch. Here the matrix lives in the LDS of a persistent cooperative grid (one
+// workgroup per CU), split by column blocks; each pivot costs one grid barrier:
+//   1. every workgroup publishes its local argmax candidate and that candidate's (current,
+//      updated) column (sc1 stores), then arrives at the barrier (agent-scope atomic counter);
+//   2. every workgroup reduces the candidates to the same winner (reference tie order), applies
+//      the stop test, swaprow!(k, p) on its own columns, swapcol!(k, q) on the replicated column
+//      position maps, and takes the pivot column from the winner's published copy;
+//   3. normalisation and the rank-1 update of its own trailing columns, fused with the next
+//      local argmax.
+// Same arithmetic as the reference (separate multiply / subtract, true division): bitwise equal
+// to the other paths. Outputs in the pass pipeline's conventions.
+constexpr int kMidThreads = 256;
+constexpr int kMidMaxGrid = 256;
+constexpr size_t kMidLds = 150 * 1024;
+
+struct MidArgs {
+    const double* A;
+    int64_t lda;
+    int m, n, mr, ncl, leftorth;
+    double reltol, abstol;
+    RrluState* st;
+    int64_t* rowphys;
+    int64_t* colphys;
+    double* pivvals;
+    double* Lp;
+    int64_t ldl;
+    double* Up;
+    int64_t ldu;
+    Cand* cand;       // one per workgroup
+    double* colbuf;   // gridDim.x x m: the published candidate columns
+    unsigned* count;  // barrier arrivals (monotonic; zeroed before launch)
+    int* fault;       // set on a barrier timeout
+};
+
+static size_t mid_lds_bytes(int m, int n, int ncl) {
+    return ((size_t)m * ncl * 8 + 15) / 16 * 16 + (size_t)m * 8 + ((size_t)(2 * n + m) * 4 + 15) / 16 * 16 +
+           (kMidThreads / 64) * sizeof(CandR) + 64;
+}
+
+// grid-wide barrier on a monotonic arrival counter: barrier number e completes at
+// (e + 1) * gridDim.x arrivals. Every wave drains its stores first (hand-off table, row 1).
+__device__ __forceinline__ bool mid_grid_sync(unsigned* count, unsigned& epoch, int* fault, int* lflag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned target = (epoch + 1) * gridDim.x;
+        const unsigned old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int bad = 0;
+        if (old + 1 < target) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24) ||
+                    __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    bad = 1;  // a peer is missing or has failed: give up instead of hanging
+                    __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        *lflag = bad;
+    }
+    ++epoch;
+    __syncthreads();
+    return *lflag == 0;
+}
+
+__global__ __launch_bounds__(kMidThreads) void k_rrlu_mid(MidArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int m = g.m, n = g.n, ncl = g.ncl;
+    const int c0 = blockIdx.x * ncl;
+    const int nc = max(0, min(ncl, n - c0));  // local columns: global c0 .. c0 + nc - 1
+    double* S = reinterpret_cast<double*>(smem);  // m x ncl, ld m
+    double* xv = reinterpret_cast<double*>(smem + ((size_t)m * ncl * 8 + 15) / 16 * 16);
+    int* cpos = reinterpret_cast<int*>(xv + m);  // replicated column position map (n)
+    int* cphys = cpos + n;                       // its inverse (n)
+    int* rperm = cphys + n;                      // row permutation (m), identical everywhere
+    CandR* red = reinterpret_cast<CandR*>(reinterpret_cast<char*>(cpos) +
+                                          ((size_t)(2 * n + m) * 4 + 15) / 16 * 16);
+    int* ctl = reinterpret_cast<int*>(red + kMidThreads / 64);
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    for (int e = tid; e < m * nc; e += kMidThreads)
+        S[e] = g.A[(e % m) + (int64_t)(c0 + e / m) * g.lda];
+    for (int j = tid; j < n; j += kMidThreads) {
+        cpos[j] = j;
+        cphys[j] = j;
+    }
+    for (int i = tid; i < m; i += kMidThreads) rperm[i] = i;
+    double maxerror = 0.0, error = __longlong_as_double(0x7ff8000000000000LL);
+    int np = 0;
+    unsigned epoch = 0;
+    __syncthreads();
+    // local argmax of the initial matrix
+    CandR best = cand_none();
+    for (int j = w; j < nc; j += kMidThreads / 64)
+        for (int i = l; i < m; i += 64) {
+            const double v = S[i + j * m];
+            const double a2 = __dmul_rn(v, v);
+            if (cand_better(a2, cpos[c0 + j], i, best.v, best.cpos, best.rpos))
+                best = CandR{a2, v, cpos[c0 + j], i, c0 + j, i};
+        }
+    for (int k = 0; k < g.mr; ++k) {
+        // 1. publish the local candidate and its column
+        wave_reduce_cand(best);
+        if (l == 0) red[w] = best;
+        __syncthreads();
+        if (tid == 0) {
+            CandR b = red[0];
+            for (int i = 1; i < kMidThreads / 64; ++i) cand_take(b, red[i]);
+            store_cand_sc1(g.cand + blockIdx.x, b);
+            ctl[0] = b.v >= 0.0 ? b.pc - c0 : -1;
+        }
+        __syncthreads();
+        if (ctl[0] >= 0) {
+            const double* col = S + (int64_t)ctl[0] * m;
+            double* dst = g.colbuf + (int64_t)blockIdx.x * m;
+            for (int i = tid; i < m; i += kMidThreads)
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + i), (uint64_t)__double_as_longlong(col[i]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!mid_grid_sync(g.count, epoch, g.fault, ctl + 4)) return;
+        // 2. the same winner everywhere
+        CandR b = cand_none();
+        for (int i = tid; i < (int)gridDim.x; i += kMidThreads) cand_take(b, load_cand_sc1(g.cand + i));
+        wave_reduce_cand(b);
+        __syncthreads();  // red reuse
+        if (l == 0) red[w] = b;
+        __syncthreads();
+        b = red[0];
+        for (int i = 1; i < kMidThreads / 64; ++i) cand_take(b, red[i]);
+        int p = b.rpos, q = b.pc;  // row position (= physical LDS row), global column
+        double val = b.val;
+        const bool allnan = !(b.v >= 0.0);
+        if (allnan) {  // every trailing value NaN: Julia keeps (k, k); the pivot column is NaN there
+            p = k;
+            q = cphys[k];
+            val = __longlong_as_double(0x7ff8000000000000LL);
+        }
+        error = fabs(val);
+        if (((fabs(error) < g.reltol * maxerror) || (fabs(error) < g.abstol)) && k > 0) break;
+        maxerror = jl_max(maxerror, error);
+        np = k + 1;
+        if (blockIdx.x == 0 && tid == 0) g.pivvals[k] = val;
+        // pivot column (pre-swap rows) from the winner's copy; its rows k and p trade places below
+        const int owner = q / ncl;
+        // (all-NaN case: only rows >= k are used, and there every value is NaN)
+        for (int i = tid; i < m; i += kMidThreads)
+            xv[i] = allnan ? __longlong_as_double(0x7ff8000000000000LL)
+                           : __longlong_as_double((long long)__hip_atomic_load(
+                                 reinterpret_cast<const uint64_t*>(g.colbuf + (int64_t)owner * m + i),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __syncthreads();
+        if (tid == 0 && p != k) {
+            const double t = xv[k];
+            xv[k] = xv[p];
+            xv[p] = t;
+            const int r = rperm[k];
+            rperm[k] = rperm[p];
+            rperm[p] = r;
+        }
+        // swaprow!(k, p) on the local columns
+        if (p != k)
+            for (int j = tid; j < nc; j += kMidThreads) {
+                const double t = S[k + j * m];
+                S[k + j * m] = S[p + j * m];
+                S[p + j * m] = t;
+            }
+        // swapcol!(k, q): positions only
+        if (tid == 0) {
+            const int cq = cpos[q], ck = cphys[k];
+            cphys[k] = q;
+            cphys[cq] = ck;
+            cpos[q] = k;
+            cpos[ck] = cq;
+        }
+        __syncthreads();
+        // 3. normalisation (matrixlu.jl:300-305): the L column in xv (and in the owner's S), the
+        // U row in place
+        const double piv = xv[k];
+        if (g.leftorth)
+            for (int i = k + 1 + tid; i < m; i += kMidThreads) xv[i] = xv[i] / piv;
+        for (int j = tid; j < nc; j += kMidThreads)
+            if (cpos[c0 + j] > k && !g.leftorth) S[k + j * m] = S[k + j * m] / piv;
+        __syncthreads();
+        if (q >= c0 && q < c0 + nc)  // the owner's pivot column becomes L column k
+            for (int i = k + tid; i < m; i += kMidThreads) S[i + (q - c0) * m] = xv[i];
+        // rank-1 update of the local trailing columns fused with the next local argmax
+        best = cand_none();
+        for (int j = w; j < nc; j += kMidThreads / 64) {
+            const int cp = cpos[c0 + j];
+            if (cp <= k) continue;
+            const double y = S[k + j * m];
+            for (int i = l; i < m; i += 64) {
+                if (i <= k) continue;
+                const double v = __dsub_rn(S[i + j * m], __dmul_rn(xv[i], y));
+                S[i + j * m] = v;
+                const double a2 = __dmul_rn(v, v);
+                if (cand_better(a2, cp, i, best.v, best.cpos, best.rpos)) best = CandR{a2, v, cp, i, c0 + j, i};
+            }
+        }
+        __syncthreads();
+    }
+    // outputs: state, permutations (workgroup 0), L columns / U rows of the local columns
+    if (blockIdx.x == 0) {
+        if (tid == 0) {
+            g.st->np = np;
+            g.st->done = 1;
+            g.st->maxerror = maxerror;
+            g.st->error = error;
+        }
+        for (int i = tid; i < m; i += kMidThreads) g.rowphys[i] = rperm[i];
+        for (int j = tid; j < n; j += kMidThreads) g.colphys[j] = cphys[j];
+    }
+    for (int j = 0; j < nc; ++j) {
+        const int pos = cpos[c0 + j];
+        if (pos < np)
+            for (int i = pos + 1 + tid; i < m; i += kMidThreads) g.Lp[rperm[i] + (int64_t)pos * g.ldl] = S[i + j * m];
+        for (int t = tid; t < min(np, pos); t += kMidThreads) g.Up[t + (int64_t)(c0 + j) * g.ldu] = S[t + j * m];
+    }
+}
+
+bool rrlu_mid_fits(int64_t m, int64_t n, int ncu) {
+    if (m <= 0 || n <= 0 || m * n > (int64_t)1 << 21) return false;
+    const int G = (int)std::min<int64_t>(std::min(ncu, kMidMaxGrid), n);
+    const int ncl = (int)((n + G - 1) / G);
+    return mid_lds_bytes((int)m, (int)n, ncl) <= kMidLds;
+}
+
+hipError_t launch_rrlu_mid(hipStream_t s, int ncu, const double* A, int64_t lda, int m, int n, int mr,
+                           double reltol, double abstol, int leftorth, RrluState* st, int64_t* rowphys,
+                           int64_t* colphys, double* pivvals, double* Lp, int64_t ldl, double* Up,
+                           int64_t ldu, Cand* cand, double* colbuf, unsigned* count, int* fault) {
+    const int G = std::min(std::min(ncu, kMidMaxGrid), n);
+    MidArgs g{A, lda, m, n, mr, (n + G - 1) / G, leftorth, reltol, abstol, st, rowphys, colphys, pivvals,
+              Lp, ldl, Up, ldu, cand, colbuf, count, fault};
+    const size_t bytes = mid_lds_bytes(m, n, g.ncl);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rrlu_mid),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_rrlu_mid),
+                                                     kMidThreads, bytes);
+    if (e != hipSuccess) return e;
+    if ((int64_t)per_cu * ncu < G) return hipErrorCooperativeLaunchTooLarge;
+    if ((e = hipMemsetAsync(count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(fault, 0, sizeof(int), s)) != hipSuccess) return e;
+    void* args[] = {&g};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_rrlu_mid), dim3(G), dim3(kMidThreads),
+                                      args, (unsigned)bytes, s);
 }
 
 // ------------------------------------------------------------ extraction

@@ -16,12 +16,14 @@ pytestmark = pytest.mark.gpu
 T = pytest.importorskip("tci_amd")
 
 
-@pytest.fixture(scope="module", params=["small", "pipeline"])
+@pytest.fixture(scope="module", params=["default", "mid", "pipeline"])
 def ctx(request):
-    """Every test runs twice: with the single-workgroup LDS rrLU for small matrices (the default)
-    and with the pass pipeline forced for every size."""
+    """Every test runs three times: with the default size-based choice of rrLU path (one-workgroup
+    LDS kernel for small Pi, persistent grid for mid-size Pi, the pass pipeline above), with the
+    mid-size path for everything it fits, and with the pass pipeline forced for every size."""
     c = T.Context(0)
-    c.check(c.lib.tci_set_rrlu_small(c.h, int(request.param == "small")))
+    c.check(c.lib.tci_set_rrlu_small(c.h, int(request.param == "default")))
+    c.check(c.lib.tci_set_rrlu_mid(c.h, int(request.param != "pipeline")))
     yield c
     c.close()
 
