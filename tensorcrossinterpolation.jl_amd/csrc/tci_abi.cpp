@@ -113,9 +113,11 @@ struct tci_func {
     int64_t* dstrides = nullptr;
     int64_t nparams = 0;
     int32_t cpK = 0;
+    int64_t ntab = 0;
     FuncDev view() const {
         FuncDev f;
         f.cpK = cpK;
+        f.ntab = ntab;
         f.kind = kind;
         f.L = L;
         f.localdims = dld;
@@ -627,6 +629,11 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
     f->ctx = c;
     f->kind = kind;
     f->cpK = cpK;
+    if (kind == TCI_F_LORENTZ) {  // quotient table p0 / (s + 1) for every reachable s
+        int64_t smax = 0;
+        for (int t = 0; t < L; ++t) smax += (int64_t)localdims[t] * localdims[t];
+        f->ntab = smax < (1 << 20) ? smax + 1 : 0;
+    }
     f->L = L;
     f->localdims.assign(localdims, localdims + L);
     f->nparams = nparams;
@@ -660,8 +667,15 @@ int tci_batcheval_d(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, 
                     double* maxabs) {
     if (!c || !f) return TCI_ERR_ARG;
     int st;
-    if ((st = upload_index(c, &c->dI, &c->capI, I, m, nl))) return st;
-    if ((st = upload_index(c, &c->dJ, &c->capJ, J, n, nr))) return st;
+    // both index tables up through one pinned stage (pageable copies would stage twice)
+    const size_t bi = (size_t)std::max<int64_t>(m * nl, 0) * 4, bj = (size_t)std::max<int64_t>(n * nr, 0) * 4;
+    if ((st = ensure(c, &c->dI, &c->capI, std::max<size_t>(bi / 4, 1)))) return st;
+    if ((st = ensure(c, &c->dJ, &c->capJ, std::max<size_t>(bj / 4, 1)))) return st;
+    if ((st = ensure_pinned(c, &c->hin, &c->capHin, bi + bj + 16))) return st;
+    if (bi) memcpy(c->hin, I, bi);
+    if (bj) memcpy(c->hin + bi, J, bj);
+    if (bi) HIPCHK(c, hipMemcpyAsync(c->dI, c->hin, bi, hipMemcpyHostToDevice, c->stream));
+    if (bj) HIPCHK(c, hipMemcpyAsync(c->dJ, c->hin + bi, bj, hipMemcpyHostToDevice, c->stream));
     return batcheval_device(c, f, c->dI, m, nl, c->dJ, n, nr, M, d_out, ldo, maxabs);
 }
 

@@ -385,29 +385,36 @@ __global__ void k_state_cols(FuncDev f, const int32_t* __restrict__ J, int n, in
     }
 }
 
-__device__ __forceinline__ double combine(const FuncDev& f, St r, St c, int nr) {
-    const double* p = f.params;
-    switch (f.kind) {
-    case F_SUM:
-        return (double)(r.i + c.i);
-    case F_LORENTZ:
-        return p[0] / (double)(r.i + c.i + 1);
-    case F_TABLE:
-        return p[r.i + c.i];
-    case F_GAUSS:
-        return exp(-(p[0] * __dadd_rn(r.d, c.d)));
-    case F_QOSC: {
-        const uint64_t idx = ((uint64_t)r.i << nr) | (uint64_t)c.i;
-        const double x = ldexp((double)idx, -f.L);
-        return exp(-(p[0] * x)) * sin(p[1] * pow(x, p[2]));
+// value of one Pi element from its row and column states. Lorentzian: the quotient
+// p0 / (s + 1) of the integer sum of squares s comes from a table of the same quotients
+// (s <= sum_t d_t^2): bitwise the same division, no per-element fp64 divide.
+template <int KIND>
+__device__ __forceinline__ double combine(const double* __restrict__ p, double p0, St r, St c, int nr,
+                                          int L, const double* __restrict__ tab, int64_t ntab) {
+    if (KIND == F_SUM) return (double)(r.i + c.i);
+    if (KIND == F_LORENTZ) {
+        const int64_t s = r.i + c.i;
+        return s < ntab ? tab[s] : p0 / (double)(s + 1);
     }
-    case F_QEXP: {
+    if (KIND == F_TABLE) return p[r.i + c.i];
+    if (KIND == F_GAUSS) return exp(-(p0 * __dadd_rn(r.d, c.d)));
+    if (KIND == F_QOSC) {
         const uint64_t idx = ((uint64_t)r.i << nr) | (uint64_t)c.i;
-        const double x = ldexp((double)idx, -f.L);
-        return __dadd_rn(p[0] * exp(-(p[1] * x)), p[2] * exp(-(p[3] * x)));
+        const double x = ldexp((double)idx, -L);
+        return exp(-(p0 * x)) * sin(p[1] * pow(x, p[2]));
     }
+    if (KIND == F_QEXP) {
+        const uint64_t idx = ((uint64_t)r.i << nr) | (uint64_t)c.i;
+        const double x = ldexp((double)idx, -L);
+        return __dadd_rn(p0 * exp(-(p[1] * x)), p[2] * exp(-(p[3] * x)));
     }
     return 0.0;
+}
+
+__global__ void k_lorentz_table(FuncDev f, double* __restrict__ tab, int64_t ntab) {
+    const double p0 = f.params[0];
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ntab; s += (int64_t)gridDim.x * blockDim.x)
+        tab[s] = p0 / (double)(s + 1);
 }
 
 __device__ __forceinline__ void block_maxabs(double v, unsigned long long* maxbits) {
@@ -429,22 +436,49 @@ __device__ __forceinline__ void block_maxabs(double v, unsigned long long* maxbi
     }
 }
 
-// Stage 2: out[R + ldo*j]; a block covers 256 consecutive rows of one or more columns.
+// Stage 2: out[R + ldo*j]. A tile is 512 rows (2 per lane: one 16-B store when ldo is even) x
+// kAsmCols columns; a lane loads its two row states once per tile.
+constexpr int kAsmCols = 8;
+
+template <int KIND>
 __global__ __launch_bounds__(256) void k_assemble(FuncDev f, const St* __restrict__ rs,
                                                   const St* __restrict__ cs, int64_t mR, int n,
                                                   int nr, double* __restrict__ out, int64_t ldo,
-                                                  unsigned long long* maxbits) {
+                                                  unsigned long long* maxbits, const double* __restrict__ tab,
+                                                  int64_t ntab, int vec) {
+    const double* p = f.params;
+    const double p0 = (KIND == F_SUM || KIND == F_TABLE) ? 0.0 : p[0];
     double mx = 0.0;
-    const int64_t rtiles = (mR + 255) / 256;
-    const int64_t ntiles = rtiles * n;
+    const int64_t rtiles = (mR + 511) / 512;
+    const int64_t ntiles = rtiles * ((n + kAsmCols - 1) / kAsmCols);
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int64_t R = (t % rtiles) * 256 + threadIdx.x;
-        const int j = (int)(t / rtiles);
-        if (R < mR) {
-            const double v = combine(f, rs[R], cs[j], nr);
-            out[R + ldo * j] = v;
-            const double av = fabs(v);
-            mx = (isnan(av) || av > mx) ? av : mx;
+        const int64_t R = (t % rtiles) * 512 + 2 * threadIdx.x;
+        const int j0 = (int)(t / rtiles) * kAsmCols;
+        const bool h0 = R < mR, h1 = R + 1 < mR;
+        if (!h0) continue;
+        St r0 = rs[R], r1;
+        r1.i = 0;
+        if (h1) r1 = rs[R + 1];
+        const int je = min(j0 + kAsmCols, n);
+        for (int j = j0; j < je; ++j) {
+            const St c = cs[j];
+            const double v0 = combine<KIND>(p, p0, r0, c, nr, f.L, tab, ntab);
+            double* o = out + R + ldo * j;
+            const double a0 = fabs(v0);
+            mx = (isnan(a0) || a0 > mx) ? a0 : mx;
+            if (h1) {
+                const double v1 = combine<KIND>(p, p0, r1, c, nr, f.L, tab, ntab);
+                const double a1 = fabs(v1);
+                mx = (isnan(a1) || a1 > mx) ? a1 : mx;
+                if (vec) {
+                    *reinterpret_cast<double2*>(o) = double2{v0, v1};
+                } else {
+                    o[0] = v0;
+                    o[1] = v1;
+                }
+            } else {
+                o[0] = v0;
+            }
         }
     }
     block_maxabs(mx, maxbits);
@@ -633,7 +667,7 @@ int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n) {
         return 8 * K4 * (cp_ld((int64_t)m * D) + cp_ld(n));
     }
     if (!staged_kind(f.kind)) return 0;
-    return 8 * ((int64_t)m * D + n);
+    return 8 * ((int64_t)m * D + n + (f.kind == F_LORENTZ ? f.ntab : 0));
 }
 
 void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, int nl,
@@ -660,10 +694,24 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
                            D, rs);
         hipLaunchKernelGGL(k_state_cols, dim3(grid_for(n, 4096)), dim3(256), 0, s, f, J, n, nr,
                            f.L - nr, cs);
-        const int64_t ntiles = ((mR + 255) / 256) * n;
+        double* tab = reinterpret_cast<double*>(cs + n);
+        const int64_t ntab = f.kind == F_LORENTZ ? f.ntab : 0;
+        if (ntab > 0)
+            hipLaunchKernelGGL(k_lorentz_table, dim3(grid_for(ntab, 256)), dim3(256), 0, s, f, tab, ntab);
+        const int64_t ntiles = ((mR + 511) / 512) * ((n + kAsmCols - 1) / kAsmCols);
         const int grid = (int)(ntiles < 4096 ? (ntiles > 0 ? ntiles : 1) : 4096);
-        hipLaunchKernelGGL(k_assemble, dim3(grid), dim3(256), 0, s, f, rs, cs, mR, n, nr, out, ldo,
-                           maxbits);
+        const int vec = (ldo % 2 == 0) && ((uintptr_t)out % 16 == 0);
+        switch (f.kind) {
+#define TCI_ASM(K)                                                                                  \
+    case K:                                                                                         \
+        hipLaunchKernelGGL(k_assemble<K>, dim3(grid), dim3(256), 0, s, f, rs, cs, mR, n, nr, out, ldo, \
+                           maxbits, tab, ntab, vec);                                                \
+        break;
+            TCI_ASM(F_SUM) TCI_ASM(F_LORENTZ) TCI_ASM(F_TABLE) TCI_ASM(F_GAUSS) TCI_ASM(F_QOSC)
+            TCI_ASM(F_QEXP)
+#undef TCI_ASM
+        default: break;
+        }
     } else {
         hipLaunchKernelGGL(k_assemble_direct, dim3(grid_for(mR * n, 4096)), dim3(256), 0, s, f, I, m,
                            nl, J, n, nr, M, D, out, ldo, maxbits);

@@ -89,6 +89,7 @@ struct FuncDev {
     int64_t nparams;
     const int64_t* strides;    // device, column-major strides for TCI_F_TABLE
     int32_t cpK;               // number of separable terms (TCI_F_GAUSSMIX, TCI_F_CP), host copy
+    int64_t ntab;              // TCI_F_LORENTZ: quotient table size (max sum of squares + 1), or 0
 };
 
 // ---- rrLU (tci_rrlu.hip)
