@@ -311,6 +311,27 @@ def extras(T, ctx):
     tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)
     res["tci2_config1"] = {"wall_s": round(time.perf_counter() - t0, 4), "ranks": ranks,
                            "final_error": errors[-1], "mode": "nsearchglobalpivot=0"}
+    # other rrLU configurations of SURVEY 8(d): config 2 (4096^2), right-orthogonal pivots, and a
+    # 16384^2 matrix (2 GiB) for the scale curve
+    res["rrlu_configs"] = []
+    for (m2, n2, r2, lo) in ((4096, 4096, 256, True), (8192, 8192, 256, False), (16384, 16384, 256, True)):
+        A = T.DeviceMatrix(m2, n2, ctx=ctx)
+        A.fill_uniform(seed=0)
+        W = T.DeviceMatrix(m2, n2, ctx=ctx)
+        W.copy_from(A)
+        T.rrlu_inplace_device(W, maxrank=r2, leftorthogonal=lo, want_perms=False)
+        ctx.synchronize()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            W.copy_from(A)
+            T.rrlu_inplace_device(W, maxrank=r2, leftorthogonal=lo, want_perms=False)
+        ctx.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        res["rrlu_configs"].append({"m": m2, "n": n2, "r": r2, "leftorthogonal": lo, "ms": round(dt * 1e3, 3),
+                                    "GFLOPs": round(rrlu_flops(m2, n2, r2) / dt / 1e9, 1)})
+        A.free()
+        W.free()
     return res
 
 
