@@ -160,6 +160,14 @@ int tci_sitetensor_h(tci_ctx* ctx, const tci_func* f, const int32_t* Ib, int64_t
 int tci_sitetensor_solve_h(tci_ctx* ctx, const double* P, int64_t r, const double* Pi1, int64_t R,
                            double* T);
 
+/* evaluate(tt, idx) (abstracttensortrain.jl:328-342) of a tensor train at npts points, as the
+ * global pivot search needs it (globalpivotfinder.jl:236): cores packed one after another, core
+ * t being (bonddims[t], dims[t], bonddims[t+1]) column-major (the site tensors of a TensorCI2);
+ * bonddims[0] = bonddims[L] = 1, bond dimensions <= 1024. X: npts x L row-major, 1-based. */
+int tci_tt_evaluate_h(tci_ctx* ctx, int32_t L, const int32_t* dims, const int32_t* bonddims,
+                      const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
+                      double* out);
+
 /* ----------------------------------------------------- synthetic inputs
  * Fills d_A (m x n, ld lda) with U[0,1): splitmix64(seed * 0xD1B54A32D192ED03 + (i + m*j)) >> 11
  * times 2^-53 -- the same stream as the oracle's orc_fill_uniform. */

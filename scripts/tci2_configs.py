@@ -47,6 +47,16 @@ def configs():
                    tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0)
     out["C3_gaussmix20d"] = gaussmix
 
+    def gaussmix_default():
+        rng = np.random.default_rng(3)
+        K = 64
+        centres = rng.uniform(1, 16, (K, 20))
+        f = T.gaussmix([16] * 20, 0.05, centres, np.ones(K))
+        p0 = T.optfirstpivot(f, [16] * 20, [int(round(c)) for c in centres[0]])
+        return run("C3' 20d sum of 64 Gaussians, default global pivot search", f, [16] * 20, [p0],
+                   tolerance=1e-10, maxbonddim=512, rng=np.random.default_rng(0))
+    out["C3_gaussmix20d_default"] = gaussmix_default
+
     def qosc():
         f = T.quantics_osc(40)
         p0 = T.optfirstpivot(f, [2] * 40)

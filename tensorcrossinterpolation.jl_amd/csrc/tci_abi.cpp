@@ -61,6 +61,8 @@ struct tci_ctx {
     unsigned long long* hmaxbits = nullptr;  // pinned
     void* scratch = nullptr;
     size_t capScratch = 0;
+    char* scratch2 = nullptr;  // tensor-train evaluation block
+    size_t capScratch2 = 0;
     int32_t* dI = nullptr;
     size_t capI = 0;
     int32_t* dJ = nullptr;
@@ -546,7 +548,8 @@ int tci_ctx_destroy(tci_ctx* c) {
     auto fr = [](void* p) { if (p) hipFree(p); };
     fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
     fr(c->ticket); fr(c->bar); fr(c->fault); fr(c->colbuf);
-    fr(c->maxbits); fr(c->scratch); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2); fr(c->dDiag);
+    fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
+    fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
     fr(c->dU);
     if (c->hst) hipHostFree(c->hst);
@@ -945,6 +948,46 @@ int tci_sitetensor_solve_h(tci_ctx* c, const double* P, int64_t r, const double*
     tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_tt_evaluate_h(tci_ctx* c, int32_t L, const int32_t* dims, const int32_t* bonddims,
+                      const double* cores, int64_t ncore, const int32_t* X, int64_t npts, double* out) {
+    if (!c || L < 1 || !dims || !bonddims || !cores || (npts > 0 && (!X || !out)))
+        return TCI_ERR_ARG;
+    if (bonddims[0] != 1 || bonddims[L] != 1)
+        return set_err(c, TCI_ERR_ARG, "tt: the first and last bond dimensions must be 1");
+    std::vector<int64_t> off(L + 1, 0);
+    int rmax = 1;
+    for (int t = 0; t < L; ++t) {
+        off[t + 1] = off[t] + (int64_t)bonddims[t] * dims[t] * bonddims[t + 1];
+        rmax = std::max(rmax, (int)bonddims[t + 1]);
+    }
+    if (off[L] > ncore) return set_err(c, TCI_ERR_ARG, "tt: core buffer smaller than the bond dimensions imply");
+    if (rmax > 1024) return set_err(c, TCI_ERR_ARG, "tt: bond dimension above 1024");
+    if (npts == 0) return TCI_OK;
+    // one device block: cores | X | dims, bonddims | offsets | out
+    const size_t bc = (size_t)off[L] * 8, bx = (size_t)(npts * L) * 4, bm = (size_t)(2 * L + 1) * 4,
+                 bo = (size_t)(L + 1) * 8, bout = (size_t)npts * 8;
+    const size_t o1 = round_up(bc, 16), o2 = o1 + round_up(bx, 16), o3 = o2 + round_up(bm, 16),
+                 o4 = o3 + round_up(bo, 16), total = o4 + bout;
+    int st;
+    if ((st = ensure(c, (char**)&c->scratch2, &c->capScratch2, total))) return st;
+    if ((st = ensure_pinned(c, &c->hin, &c->capHin, o4))) return st;
+    memcpy(c->hin, cores, bc);
+    memcpy(c->hin + o1, X, bx);
+    memcpy(c->hin + o2, dims, (size_t)L * 4);
+    memcpy(c->hin + o2 + (size_t)L * 4, bonddims, (size_t)(L + 1) * 4);
+    memcpy(c->hin + o3, off.data(), bo);
+    char* d = c->scratch2;
+    HIPCHK(c, hipMemcpyAsync(d, c->hin, o4, hipMemcpyHostToDevice, c->stream));
+    tci::launch_tt_eval(c->stream, reinterpret_cast<const double*>(d), reinterpret_cast<const int64_t*>(d + o3),
+                        reinterpret_cast<const int32_t*>(d + o2 + (size_t)L * 4),
+                        reinterpret_cast<const int32_t*>(d + o2), L, reinterpret_cast<const int32_t*>(d + o1),
+                        (int)npts, reinterpret_cast<double*>(d + o4), rmax);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(out, d + o4, bout, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }

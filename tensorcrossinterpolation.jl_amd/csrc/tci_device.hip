@@ -718,6 +718,57 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
     }
 }
 
+// ------------------------------------------------ tensor-train evaluation
+// evaluate(tt, idx) = only(prod(T[:, i, :])) (abstracttensortrain.jl:328-342) at many points, for
+// the global pivot search (globalpivotfinder.jl:236): a workgroup carries kTtPts row vectors
+// through the chain of vector-matrix products, one output entry per thread and step, the
+// vectors in LDS. Core t is (r_t, d_t, r_{t+1}) column-major at offset off[t].
+constexpr int kTtPts = 8;
+
+__global__ __launch_bounds__(256) void k_tt_eval(const double* __restrict__ cores,
+                                                 const int64_t* __restrict__ off,
+                                                 const int32_t* __restrict__ rdim,
+                                                 const int32_t* __restrict__ dims, int L,
+                                                 const int32_t* __restrict__ X, int npts,
+                                                 double* __restrict__ out, int rmax) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* v = reinterpret_cast<double*>(smem);  // [pt][rmax]
+    double* w = v + kTtPts * rmax;
+    const int p0 = blockIdx.x * kTtPts;
+    const int np = min(kTtPts, npts - p0);
+    for (int t = 0; t < L; ++t) {
+        const int ra = rdim[t], rb = rdim[t + 1], d = dims[t];
+        const double* core = cores + off[t];
+        for (int e = threadIdx.x; e < np * rb; e += blockDim.x) {
+            const int pt = e / rb, b = e % rb;
+            const int x = X[(int64_t)(p0 + pt) * L + t] - 1;
+            const double* col = core + (int64_t)ra * x + (int64_t)ra * d * b;
+            double s;
+            if (t == 0) {
+                s = col[0];  // r_0 == 1: the row of the first core
+            } else {
+                s = 0.0;
+                for (int a = 0; a < ra; ++a) s = __dadd_rn(s, __dmul_rn(v[pt * rmax + a], col[a]));
+            }
+            w[pt * rmax + b] = s;
+        }
+        __syncthreads();
+        double* tmp = v;
+        v = w;
+        w = tmp;
+    }
+    if (threadIdx.x < np) out[p0 + threadIdx.x] = v[threadIdx.x * rmax];
+}
+
+void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, const int32_t* rdim,
+                    const int32_t* dims, int L, const int32_t* X, int npts, double* out, int rmax) {
+    const size_t bytes = 2 * (size_t)kTtPts * rmax * sizeof(double);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tt_eval), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)bytes);
+    hipLaunchKernelGGL(k_tt_eval, dim3((npts + kTtPts - 1) / kTtPts), dim3(256), bytes, s, cores, off, rdim,
+                       dims, L, X, npts, out, rmax);
+}
+
 // ------------------------------------------------------ site-tensor solve
 // T = Pi1 * P^-1 (tensorci2.jl:626): A = P^T is factorised in place with partial pivoting
 // (first maximal |a| in a column, as getrf/idamax), one workgroup; then each thread solves one

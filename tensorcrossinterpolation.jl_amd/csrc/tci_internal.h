@@ -148,6 +148,10 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
                       unsigned long long* maxbits, void* scratch);
 int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n);
 
+// tensor-train values at npts points (X: npts x L, 1-based); rmax = max bond dimension (<= 1024)
+void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, const int32_t* rdim,
+                    const int32_t* dims, int L, const int32_t* X, int npts, double* out, int rmax);
+
 // site-tensor solve: T (R x r) = Pi1 (R x r) * P^-1; P overwritten by its LU (partial pivot of P^T)
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
                              int* piv);

@@ -42,7 +42,8 @@ class DefaultGlobalPivotFinder(AbstractGlobalPivotFinder):
                     x[p] = v
                     cands.append(x)
         X = np.asarray(cands, np.int32)
-        err = np.abs(f.points(X) - tci.evaluate_many(X))
+        ctx = getattr(f, "ctx", None) or getattr(getattr(f, "local", None), "ctx", None)
+        err = np.abs(f.points(X) - tci.evaluate_many(X, ctx=ctx))
         found = []
         off = 0
         per = sum(localdims)

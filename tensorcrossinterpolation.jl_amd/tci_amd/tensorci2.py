@@ -406,13 +406,20 @@ class TensorCI2:
             v = v @ self.sitetensors[p][:, int(i) - 1, :]
         return float(v[0, 0])
 
-    def evaluate_many(self, X):
-        X = np.asarray(X, np.int64)
-        v = np.ones((len(X), 1))
-        for p in range(len(self)):
-            T = self.sitetensors[p]
-            v = np.einsum("na,anb->nb", v, T[:, X[:, p] - 1, :])
-        return v[:, 0]
+    def evaluate_many(self, X, ctx=None):
+        """evaluate at every row of X in one device call (tci_tt_evaluate_h): the batched
+        tensor-train evaluation of the global pivot search (globalpivotfinder.jl:236)."""
+        X = np.ascontiguousarray(np.asarray(X, np.int32).reshape(-1, len(self)))
+        if len(X) == 0:
+            return np.zeros(0)
+        ctx = ctx or _lib.context()
+        dims = np.asarray(self.localdims, np.int32)
+        bd = np.asarray([self.sitetensors[0].shape[0]] + [T.shape[2] for T in self.sitetensors], np.int32)
+        cores = np.concatenate([np.asarray(T, np.float64).ravel(order="F") for T in self.sitetensors])
+        out = np.zeros(len(X))
+        ctx.check(ctx.lib.tci_tt_evaluate_h(ctx.h, len(self), _lib.ptr(dims), _lib.ptr(bd), _lib.ptr(cores),
+                                            cores.size, _lib.ptr(X), len(X), _lib.ptr(out)))
+        return out
 
     def sum(self):
         v = np.ones((1, 1))

@@ -268,6 +268,22 @@ def _compare_tci(tci, ranks, errors, rt, rranks, rerrors, rtol=1e-10, exact_f=Tr
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-9 * rt.maxsamplevalue)
 
 
+@pytest.mark.parametrize("bd", [[1, 3, 1], [1, 5, 70, 9, 1], [1, 130, 260, 4, 1]])
+def test_tt_evaluate_many_vs_oracle(ctx, bd):
+    # batched tensor-train evaluation (global pivot search) vs the oracle's evaluate chain
+    rng = np.random.default_rng(len(bd) + bd[1])
+    L = len(bd) - 1
+    ld = [3, 4, 2, 5][:L]
+    cores = [rng.random((bd[p], ld[p], bd[p + 1])) - 0.5 for p in range(L)]
+    tci = T.TensorCI2(ld)
+    tci.sitetensors = cores
+    X = np.stack([rng.integers(1, d + 1, 257) for d in ld], axis=1).astype(np.int32)
+    got = tci.evaluate_many(X, ctx=ctx)
+    params = np.concatenate([np.array(bd, float)] + [c.ravel(order="F") for c in cores])
+    ref = np.array([O.feval(7, params, ld, x) for x in X])
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-13 * np.abs(ref).max())
+
+
 def test_tci2_pivoterrors_kat(kats, ctx):
     k = kats["tci2_pivoterrors"]
     M = np.diag(k["diags"])
