@@ -1,0 +1,59 @@
+"""Golden TCI2 results for the BASELINE configurations (scaled where the full size would take the
+CPU oracle minutes), produced by the oracle (pinned by the reference's known-answer tests; the
+reference itself is Julia and cannot run here). Writes tests/golden/config_golden.json.
+
+  python tests/golden/make_config_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import oracle_lib as O  # noqa: E402
+
+QOSC = [10.0, 2 * np.pi * 100, 1.1]
+
+
+def configs():
+    rng = np.random.default_rng(3)
+    centres = rng.uniform(1, 8, (8, 8))
+    gm = np.concatenate([[8, 0.05], centres.ravel(), np.ones(8)]).tolist()
+    g = 0.5 + np.random.default_rng(2).random((16, 6, 8))
+    cp = np.concatenate([[16, 8], g.ravel()]).tolist()
+    return [
+        {"name": "C1_lorentz8d", "kind": 1, "params": [1.0], "localdims": [10] * 8, "initialpivots": None,
+         "kw": {"tolerance": 1e-8}},
+        {"name": "C3_gauss10d_d16", "kind": 3, "params": [0.05, 8.5], "localdims": [16] * 10,
+         "initialpivots": [[8] * 10], "kw": {"tolerance": 1e-10, "maxbonddim": 512}},
+        {"name": "C3p_gaussmix8d_K8", "kind": 4, "params": gm, "localdims": [8] * 8,
+         "initialpivots": [[int(round(c)) for c in centres[0]]], "kw": {"tolerance": 1e-10}},
+        {"name": "C4_qosc40", "kind": 5, "params": QOSC, "localdims": [2] * 40,
+         "initialpivots": [[1] + [2] * 39], "kw": {"tolerance": 1e-8}},
+        {"name": "C5_cp6d_K16", "kind": 8, "params": cp, "localdims": [8] * 6, "initialpivots": [[1] * 6],
+         "kw": {"tolerance": 1e-10}},
+    ]
+
+
+def run(c):
+    t, ranks, errors = O.crossinterpolate2(c["kind"], c["params"], c["localdims"], c["initialpivots"], **c["kw"])
+    L = len(c["localdims"])
+    rng = np.random.default_rng(0)
+    X = np.stack([rng.integers(1, d + 1, 64) for d in c["localdims"]], axis=1).astype(np.int32)
+    return {"ranks": [int(r) for r in ranks], "errors": [float(e) for e in errors],
+            "linkdims": t.linkdims(), "maxsamplevalue": t.maxsamplevalue,
+            "Iset": [t.Iset(p).tolist() for p in range(L)], "Jset": [t.Jset(p).tolist() for p in range(L)],
+            "points": X.tolist(), "values": [t.evaluate(x) for x in X]}
+
+
+if __name__ == "__main__":
+    out = []
+    for c in configs():
+        r = run(c)
+        print(c["name"], r["ranks"], r["errors"][-1])
+        out.append({**c, "result": r})
+    with open(os.path.join(HERE, "config_golden.json"), "w") as fh:
+        json.dump(out, fh)
