@@ -455,6 +455,73 @@ void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* r
 #define TCI_SMALL_THREADS 1024
 #endif
 constexpr int kSmallThreads = TCI_SMALL_THREADS;
+#ifdef TCI_SMALL_PROF
+#define SPROF(i) (prof_t[i] = wall_clock64())
+#else
+#define SPROF(i) ((void)prof_t)
+#endif
+// Argmax reductions on DPP lane moves (VALU, no LDS round trip as ds_bpermute has): a candidate
+// is (abs2 value, key), larger value first, then the smaller key; NaN never wins.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void dpp_take(double& bv, unsigned& bk, double& bx) {
+    const double ov = dpp_f64<CTRL>(bv), ox = dpp_f64<CTRL>(bx);
+    const unsigned ok = (unsigned)__builtin_amdgcn_update_dpp(0, (int)bk, CTRL, 0xf, 0xf, false);
+    const bool better = (ov > bv) || (ov == bv && ok < bk);
+    bv = better ? ov : bv;
+    bk = better ? ok : bk;
+    bx = better ? ox : bx;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// winner of each row of 16 lanes, in every lane of that row (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror)
+__device__ __forceinline__ void row16_argmax_dpp(double& bv, unsigned& bk, double& bx) {
+    dpp_take<0xb1>(bv, bk, bx);
+    dpp_take<0x4e>(bv, bk, bx);
+    dpp_take<0x141>(bv, bk, bx);
+    dpp_take<0x140>(bv, bk, bx);
+}
+
+// winner of lanes 0..15, uniform in every lane
+__device__ __forceinline__ void row_argmax_dpp(double& bv, unsigned& bk, double& bx) {
+    row16_argmax_dpp(bv, bk, bx);
+    bv = readlane_f64(bv, 0);
+    bk = (unsigned)__builtin_amdgcn_readlane((int)bk, 0);
+    bx = readlane_f64(bx, 0);
+}
+
+// winner of the whole wave, uniform in every lane
+__device__ __forceinline__ void wave_argmax_dpp(double& bv, unsigned& bk) {
+    double bx = 0.0;
+    row16_argmax_dpp(bv, bk, bx);
+    double v = readlane_f64(bv, 0);
+    unsigned key = (unsigned)__builtin_amdgcn_readlane((int)bk, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const double ov = readlane_f64(bv, r);
+        const unsigned ok = (unsigned)__builtin_amdgcn_readlane((int)bk, r);
+        const bool better = (ov > v) || (ov == v && ok < key);
+        v = better ? ov : v;
+        key = better ? ok : key;
+    }
+    bv = v;
+    bk = key;
+}
+
 struct SmallCand {
     double v;
     unsigned key;
@@ -465,11 +532,11 @@ constexpr int64_t kSmallElems = 16384;  // 128 KiB of fp64 in LDS
 constexpr int64_t kSmallPerm = 2048;    // m + n
 
 bool rrlu_small_fits(int64_t m, int64_t n) {
-    return m > 0 && n > 0 && m * n <= kSmallElems && m + n <= kSmallPerm;
+    return m > 0 && n > 0 && (m | 1) * n <= kSmallElems && m + n <= kSmallPerm;
 }
 
 static size_t small_lds_bytes(int m, int n) {
-    const size_t a = ((size_t)m * n * sizeof(double) + 15) / 16 * 16;
+    const size_t a = ((size_t)(m | 1) * n * sizeof(double) + 15) / 16 * 16;
     const size_t p = ((size_t)(m + n) * sizeof(int) + 15) / 16 * 16;
     return a + p + (kSmallThreads / 64) * sizeof(CandR) + 32 + (size_t)(m + n) * sizeof(double);
 }
@@ -479,8 +546,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     int leftorth, RrluState* st, int64_t* rowphys, int64_t* colphys, double* pivvals,
     double* Lp, int64_t ldl, double* Up, int64_t ldu, SmallOut out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* S = reinterpret_cast<double*>(smem);  // m x n, ld m
-    int* rp = reinterpret_cast<int*>(smem + ((size_t)m * n * sizeof(double) + 15) / 16 * 16);
+    // m x n with an odd leading dimension: row accesses (swaps, the pivot row) hit distinct banks
+    const int ldS = m | 1;
+    double* S = reinterpret_cast<double*>(smem);
+    int* rp = reinterpret_cast<int*>(smem + ((size_t)ldS * n * sizeof(double) + 15) / 16 * 16);
     int* cp = rp + m;
     CandR* red = reinterpret_cast<CandR*>(reinterpret_cast<char*>(rp) +
                                           ((size_t)(m + n) * sizeof(int) + 15) / 16 * 16);
@@ -491,7 +560,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     constexpr int NW = kSmallThreads / 64;
     for (int j = w; j < n; j += NW)
-        for (int i = l; i < m; i += 64) S[i + j * m] = A[i + (int64_t)j * lda];
+        for (int i = l; i < m; i += 64) S[i + j * ldS] = A[i + (int64_t)j * lda];
     for (int i = tid; i < m; i += kSmallThreads) rp[i] = i;
     for (int j = tid; j < n; j += kSmallThreads) cp[j] = j;
     // every thread tracks the loop state (identical everywhere); thread 0 publishes it
@@ -510,43 +579,39 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     };
     for (int j = w; j < n; j += NW)
         for (int i = l; i < m; i += 64) {
-            const double v = S[i + j * m];
+            const double v = S[i + j * ldS];
             take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
         }
     SmallCand* red2 = reinterpret_cast<SmallCand*>(red);
+    long long prof_t[8];
     for (int k = 0; k < mr; ++k) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double ov = __shfl_xor(bv, off);
-            const unsigned ok = __shfl_xor(bk, off);
-            take(ov, ok);
-        }
+        SPROF(0);
+        wave_argmax_dpp(bv, bk);  // every lane now holds the wave's winner
         if (l == 0)  // the wave's winner and its value (no swap can be under way here)
-            red2[w] = SmallCand{bv, bk, 0u, bv >= 0.0 ? S[(bk & 0xffffu) + (bk >> 16) * m] : 0.0};
+            red2[w] = SmallCand{bv, bk, 0u, bv >= 0.0 ? S[(bk & 0xffffu) + (bk >> 16) * ldS] : 0.0};
         __syncthreads();
-        SmallCand b = red2[0];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) {
-            const SmallCand o = red2[i];
-            if ((o.v > b.v) || (o.v == b.v && o.key < b.key)) b = o;
-        }
+        SPROF(1);
+        // the workgroup's winner: lanes 0..NW-1 of every wave take one wave's entry each
+        SmallCand b = l < NW ? red2[l] : SmallCand{-1.0, 0xffffffffu, 0u, 0.0};
+        row_argmax_dpp(b.v, b.key, b.val);
         int p = (int)(b.key & 0xffffu), q = (int)(b.key >> 16);
         double val = b.val;
         if (!(b.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
             p = q = k;
-            val = S[k + k * m];
+            val = S[k + k * ldS];
         }
         error = fabs(val);
         if (((fabs(error) < reltol * maxerror) || (fabs(error) < abstol)) && k > 0) break;
         maxerror = jl_max(maxerror, error);
         np = k + 1;
         if (tid == 0) pivvals[k] = val;
+        SPROF(2);
         // swaprow!(k, p) then swapcol!(k, q) (matrixlu.jl:254-275)
         if (p != k) {
             for (int j = tid; j < n; j += kSmallThreads) {
-                const double t = S[k + j * m];
-                S[k + j * m] = S[p + j * m];
-                S[p + j * m] = t;
+                const double t = S[k + j * ldS];
+                S[k + j * ldS] = S[p + j * ldS];
+                S[p + j * ldS] = t;
             }
             if (tid == 0) {
                 const int t = rp[k];
@@ -557,9 +622,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
         }
         if (q != k) {
             for (int i = tid; i < m; i += kSmallThreads) {
-                const double t = S[i + k * m];
-                S[i + k * m] = S[i + q * m];
-                S[i + q * m] = t;
+                const double t = S[i + k * ldS];
+                S[i + k * ldS] = S[i + q * ldS];
+                S[i + q * ldS] = t;
             }
             if (tid == 0) {
                 const int t = cp[k];
@@ -568,32 +633,63 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
             }
             __syncthreads();
         }
+        SPROF(3);
         // normalisation by the pivot (true division; matrixlu.jl:300-305) into S and xv / yv
-        const double piv = S[k + k * m];
+        const double piv = S[k + k * ldS];
         for (int i = k + 1 + tid; i < m; i += kSmallThreads) {
-            const double x = leftorth ? S[i + k * m] / piv : S[i + k * m];
+            const double x = leftorth ? S[i + k * ldS] / piv : S[i + k * ldS];
             xv[i] = x;
-            S[i + k * m] = x;
+            S[i + k * ldS] = x;
         }
         for (int j = k + 1 + tid; j < n; j += kSmallThreads) {
-            const double y = leftorth ? S[k + j * m] : S[k + j * m] / piv;
+            const double y = leftorth ? S[k + j * ldS] : S[k + j * ldS] / piv;
             yv[j] = y;
-            S[k + j * m] = y;
+            S[k + j * ldS] = y;
         }
         __syncthreads();
+        SPROF(4);
         // rank-1 update (mul then sub, matrixlu.jl:314-320) fused with the next pivot's argmax
         bv = -1.0;
         bk = 0xffffffffu;
-        for (int j = w; j < n; j += NW) {
-            if (j <= k) continue;
-            const double y = yv[j];
-            for (int i = l; i < m; i += 64) {
-                if (i <= k) continue;
-                const double v = __dsub_rn(S[i + j * m], __dmul_rn(xv[i], y));
-                S[i + j * m] = v;
-                take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
+        if (m <= 64 * 4) {  // this lane's (at most 4) rows: their x's stay in registers
+            double xr[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const int i = l + 64 * a;
+                xr[a] = (i < m && i > k) ? xv[i] : 0.0;
+            }
+            // (the update is fp64-VALU-bound here: ~3 us/pivot at 14k elements on one CU)
+            for (int j = w; j < n; j += NW) {
+                if (j <= k) continue;
+                const double y = yv[j];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const int i = l + 64 * a;
+                    if (i >= m || i <= k) continue;
+                    const double v = __dsub_rn(S[i + j * ldS], __dmul_rn(xr[a], y));
+                    S[i + j * ldS] = v;
+                    take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
+                }
+            }
+        } else {
+            for (int j = w; j < n; j += NW) {
+                if (j <= k) continue;
+                const double y = yv[j];
+                for (int i = l; i < m; i += 64) {
+                    if (i <= k) continue;
+                    const double v = __dsub_rn(S[i + j * ldS], __dmul_rn(xv[i], y));
+                    S[i + j * ldS] = v;
+                    take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
+                }
             }
         }
+        SPROF(5);
+#ifdef TCI_SMALL_PROF
+        if (tid == 0 && k == 5)
+            printf("small k=5 m=%d n=%d: reduce %lld decide %lld swap %lld norm %lld update %lld\n", m, n,
+                   prof_t[1] - prof_t[0], prof_t[2] - prof_t[1], prof_t[3] - prof_t[2], prof_t[4] - prof_t[3],
+                   prof_t[5] - prof_t[4]);
+#endif
     }
     if (tid == 0) {
         st->np = np;
@@ -612,12 +708,12 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     if (Lp)
         for (int e = tid; e < m * np; e += kSmallThreads) {
             const int pos = e % m, t = e / m;
-            if (pos > t) Lp[rp[pos] + (int64_t)t * ldl] = S[pos + t * m];
+            if (pos > t) Lp[rp[pos] + (int64_t)t * ldl] = S[pos + t * ldS];
         }
     if (Up)
         for (int e = tid; e < np * n; e += kSmallThreads) {
             const int t = e % np, pos = e / np;
-            if (pos > t) Up[t + (int64_t)cp[pos] * ldu] = S[t + pos * m];
+            if (pos > t) Up[t + (int64_t)cp[pos] * ldu] = S[t + pos * ldS];
         }
     if (!out.flag) return;
     // NaN checks of tril(A[:, 1:np]) / triu(A[1:np, :]) before the unit diagonal is set
@@ -626,11 +722,11 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
         int fl = 0;
         for (int e = tid; e < m * np; e += kSmallThreads) {
             const int pos = e % m, t = e / m;
-            if (pos >= t && isnan(S[pos + t * m])) fl |= 1;
+            if (pos >= t && isnan(S[pos + t * ldS])) fl |= 1;
         }
         for (int e = tid; e < np * n; e += kSmallThreads) {
             const int t = e % np, pos = e / np;
-            if (pos >= t && isnan(S[t + pos * m])) fl |= 2;
+            if (pos >= t && isnan(S[t + pos * ldS])) fl |= 2;
         }
         if (fl) atomicOr(&ctl[4], fl);
         __syncthreads();
@@ -647,21 +743,21 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
                 const int a = e % np, j = e / np;
                 double s = 0.0;
                 for (int t = 0; t <= min(a, j); ++t)
-                    s = __dadd_rn(s, __dmul_rn(t == a ? 1.0 : S[a + t * m], S[t + j * m]));
+                    s = __dadd_rn(s, __dmul_rn(t == a ? 1.0 : S[a + t * ldS], S[t + j * ldS]));
                 out.right[a + (int64_t)cp[j] * np] = s;
             }
         if (out.left) {  // colstimespivotinv: rows >= np solve X L11 = L21 in place
             __syncthreads();
             for (int i = np + tid; i < m; i += kSmallThreads)
                 for (int j = np - 1; j >= 0; --j) {
-                    double s = S[i + j * m];
-                    for (int t = j + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[i + t * m], S[t + j * m]));
-                    S[i + j * m] = s;
+                    double s = S[i + j * ldS];
+                    for (int t = j + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[i + t * ldS], S[t + j * ldS]));
+                    S[i + j * ldS] = s;
                 }
             __syncthreads();
             for (int e = tid; e < m * np; e += kSmallThreads) {
                 const int i = e % m, j = e / m;
-                out.left[rp[i] + (int64_t)j * m] = i < np ? (i == j ? 1.0 : 0.0) : S[i + j * m];
+                out.left[rp[i] + (int64_t)j * m] = i < np ? (i == j ? 1.0 : 0.0) : S[i + j * ldS];
             }
         }
     } else {
@@ -670,21 +766,21 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
                 const int i = e % m, j = e / m;
                 double s = 0.0;
                 for (int t = 0; t <= min(i, j); ++t)
-                    s = __dadd_rn(s, __dmul_rn(S[i + t * m], t == j ? 1.0 : S[t + j * m]));
+                    s = __dadd_rn(s, __dmul_rn(S[i + t * ldS], t == j ? 1.0 : S[t + j * ldS]));
                 out.left[rp[i] + (int64_t)j * m] = s;
             }
         if (out.right) {  // pivotinvtimesrows: columns >= np solve U11 x = U[:, c] in place
             __syncthreads();
             for (int c = np + tid; c < n; c += kSmallThreads)
                 for (int a = np - 1; a >= 0; --a) {
-                    double s = S[a + c * m];
-                    for (int t = a + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[a + t * m], S[t + c * m]));
-                    S[a + c * m] = s;
+                    double s = S[a + c * ldS];
+                    for (int t = a + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[a + t * ldS], S[t + c * ldS]));
+                    S[a + c * ldS] = s;
                 }
             __syncthreads();
             for (int e = tid; e < np * n; e += kSmallThreads) {
                 const int a = e % np, j = e / np;
-                out.right[a + (int64_t)cp[j] * np] = j < np ? (a == j ? 1.0 : 0.0) : S[a + j * m];
+                out.right[a + (int64_t)cp[j] * np] = j < np ? (a == j ? 1.0 : 0.0) : S[a + j * ldS];
             }
         }
     }
