@@ -311,6 +311,32 @@ def extras(T, ctx):
     tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)
     res["tci2_config1"] = {"wall_s": round(time.perf_counter() - t0, 4), "ranks": ranks,
                            "final_error": errors[-1], "mode": "nsearchglobalpivot=0"}
+    # separable (CP-rank-K) Pi assembly of config 5 as an fp64 MFMA GEMM: 8192^2, K = 1024,
+    # 12 legs of d = 32, against the measured fp64 MFMA peak
+    import ctypes as C
+    peak = C.c_double()
+    ctx.check(ctx.lib.tci_diag_mfma_f64(ctx.h, C.byref(peak)))
+    K, L, d = 1024, 12, 32
+    g = 0.5 + np.random.default_rng(2).random((K, L, d))
+    fcp = T.cp_function(g, ctx=ctx)
+    Ic = rng.integers(1, d + 1, (m, 6)).astype(np.int32)
+    Jc = rng.integers(1, d + 1, (n, 6)).astype(np.int32)
+    dm = T.DeviceMatrix(m, n, ctx=ctx)
+    mx = C.c_double()
+    for _ in range(2):
+        ctx.check(ctx.lib.tci_batcheval_d(ctx.h, fcp.h, T._lib.ptr(Ic), m, 6, T._lib.ptr(Jc), n, 6, 0, dm.ptr,
+                                          dm.ld, C.byref(mx)))
+    ctx.set_timing(True)
+    for _ in range(3):
+        ctx.check(ctx.lib.tci_batcheval_d(ctx.h, fcp.h, T._lib.ptr(Ic), m, 6, T._lib.ptr(Jc), n, 6, 0, dm.ptr,
+                                          dm.ld, C.byref(mx)))
+    kms, kn = ctx.kernel_stats(1)
+    ctx.set_timing(False)
+    dm.free()
+    tfl = 2.0 * m * n * K / (kms / kn * 1e-3) / 1e12
+    res["pi_cp_gemm"] = {"m": m, "n": n, "K": K, "L": L, "ms_device": round(kms / kn, 3), "TFLOPs": round(tfl, 2),
+                         "mfma_f64_peak_measured_TFLOPs": round(peak.value, 2),
+                         "frac_of_measured_peak": round(tfl / peak.value, 3)}
     # other rrLU configurations of SURVEY 8(d): config 2 (4096^2), right-orthogonal pivots, and a
     # 16384^2 matrix (2 GiB) for the scale curve
     res["rrlu_configs"] = []

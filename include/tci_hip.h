@@ -180,6 +180,10 @@ int tci_fill_uniform_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t 
 int tci_diag_stream_d(tci_ctx* ctx, const double* d_a, double* d_b, int64_t n, int reps, int grid,
                       double* ms_read, double* ms_copy);
 
+/* Diagnostic: measured fp64 MFMA throughput (TFLOP/s) of independent v_mfma_f64_16x16x4f64
+ * chains on every SIMD -- the peak the separable-assembly GEMM is rated against. */
+int tci_diag_mfma_f64(tci_ctx* ctx, double* tflops);
+
 /* ------------------------------------------------------------ device mem */
 int tci_malloc_d(tci_ctx* ctx, void** p, int64_t bytes);
 int tci_free_d(tci_ctx* ctx, void* p);

@@ -952,6 +952,28 @@ int tci_sitetensor_solve_h(tci_ctx* c, const double* P, int64_t r, const double*
     return TCI_OK;
 }
 
+int tci_diag_mfma_f64(tci_ctx* c, double* tflops) {
+    if (!c || !tflops) return TCI_ERR_ARG;
+    int st;
+    if ((st = ensure(c, &c->dF2, &c->capF2, 64))) return st;
+    const int grid = std::max(c->ncu, 1) * 4, iters = 4096;  // one wave per SIMD
+    tci::launch_mfma_f64_probe(c->stream, grid, 64, c->dF2);   // warm
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    tci::launch_mfma_f64_probe(c->stream, grid, iters, c->dF2);
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventSynchronize(e1));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    const double flops = (double)grid * 4 /* waves */ * iters * 8 * (16.0 * 16 * 4 * 2);
+    *tflops = flops / (ms * 1e-3) / 1e12;
+    return TCI_OK;
+}
+
 int tci_tt_evaluate_h(tci_ctx* c, int32_t L, const int32_t* dims, const int32_t* bonddims,
                       const double* cores, int64_t ncore, const int32_t* X, int64_t npts, double* out) {
     if (!c || L < 1 || !dims || !bonddims || !cores || (npts > 0 && (!X || !out)))

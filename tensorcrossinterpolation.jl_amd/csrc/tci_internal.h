@@ -148,6 +148,9 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
                       unsigned long long* maxbits, void* scratch);
 int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n);
 
+// diagnostic fp64 MFMA throughput probe: grid x 256 threads, iters x 8 x v_mfma_f64_16x16x4 per wave
+void launch_mfma_f64_probe(hipStream_t s, int grid, int iters, double* sink);
+
 // tensor-train values at npts points (X: npts x L, 1-based); rmax = max bond dimension (<= 1024)
 void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, const int32_t* rdim,
                     const int32_t* dims, int L, const int32_t* X, int npts, double* out, int rmax);

@@ -69,6 +69,7 @@ SIGNATURES = {
     "tci_tt_evaluate_h": ([vp, i32, vp, vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_fill_uniform_d": ([vp, vp, i64, i64, i64, C.c_uint64], C.c_int),
     "tci_diag_stream_d": ([vp, vp, vp, i64, C.c_int, C.c_int, pdbl, pdbl], C.c_int),
+    "tci_diag_mfma_f64": ([vp, pdbl], C.c_int),
     "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
     "tci_free_d": ([vp, vp], C.c_int),
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),
