@@ -122,6 +122,11 @@ def main():
     assert np_ == min(r, m, n), np_
     wb_ms, wb_launches = ctx.kernel_stats(0)
     ro_ms, ro_launches = ctx.kernel_stats(2)
+    by_pending = {}  # read-only pass time by pending depth P (sub-families 3 + P)
+    for P in range(1, args.nb):
+        pm, pn = ctx.kernel_stats(3 + P)
+        if pn:
+            by_pending[P] = round(pm / pn, 5)
     ctx.set_timing(False)
     if dist is not None:
         import torch
@@ -153,7 +158,8 @@ def main():
                                  if wb_launches else None},
              "read_only_pass": {"launches": ro_launches, "avg_ms": round(ro_ms / max(ro_launches, 1), 5),
                                 "GBps": round(ro_b / max(ro_n, 1) / (ro_ms / max(ro_launches, 1) * 1e-3) / 1e9, 1)
-                                if ro_launches else None}}
+                                if ro_launches else None,
+                                "avg_ms_by_pending_depth": by_pending}}
     out = {
         "metric": "rrLU GFLOP/s at (m,n,r)=(8192,8192,256)" if (m, n, r) == (8192, 8192, 256)
         else f"rrLU GFLOP/s at (m,n,r)=({m},{n},{r})",

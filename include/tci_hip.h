@@ -63,7 +63,8 @@ int tci_ctx_synchronize(tci_ctx* ctx);
 /* Device time (ms, summed) and launch count of a kernel family since tci_set_timing(ctx, 1),
  * measured with hipEvents on the context stream: family 0 = rrLU pass that writes the Schur
  * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
- * 1 = batch evaluation. */
+ * 1 = batch evaluation; 3 + P (P = 1..16) = the read-only passes that applied P pending updates
+ * (a breakdown of family 2). */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */

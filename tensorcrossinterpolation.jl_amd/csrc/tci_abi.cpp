@@ -40,6 +40,7 @@ struct tci_ctx {
     int flush_every = 10;  // deferred-update depth nb (1 = write back every pivot; 10 measured best)
     int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
+    int pass_percu = 1;    // one workgroup per CU, dynamic chunks (env TCI_PASS_PERCU=0: k_pass)
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int ncu = 0;           // compute units of the device
@@ -100,9 +101,16 @@ struct tci_ctx {
     int timing_stride = 1;  // rrLU passes: only every timing_stride-th pivot's pass is timed
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
-    std::vector<std::pair<int, size_t>> evpairs;  // (family, index of start event)
-    double fam_ms[3] = {0, 0, 0};
-    int64_t fam_n[3] = {0, 0, 0};
+    // (family, sub-family or -1, index of start event); sub-families 3 + P: read-only rrLU pass
+    // with P pending updates
+    struct EvPair {
+        int fam, sub;
+        size_t idx;
+    };
+    std::vector<EvPair> evpairs;
+    static constexpr int kFams = 3 + tci::kMaxPend + 1;
+    double fam_ms[kFams] = {};
+    int64_t fam_n[kFams] = {};
 };
 
 struct tci_func {
@@ -206,7 +214,7 @@ int ensure_pinned(tci_ctx* c, char** p, size_t* cap, size_t bytes) {
     return TCI_OK;
 }
 
-void ev_begin(tci_ctx* c, int fam, bool sampled = true) {
+void ev_begin(tci_ctx* c, int fam, bool sampled = true, int sub = -1) {
     if (!c->timing || !sampled) return;
     if (c->evused + 2 > c->evpool.size()) {
         size_t add = std::max<size_t>(64, c->evpool.size());
@@ -216,18 +224,18 @@ void ev_begin(tci_ctx* c, int fam, bool sampled = true) {
             c->evpool.push_back(e);
         }
     }
-    c->evpairs.push_back({fam, c->evused});
+    c->evpairs.push_back({fam, sub, c->evused});
     hipEventRecord(c->evpool[c->evused], c->stream);
     c->evused += 2;
 }
 void ev_end(tci_ctx* c, bool sampled = true) {
     if (!c->timing || !sampled) return;
-    hipEventRecord(c->evpool[c->evpairs.back().second + 1], c->stream);
+    hipEventRecord(c->evpool[c->evpairs.back().idx + 1], c->stream);
 }
 void ev_reset(tci_ctx* c) {
     c->evused = 0;
     c->evpairs.clear();
-    for (int f = 0; f < 3; ++f) {
+    for (int f = 0; f < tci_ctx::kFams; ++f) {
         c->fam_ms[f] = 0;
         c->fam_n[f] = 0;
     }
@@ -237,9 +245,13 @@ void ev_collect(tci_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (auto& pr : c->evpairs) {
         float ms = 0;
-        hipEventElapsedTime(&ms, c->evpool[pr.second], c->evpool[pr.second + 1]);
-        c->fam_ms[pr.first] += ms;
-        c->fam_n[pr.first] += 1;
+        hipEventElapsedTime(&ms, c->evpool[pr.idx], c->evpool[pr.idx + 1]);
+        c->fam_ms[pr.fam] += ms;
+        c->fam_n[pr.fam] += 1;
+        if (pr.sub >= 0) {
+            c->fam_ms[pr.sub] += ms;
+            c->fam_n[pr.sub] += 1;
+        }
     }
     c->evpairs.clear();
     c->evused = 0;
@@ -348,8 +360,10 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     g.abstol = abstol;
     g.ticket = c->ticket;
     g.selk = 0;
-    const int grid = tci::argmax_grid(mi, ni, -1, g.cb, std::min(c->pass_grid, kMaxGrid));
-    tci::launch_pass(c->stream, 0, false, g, grid);  // argmax of A, selects pivot 0
+    const bool percu = c->pass_percu && c->ncu > 0;
+    const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
+                                      percu ? std::min(c->ncu, kMaxGrid) : std::min(c->pass_grid, kMaxGrid));
+    tci::launch_pass(c->stream, 0, false, percu, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
     while (k < mr && !stopped) {
@@ -364,8 +378,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
-            ev_begin(c, flush ? 0 : 2, sampled);
-            tci::launch_pass(c->stream, P, flush, g, grid);
+            ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
+            tci::launch_pass(c->stream, P, flush, percu, g, grid);
             ev_end(c, sampled);
             if (flush) t0 = kk + 1;
         }
@@ -510,6 +524,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
+    if (const char* e = getenv("TCI_PASS_PERCU")) c->pass_percu = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     {
@@ -596,7 +611,8 @@ int tci_set_timing(tci_ctx* c, int enabled) {
     return TCI_OK;
 }
 int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* launches) {
-    if (family < 0 || family > 2) return set_err(c, TCI_ERR_ARG, "family must be 0, 1 or 2");
+    if (family < 0 || family >= tci_ctx::kFams)
+        return set_err(c, TCI_ERR_ARG, "family must be in 0.." + std::to_string(tci_ctx::kFams - 1));
     ev_collect(c);
     if (total_ms) *total_ms = c->fam_ms[family];
     if (launches) *launches = c->fam_n[family];

@@ -96,7 +96,9 @@ struct FuncDev {
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
-void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid);
+// percu: one 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2);
+// otherwise 256-thread workgroups with static shares (k_pass)
+void launch_pass(hipStream_t s, int P, bool flush, bool percu, const PassArgs& g, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:

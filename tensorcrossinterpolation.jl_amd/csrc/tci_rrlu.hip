@@ -33,6 +33,9 @@
 #ifndef TCI_PASS_U
 #define TCI_PASS_U 4  // columns per lane whose 16-B loads are in flight together (measured)
 #endif
+#ifndef TCI_PASS2_U
+#define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
+#endif
 #ifndef TCI_FLUSH_NT
 #define TCI_FLUSH_NT 0  // write-back pass stores non-temporal
 #endif
@@ -139,6 +142,115 @@ __device__ __forceinline__ CandR load_cand_sc1(const Cand* src) {
                  (int)(uint32_t)(w3 >> 32)};
 }
 
+// Phase profile of one pass (build with -DTCI_PASS_PROF=K): every workgroup stamps entry, end of
+// start-up, end of staging, end of streaming and its ticket (100 MHz wall clock); the last one
+// prints the spread at pivot selections K and K + 1, including the gap since the previous pass's
+// commit.
+#ifndef TCI_PASS_PROF
+#define TCI_PASS_PROF 0
+#endif
+#if TCI_PASS_PROF
+__device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
+#define PPROF(i) (pt[i] = wall_clock64())
+#else
+#define PPROF(i) ((void)pt)
+#endif
+
+// Pass tail: block reduction of the workgroups' candidates, then the hand-off to the last one
+// (sc1 stores + agent-scope ticket), which reduces all of them and commits pivot sel.selk.
+template <int NT>
+__device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* __restrict__ cand,
+                                          unsigned long long (&pt)[6], int m, int P, int flush) {
+    RrluState* st = sel.st;
+    (void)m;
+    (void)P;
+    (void)flush;
+    block_reduce_cand<NT>(best);
+    if (sel.selk < 0) return;
+    __shared__ int last_s;
+    if (threadIdx.x == 0) {
+#if TCI_PASS_PROF
+        for (int i = 0; i < 4; ++i)
+            __hip_atomic_store(&g_pprof[blockIdx.x * 8 + i], pt[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        store_cand_sc1(cand + blockIdx.x, best);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old =
+            __hip_atomic_fetch_add(sel.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = (old == gridDim.x - 1);
+        PPROF(4);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
+    constexpr int CPT = kMaxPassGrid / NT;
+    CandR cs[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int i = threadIdx.x + u * NT;
+        cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
+    }
+    CandR w = cs[0];
+#pragma unroll
+    for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
+    __syncthreads();  // block_reduce_cand's LDS slots are reused
+    block_reduce_cand<NT>(w);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
+                     sel.colphys, sel.pivvals);
+#if TCI_PASS_PROF
+        __threadfence();
+        PPROF(5);
+        unsigned long long* gp = g_pprof;
+        const unsigned long long prev5 = gp[kMaxPassGrid * 8];
+        gp[kMaxPassGrid * 8] = pt[5];
+        if (sel.selk == TCI_PASS_PROF || sel.selk == TCI_PASS_PROF + 1) {
+            unsigned long long t0min = ~0ull, t0max = 0, t3max = 0, t3min = ~0ull;
+            double s01 = 0, s12 = 0, s23 = 0;
+            // stream-end times (from the first entry) averaged by XCD (blockIdx % 8) and by
+            // dispatch round (blockIdx / 256)
+            unsigned long long ex[8] = {}, eq[8] = {};
+            int nx[8] = {}, nr[8] = {};
+            for (int i = 0; i < (int)gridDim.x; ++i) {
+                unsigned long long t[4];
+                for (int z = 0; z < 4; ++z)
+                    t[z] = __hip_atomic_load(&gp[i * 8 + z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ex[i % 8] += t[3];
+                nx[i % 8]++;
+                eq[min(i / 256, 7)] += t[3];
+                nr[min(i / 256, 7)]++;
+                t0min = min(t0min, t[0]);
+                t0max = max(t0max, t[0]);
+                t3min = min(t3min, t[3]);
+                t3max = max(t3max, t[3]);
+                s01 += (double)(t[1] - t[0]);
+                s12 += (double)(t[2] - t[1]);
+                s23 += (double)(t[3] - t[2]);
+            }
+            const double us = 0.01, G = (double)gridDim.x;  // 100 MHz ticks
+
+            printf("[pass k=%d P=%d flush=%d grid=%d] gap-since-prev-commit %.2f us | entry spread %.2f | "
+                   "avg startup %.2f staging %.2f stream %.2f | first/last stream end %.2f/%.2f | "
+                   "ticket->last %.2f | reduce+commit %.2f | total %.2f\n",
+                   sel.selk, P, flush, (int)gridDim.x, (double)(t0min - prev5) * us,
+                   (double)(t0max - t0min) * us, s01 / G * us, s12 / G * us, s23 / G * us,
+                   (double)(t3min - t0min) * us, (double)(t3max - t0min) * us,
+                   (double)(pt[4] - t3max) * us, (double)(pt[5] - pt[4]) * us,
+                   (double)(pt[5] - t0min) * us);
+            printf("  [k=%d] end by XCD: %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f | by round: %.1f %.1f %.1f %.1f\n",
+                   sel.selk, (ex[0] / nx[0] - t0min) * us, (ex[1] / nx[1] - t0min) * us,
+                   (ex[2] / nx[2] - t0min) * us, (ex[3] / nx[3] - t0min) * us,
+                   (ex[4] / nx[4] - t0min) * us, (ex[5] / nx[5] - t0min) * us,
+                   (ex[6] / nx[6] - t0min) * us, (ex[7] / nx[7] - t0min) * us,
+                   nr[0] ? (eq[0] / nr[0] - t0min) * us : 0.0, nr[1] ? (eq[1] / nr[1] - t0min) * us : 0.0,
+                   nr[2] ? (eq[2] / nr[2] - t0min) * us : 0.0, nr[3] ? (eq[3] / nr[3] - t0min) * us : 0.0);
+        }
+#endif
+    }
+}
+
 template <int P, bool FLUSH>
 __global__ __launch_bounds__(kUpdThreads) void k_pass(
     double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
@@ -148,7 +260,8 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     RrluState* st = sel.st;
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
-    if (st->done) return;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
     constexpr int U = TCI_PASS_U;  // columns whose loads are in flight together
     constexpr int PP = P > 0 ? P : 1;
     // y_s of up to kStageCols of the workgroup's columns, [local column][slot]; slot P-1 = y_k
@@ -162,6 +275,33 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     // column tiles q, q + nq, q + 2 nq, ...: at any moment the grid streams one contiguous band
     // of nq column tiles (spread over every HBM channel), band after band
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    // The workgroup's columns stream in chunks of U (U divides cb: a chunk never straddles a
+    // tile), chunk h of a staging group covering local columns h*U .. h*U+U-1. Two chunks are in
+    // flight per lane (double-buffered registers). The stale values depend on nothing the pass
+    // derives, so the first two chunks are requested before the start-up chain (pivot, maps,
+    // pending vectors) and arrive while it runs.
+    const int G = kStageCols / cb;
+    const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;  // this thread's two rows
+    static_assert(U <= 8 && 8 % U == 0, "U must divide every column-tile width");
+    const bool rowok = r0 < m, pair = r0 + 1 < m;
+    double* const base = A + r0;
+    auto chunk_col = [&](int g0, int h) -> int {  // first (physical) column of chunk h
+        const int it = g0 + (h * U) / cb;
+        return (q + (rev ? ntc - 1 - it : it) * nq) * cb + (h * U) % cb;
+    };
+    auto load_chunk = [&](int g0, int h, double2 (&v)[U]) {
+        const int j = chunk_col(g0, h);
+#pragma unroll
+        for (int u = 0; u < U; ++u)  // past the last column: any valid address (never used)
+            v[u] = *reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
+    };
+    double2 va[U], vb[U];
+    if (rowok && ntc > 0) {
+        const int nch0 = min(G, ntc) * cb / U;
+        load_chunk(0, 0, va);
+        if (nch0 > 1) load_chunk(0, 1, vb);
+    }
+    if (st->done) return;
     int a = 0, b = 0;
     double piv = 1.0;
     if (P > 0) {
@@ -169,9 +309,8 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         b = (int)st->q;
         piv = st->pval;
     }
-    // this thread's two rows, their pending x's and x_k
-    const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;
-    const int rp0 = r0 < m ? rowpos[r0] : -1;
+    // this thread's rows' positions, pending x's and x_k
+    const int rp0 = rowok ? rowpos[r0] : -1;
     const int rp1 = r0 + 1 < m ? rowpos[r0 + 1] : -1;
     const bool in0 = rp0 > k, in1 = rp1 > k;
     const bool active = in0 || in1;
@@ -210,12 +349,17 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
             }
         }
     }
+    PPROF(1);
     CandR best = cand_none();
     // staging groups: the y's of G column tiles are staged at once (one barrier pair per group,
     // usually one group per pass), then the group's tiles stream without barriers
-    const int G = kStageCols / cb;
     for (int g0 = 0; g0 < ntc; g0 += G) {
         const int gn = min(G, ntc - g0);
+        const int nch = gn * cb / U;
+        if (g0 > 0 && active) {
+            load_chunk(g0, 0, va);
+            if (nch > 1) load_chunk(g0, 1, vb);
+        }
         __syncthreads();  // previous group's readers are done with ys / cpos_s
         for (int lc = threadIdx.x; lc < gn * cb; lc += kUpdThreads) {
             const int it = g0 + lc / cb;
@@ -242,91 +386,266 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
             }
         }
         __syncthreads();
+        if (g0 == 0) PPROF(2);
         if (!active) continue;
-        for (int it = g0; it < g0 + gn; ++it) {
-            const int tc = q + (rev ? ntc - 1 - it : it) * nq;
-            const int j0 = tc * cb;
-            const int j1 = min(j0 + cb, n);
-            const int l0 = (it - g0) * cb;  // local column index of j0
-            // one column: apply the P pending updates in order (rows outside the block keep their
-            // value), write back if FLUSH, fold both rows into the running candidate
-            auto column = [&](double2 v, int c, double2* pa) {
-                const int cp = cpos_s[l0 + c];
-                if (cp <= k) return;  // column already pivoted: not in the trailing block
-                double u0 = v.x, u1 = v.y;
+        // one column (local index lc, physical j): apply the P pending updates in order, write
+        // back if FLUSH, fold the block's rows into the running candidate. Rows outside the block
+        // are updated too (their values are never read again), which saves the selects.
+        auto column = [&](double2 v, int lc, int j) {
+            const int cp = cpos_s[lc];
+            if (cp <= k) return;  // pivoted column or past the last one: not in the trailing block
 #pragma unroll
-                for (int s = 0; s < P; ++s) {
-                    const double y = ys[(l0 + c) * PP + s];
-                    u0 = __dsub_rn(u0, __dmul_rn(x0[s], y));
-                    u1 = __dsub_rn(u1, __dmul_rn(x1[s], y));
-                }
-                v.x = in0 ? u0 : v.x;
-                v.y = in1 ? u1 : v.y;
-                if (FLUSH) {
-                    if (TCI_FLUSH_NT) {
-                        typedef double dv2 __attribute__((ext_vector_type(2)));
-                        dv2 w = {v.x, v.y};
-                        __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
-                    } else {
-                        *pa = v;
-                    }
-                }
-                // the full (value, column, row) comparison only matters when v >= best.v, which is
-                // rare once a large value has been seen: test that first (NaN fails it, as it should)
-                const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
-                if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
-                    const int j = j0 + c;
-                    if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
-                    if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
-                }
-            };
-            double* base = A + r0;
-            int c = 0;
-            for (; c + U <= j1 - j0; c += U) {
-                double2 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    v[u] = *reinterpret_cast<const double2*>(base + (int64_t)(j0 + c + u) * lda);
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    column(v[u], c + u, reinterpret_cast<double2*>(base + (int64_t)(j0 + c + u) * lda));
+            for (int s = 0; s < P; ++s) {
+                const double y = ys[lc * PP + s];
+                v.x = __dsub_rn(v.x, __dmul_rn(x0[s], y));
+                v.y = __dsub_rn(v.y, __dmul_rn(x1[s], y));
             }
-            for (; c < j1 - j0; ++c) {
-                double2* pa = reinterpret_cast<double2*>(base + (int64_t)(j0 + c) * lda);
-                column(*pa, c, pa);
+            if (FLUSH) {
+                double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
+                if (!pair) {
+                    pa->x = v.x;  // odd m: row m is the caller's padding, left untouched
+                } else if (TCI_FLUSH_NT) {
+                    typedef double dv2 __attribute__((ext_vector_type(2)));
+                    dv2 w = {v.x, v.y};
+                    __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
+                } else {
+                    *pa = v;
+                }
+            }
+            // the full (value, column, row) comparison only matters when v >= best.v, which is
+            // rare once a large value has been seen: test that first (NaN fails it, as it should)
+            const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
+            if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
+                if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
+            }
+        };
+        auto process = [&](int h, const double2 (&v)[U]) {
+            const int j = chunk_col(g0, h);
+#pragma unroll
+            for (int u = 0; u < U; ++u) column(v[u], h * U + u, j + u);
+        };
+        for (int h = 0; h < nch; h += 2) {
+            process(h, va);
+            if (h + 2 < nch) load_chunk(g0, h + 2, va);
+            if (h + 1 < nch) {
+                process(h + 1, vb);
+                if (h + 3 < nch) load_chunk(g0, h + 3, vb);
             }
         }
     }
-    block_reduce_cand<kUpdThreads>(best);
-    if (sel.selk < 0) return;
-    __shared__ int last_s;
-    if (threadIdx.x == 0) {
-        store_cand_sc1(cand + blockIdx.x, best);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old =
-            __hip_atomic_fetch_add(sel.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_s = (old == gridDim.x - 1);
-    }
-    __syncthreads();
-    if (!last_s) return;
-    // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
-    constexpr int CPT = kMaxPassGrid / kUpdThreads;
-    CandR cs[CPT];
+    PPROF(3);
+    pass_tail<kUpdThreads>(best, sel, cand, pt, m, P, (int)FLUSH);
+}
+
+// ------------------------------------------------------------------ pass, one workgroup per CU
+// The same pass (same values, same candidate order) with the work balanced inside each CU. With
+// four 256-thread workgroups per CU the oldest one finishes its fixed share first (measured: the
+// four dispatch rounds ended 64 / 70 / 79 / 89 us into a 100 us pass) and the CU idles on the last.
+// Here a CU runs ONE 1024-thread workgroup: its 512-row tile is cut into 4 row slices of 128 rows
+// (one wave each, x's in registers) and every slice is served by 4 waves, which take U-column
+// chunks of the workgroup's columns from a per-slice LDS counter -- the faster waves take more.
+// Start-up: the first two chunks of every wave are assigned statically and requested before
+// anything else; every load that does not need the pivot (maps, pending x's and y's) goes out
+// before the pivot is read.
+constexpr int kP2Threads = 1024;
+constexpr int kP2Slices = kRowsPerTile / 128;              // 128-row slices of a tile
+constexpr int kP2Reps = kP2Threads / 64 / kP2Slices;        // waves per slice
+constexpr int kP2StageCols = 512;                           // columns staged at once
+static_assert(kP2StageCols <= kP2Threads, "one staged column per thread");
+
+template <int P, bool FLUSH>
+__global__ __launch_bounds__(kP2Threads) void k_pass2(
+    double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
+    double* __restrict__ Y, int64_t ldy, double* __restrict__ Lp, int64_t ldl,
+    double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand, int cb, int rev,
+    SelArgs sel) {
+    RrluState* st = sel.st;
+    const int32_t* rowpos = sel.rowpos;
+    const int32_t* colpos = sel.colpos;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
+    constexpr int U = TCI_PASS2_U;
+    static_assert(U <= 8 && 8 % U == 0, "U must divide every column-tile width");
+    constexpr int PP = P > 0 ? P : 1;
+    __shared__ double ys[kP2StageCols * PP];
+    __shared__ int cpos_s[kP2StageCols];
+    __shared__ int cnt[kP2Slices];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slice = wave % kP2Slices, rep = wave / kP2Slices;
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const int tiles_c = (n + cb - 1) / cb;
+    const int nq = gridDim.x / tiles_r;
+    const int tr = blockIdx.x % tiles_r;
+    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    const int G = kP2StageCols / cb;
+    const int r0 = tr * kRowsPerTile + slice * 128 + 2 * lane;
+    const bool rowok = r0 < m, pair = r0 + 1 < m;
+    double* const base = A + (rowok ? r0 : 0);  // rows past m read row 0 (never used)
+    auto chunk_col = [&](int g0, int h) -> int {
+        const int it = g0 + (h * U) / cb;
+        return (q + (rev ? ntc - 1 - it : it) * nq) * cb + (h * U) % cb;
+    };
+    auto load_chunk = [&](int g0, int h, double2 (&v)[U]) {
+        const int j = chunk_col(g0, h);
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-        const int i = threadIdx.x + u * kUpdThreads;
-        cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
-    }
-    CandR w = cs[0];
+        for (int u = 0; u < U; ++u)
+            v[u] = *reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
+    };
+    auto stage_col = [&](int g0) -> int {  // the column this thread stages in group g0 (or -1)
+        const int gn = min(G, ntc - g0);
+        const int lc = threadIdx.x;
+        if (lc >= gn * cb) return -1;
+        const int it = g0 + lc / cb;
+        return (q + (rev ? ntc - 1 - it : it) * nq) * cb + lc % cb;
+    };
+    // loads that need no pivot: this thread's rows' positions and pending x's, its staged column's
+    // position, then the first two chunks of the matrix
+    const int rp0 = rowok ? rowpos[r0] : -1;
+    const int rp1 = pair ? rowpos[r0 + 1] : -1;
+    double x0[PP], x1[PP];
+    if constexpr (P > 1) {
 #pragma unroll
-    for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
-    __syncthreads();  // block_reduce_cand's LDS slots are reused
-    block_reduce_cand<kUpdThreads>(w);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
-                     sel.colphys, sel.pivvals);
+        for (int s = 0; s < P - 1; ++s) {
+            const double2 u = *reinterpret_cast<const double2*>(X + (int64_t)s * ldx + (rowok ? r0 : 0));
+            x0[s] = u.x;
+            x1[s] = u.y;
+        }
     }
+    int jst = ntc > 0 ? stage_col(0) : -1;
+    int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+    double2 va[U], vb[U];
+    const int nch0 = ntc > 0 ? min(G, ntc) * cb / U : 0;
+    if (rep < nch0) load_chunk(0, rep, va);
+    if (rep + kP2Reps < nch0) load_chunk(0, rep + kP2Reps, vb);
+    if (st->done) return;
+    int a = 0, b = 0;
+    double piv = 1.0;
+    if (P > 0) {
+        a = (int)st->p;
+        b = (int)st->q;
+        piv = st->pval;
+    }
+    const bool in0 = rp0 > k, in1 = rp1 > k;
+    const bool active = in0 || in1;
+    if constexpr (P > 0) {
+        // x_k of this thread's rows (pivot k's column, pending updates applied)
+        const double2 cb2 = *reinterpret_cast<const double2*>(A + (rowok ? r0 : 0) + (int64_t)b * lda);
+        double xk0 = cb2.x, xk1 = cb2.y;
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) {
+            const double yv = Y[(int64_t)s * ldy + b];
+            xk0 = __dsub_rn(xk0, __dmul_rn(x0[s], yv));
+            xk1 = __dsub_rn(xk1, __dmul_rn(x1[s], yv));
+        }
+        if (leftorth) {
+            xk0 = xk0 / piv;
+            xk1 = xk1 / piv;
+        }
+        x0[P - 1] = xk0;
+        x1[P - 1] = xk1;
+        if (q == 0 && rep == 0) {
+            double* xs = X + (int64_t)(P - 1) * ldx;
+            if (in0) {
+                xs[r0] = xk0;
+                Lp[r0 + (int64_t)k * ldl] = xk0;
+            }
+            if (in1) {
+                xs[r0 + 1] = xk1;
+                Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
+            }
+        }
+    }
+    PPROF(1);
+    CandR best = cand_none();
+    const bool wact = __any(active);  // wave-uniform: the slice has rows in the trailing block
+    for (int g0 = 0; g0 < ntc; g0 += G) {
+        const int gn = min(G, ntc - g0);
+        const int nch = gn * cb / U;
+        if (g0 > 0) {
+            jst = stage_col(g0);
+            cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+            if (wact) {
+                if (rep < nch) load_chunk(g0, rep, va);
+                if (rep + kP2Reps < nch) load_chunk(g0, rep + kP2Reps, vb);
+            }
+            __syncthreads();  // previous group's readers are done with ys / cpos_s / cnt
+        }
+        if (jst >= 0) {
+            const int lc = threadIdx.x;
+            cpos_s[lc] = cpst;  // -1 past the last column: skipped like a pivoted one
+            if (P > 0 && cpst > k) {
+                double yk = A[a + (int64_t)jst * lda];
+#pragma unroll
+                for (int s = 0; s < P - 1; ++s) {
+                    const double ysv = Y[(int64_t)s * ldy + jst];
+                    ys[lc * PP + s] = ysv;
+                    yk = __dsub_rn(yk, __dmul_rn(X[(int64_t)s * ldx + a], ysv));
+                }
+                if (!leftorth) yk = yk / piv;
+                ys[lc * PP + P - 1] = yk;
+                if (tr == 0) {
+                    Y[(int64_t)(P - 1) * ldy + jst] = yk;
+                    Up[k + (int64_t)jst * ldu] = yk;
+                }
+            }
+        }
+        if (threadIdx.x < kP2Slices) cnt[threadIdx.x] = 2 * kP2Reps;
+        __syncthreads();
+        if (g0 == 0) PPROF(2);
+        if (!wact) continue;
+        auto column = [&](double2 v, int lc, int j) {
+            const int cp = cpos_s[lc];
+            if (cp <= k) return;
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const double y = ys[lc * PP + s];
+                v.x = __dsub_rn(v.x, __dmul_rn(x0[s], y));
+                v.y = __dsub_rn(v.y, __dmul_rn(x1[s], y));
+            }
+            if (FLUSH && rowok) {
+                double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
+                if (!pair) {
+                    pa->x = v.x;
+                } else if (TCI_FLUSH_NT) {
+                    typedef double dv2 __attribute__((ext_vector_type(2)));
+                    dv2 w = {v.x, v.y};
+                    __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
+                } else {
+                    *pa = v;
+                }
+            }
+            const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
+            if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
+                if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
+            }
+        };
+        auto process = [&](int h, const double2 (&v)[U]) {
+            const int j = chunk_col(g0, h);
+#pragma unroll
+            for (int u = 0; u < U; ++u) column(v[u], h * U + u, j + u);
+        };
+        auto grab = [&]() -> int {
+            int h = 0;
+            if (lane == 0) h = atomicAdd(&cnt[slice], 1);
+            return __shfl(h, 0);
+        };
+        // h0's values in va, h1's in vb; every grab returns a larger index than both
+        int h0 = rep, h1 = rep + kP2Reps;
+        while (h0 < nch) {
+            process(h0, va);
+            h0 = grab();
+            if (h0 < nch) load_chunk(g0, h0, va);
+            if (h1 >= nch) break;
+            process(h1, vb);
+            h1 = grab();
+            if (h1 < nch) load_chunk(g0, h1, vb);
+        }
+    }
+    PPROF(3);
+    pass_tail<kP2Threads>(best, sel, cand, pt, m, P, (int)FLUSH);
 }
 
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
@@ -342,23 +661,30 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 }
 
 template <int P>
-static void launch_pass_p(hipStream_t s, bool flush, const PassArgs& g, int grid) {
+static void launch_pass_p(hipStream_t s, bool flush, bool percu, const PassArgs& g, int grid) {
     const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals,
                       g.st,     g.ticket, g.reltol,  g.abstol,  g.selk};
-    if (flush)
-        hipLaunchKernelGGL((k_pass<P, true>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m, g.n,
-                           g.k, g.X, g.ldx, g.Y, g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand,
-                           g.cb, g.rev, sel);
-    else
-        hipLaunchKernelGGL((k_pass<P, false>), dim3(grid), dim3(kUpdThreads), 0, s, g.A, g.lda, g.m,
-                           g.n, g.k, g.X, g.ldx, g.Y, g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth,
-                           g.cand, g.cb, g.rev, sel);
+#define TCI_PASS_LAUNCH(KERN, NT)                                                                  \
+    hipLaunchKernelGGL(KERN, dim3(grid), dim3(NT), 0, s, g.A, g.lda, g.m, g.n, g.k, g.X, g.ldx, g.Y, \
+                       g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb, g.rev, sel)
+    if (percu) {
+        if (flush)
+            TCI_PASS_LAUNCH((k_pass2<P, true>), kP2Threads);
+        else
+            TCI_PASS_LAUNCH((k_pass2<P, false>), kP2Threads);
+    } else {
+        if (flush)
+            TCI_PASS_LAUNCH((k_pass<P, true>), kUpdThreads);
+        else
+            TCI_PASS_LAUNCH((k_pass<P, false>), kUpdThreads);
+    }
+#undef TCI_PASS_LAUNCH
 }
 
-void launch_pass(hipStream_t s, int P, bool flush, const PassArgs& g, int grid) {
+void launch_pass(hipStream_t s, int P, bool flush, bool percu, const PassArgs& g, int grid) {
     switch (P) {
 #define TCI_PASS_CASE(p) \
-    case p: launch_pass_p<p>(s, flush, g, grid); break;
+    case p: launch_pass_p<p>(s, flush, percu, g, grid); break;
         TCI_PASS_CASE(0) TCI_PASS_CASE(1) TCI_PASS_CASE(2) TCI_PASS_CASE(3) TCI_PASS_CASE(4)
         TCI_PASS_CASE(5) TCI_PASS_CASE(6) TCI_PASS_CASE(7) TCI_PASS_CASE(8) TCI_PASS_CASE(9)
         TCI_PASS_CASE(10) TCI_PASS_CASE(11) TCI_PASS_CASE(12) TCI_PASS_CASE(13) TCI_PASS_CASE(14)
