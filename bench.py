@@ -142,12 +142,12 @@ def main():
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
-        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,false> (read-only: pending updates "
+        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass2<P,false> (read-only: pending updates "
                                                        "applied on the fly + abs2 argmax)", ro_ms,
                                                        ro_launches, ro_b, ro_n)
     else:
         dom_key = "rrlu_write_back_pass"
-        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass<P,true> (pending updates applied and "
+        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass2<P,true> (pending updates applied and "
                                                        "written back + abs2 argmax)", wb_ms, wb_launches,
                                                        wb_b, wb_n)
     avg_launch_ms = dom_ms / max(dom_launches, 1)

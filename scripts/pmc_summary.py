@@ -18,7 +18,7 @@ from collections import defaultdict
 
 def family(name):
     short = name.split("(")[0].replace("void ", "").strip()
-    if short.startswith("tci::k_pass<"):
+    if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
         return "rrlu_write_back_pass" if "true>" in short else "rrlu_read_only_pass"
     return short
 
