@@ -29,11 +29,15 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def pass_bytes(m, n, r, nb, stride=1):
+def pass_bytes(m, n, r, nb, stride=1, shadow=True):
     """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-1 with k % stride == 0
-    (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block: a read-only pass
-    reads 8 B/element, every nb-th pass (pending count reaches nb; never the last) also writes
-    8 B/element back. Returns (read_only, write_back) as (bytes, launches)."""
+    (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block. Exact passes: a
+    read-only pass reads 8 B/element, every nb-th pass (pending count reaches nb; never the last)
+    also writes 8 B/element back. With the certified fp32 shadow search a
+    read-only pass streams the 4-B shadow instead, and a write-back pass also writes the shadow
+    (8 + 8 + 4 B/element); the exact re-reads of candidate chunks are data-dependent and not
+    counted. Returns (read_only, write_back) as (bytes, launches)."""
+    ro_per, wb_per = (4.0, 20.0) if shadow else (8.0, 16.0)
     ro_b = wb_b = 0.0
     ro_n = wb_n = 0
     pend = 0
@@ -46,10 +50,10 @@ def pass_bytes(m, n, r, nb, stride=1):
         if k % stride:
             continue
         if flush:
-            wb_b += 16.0 * elems
+            wb_b += wb_per * elems
             wb_n += 1
         else:
-            ro_b += 8.0 * elems
+            ro_b += ro_per * elems
             ro_n += 1
     return (ro_b, ro_n), (wb_b, wb_n)
 
@@ -69,8 +73,10 @@ def main():
                     help="diagnostic: no HIP events in the timed region (no roofline line)")
     ap.add_argument("--timing-stride", type=int, default=5,
                     help="time the rrLU pass of every s-th pivot with HIP events")
-    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "10")),
+    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "12")),
                     help="deferred-update depth of the rrLU (results are identical for every nb)")
+    ap.add_argument("--no-shadow", action="store_true",
+                    help="exact fp64 read-only passes instead of the certified fp32 shadow search")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,6 +93,8 @@ def main():
     # rehearse the multi-rank control flow on a one-GPU machine
     ctx = T.context(int(os.environ.get("TCI_BENCH_DEVICE", local_rank)))
     ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, args.nb))
+    shadow = not args.no_shadow and os.environ.get("TCI_RRLU_SHADOW", "1") != "0"
+    ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, int(shadow)))
     m, n, r = args.m, args.n, args.r
     A = T.DeviceMatrix(m, n, ctx=ctx)
     A.fill_uniform(seed=rank)
@@ -138,13 +146,15 @@ def main():
     flops = rrlu_flops(m, n, r)
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
-    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride)
+    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride, shadow)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
-        dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass2<P,false> (read-only: pending updates "
-                                                       "applied on the fly + abs2 argmax)", ro_ms,
-                                                       ro_launches, ro_b, ro_n)
+        dom, dom_ms, dom_launches, dom_bytes, dom_n = (
+            ("k_pass_sh<P> (read-only: fp32 shadow streamed, pending updates applied in fp32, "
+             "certified abs2 argmax with exact fp64 re-reads of candidate chunks)") if shadow else
+            "k_pass2<P,false> (read-only: pending updates applied on the fly + abs2 argmax)",
+            ro_ms, ro_launches, ro_b, ro_n)
     else:
         dom_key = "rrlu_write_back_pass"
         dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass2<P,true> (pending updates applied and "
@@ -180,11 +190,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
-                     "deferred_depth_nb": nb},
+                     "deferred_depth_nb": nb, "shadow_search": shadow},
     }
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
-    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb))
+    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, shadow))
     # roofline calibration on the same buffers: 16-B stream read and stream copy, best grid
     import ctypes as C
     nel = A.ld * n
@@ -213,12 +223,13 @@ def main():
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10}  # the bench command profiled there
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 12, "shadow": True}  # the profiled command
 
 
-def pmc_traffic(fam, m, n, r, nb):
+def pmc_traffic(fam, m, n, r, nb, shadow):
     """HBM bytes per launch of kernel family `fam` from the committed rocprofv3 PMC summary."""
-    if {"m": m, "n": n, "r": r, "nb": nb} != PMC_CONFIG or not os.path.exists(PMC_SUMMARY):
+    if ({"m": m, "n": n, "r": r, "nb": nb, "shadow": shadow} != PMC_CONFIG
+            or not os.path.exists(PMC_SUMMARY)):
         return {"traffic": None}
     with open(PMC_SUMMARY) as fh:
         rec = json.load(fh).get(fam, {})

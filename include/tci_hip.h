@@ -69,7 +69,7 @@ int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* l
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
-/* Deferred-update depth of the rrLU (1..16; default 10, env TCI_RRLU_NB): up to nb rank-1
+/* Deferred-update depth of the rrLU (1..16; default 12, env TCI_RRLU_NB): up to nb rank-1
  * updates are applied on the fly by read-only passes and written back every nb-th pivot.
  * Results are bitwise identical for every nb. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
@@ -82,6 +82,12 @@ int tci_set_rrlu_small(tci_ctx* ctx, int enabled);
  * enabled = 0 forces the pass pipeline. Bitwise identical results. Default on (env
  * TCI_RRLU_MID=0: off). */
 int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
+/* Certified fp32 search in the read-only passes of the pass pipeline: the write-back passes also
+ * keep an fp32 shadow of the stale values (+4 B/element of device memory), and a read-only pass
+ * streams it (4 B/element instead of 8), bounds the fp32 error, and re-reads in fp64 only the
+ * chunks that can hold the argmax. Bitwise identical results (same argmax, same tie order as
+ * submatrixargmax, matrixlu.jl:46-87). Default on (env TCI_RRLU_SHADOW=0: off). */
+int tci_set_rrlu_shadow(tci_ctx* ctx, int enabled);
 
 /* ------------------------------------------------------------ integrands */
 /* Uploads an integrand's parameters to the device once; localdims has L entries. */

@@ -18,8 +18,11 @@ from collections import defaultdict
 
 def family(name):
     short = name.split("(")[0].replace("void ", "").strip()
+    if short.startswith("tci::k_pass_sh<"):
+        return "rrlu_read_only_pass"
     if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
-        return "rrlu_write_back_pass" if "true>" in short else "rrlu_read_only_pass"
+        targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
+        return "rrlu_write_back_pass" if targs[1] == "true" else "rrlu_read_only_pass"
     return short
 
 

@@ -37,10 +37,13 @@ struct tci_ctx {
     size_t capX = 0;
     double* ybuf = nullptr;
     size_t capY = 0;
-    int flush_every = 10;  // deferred-update depth nb (1 = write back every pivot; 10 measured best)
+    int flush_every = 12;  // deferred-update depth nb (1 = write back every pivot; 12 measured best with the shadow search)
     int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int pass_percu = 1;    // one workgroup per CU, dynamic chunks (env TCI_PASS_PERCU=0: k_pass)
+    int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
+    float* sbuf = nullptr; // its fp32 shadow of the matrix
+    size_t capS = 0;
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int ncu = 0;           // compute units of the device
@@ -361,9 +364,18 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     g.ticket = c->ticket;
     g.selk = 0;
     const bool percu = c->pass_percu && c->ncu > 0;
+    // fp32 shadow for the certified search (4-row lanes need lda, lds multiples of 4)
+    const bool shadow = percu && c->shadow && lda % 4 == 0;
+    g.S = nullptr;
+    g.lds = 0;
+    if (shadow) {
+        g.lds = round_up(m, 16);
+        if ((st = ensure(c, &c->sbuf, &c->capS, (size_t)(g.lds * n)))) return st;
+        g.S = c->sbuf;
+    }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
                                       percu ? std::min(c->ncu, kMaxGrid) : std::min(c->pass_grid, kMaxGrid));
-    tci::launch_pass(c->stream, 0, false, percu, g, grid);  // argmax of A, selects pivot 0
+    tci::launch_pass(c->stream, 0, false, percu, shadow, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
     while (k < mr && !stopped) {
@@ -379,7 +391,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
             ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
-            tci::launch_pass(c->stream, P, flush, percu, g, grid);
+            tci::launch_pass(c->stream, P, flush, percu, shadow, g, grid);
             ev_end(c, sampled);
             if (flush) t0 = kk + 1;
         }
@@ -525,6 +537,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
     if (const char* e = getenv("TCI_PASS_PERCU")) c->pass_percu = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     {
@@ -561,7 +574,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (!c) return TCI_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     auto fr = [](void* p) { if (p) hipFree(p); };
-    fr(c->dA); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
+    fr(c->dA); fr(c->sbuf); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
     fr(c->ticket); fr(c->bar); fr(c->fault); fr(c->colbuf);
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
@@ -594,6 +607,11 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
 
 int tci_set_rrlu_small(tci_ctx* c, int enabled) {
     c->small_path = enabled != 0;
+    return TCI_OK;
+}
+
+int tci_set_rrlu_shadow(tci_ctx* c, int enabled) {
+    c->shadow = enabled != 0;
     return TCI_OK;
 }
 

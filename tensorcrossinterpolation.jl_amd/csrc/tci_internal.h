@@ -65,6 +65,10 @@ struct PassArgs {
     double* pivvals;
     double reltol, abstol;
     unsigned* ticket;  // zero between passes
+    // fp32 shadow of the stale values for the certified read-only passes (k_pass_sh), ld lds
+    // (multiple of 4); null when the shadow search is off
+    float* S;
+    int64_t lds;
 };
 
 // Selection fields of PassArgs as seen by the device.
@@ -98,7 +102,10 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // last workgroup selects pivot g.selk
 // percu: one 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2);
 // otherwise 256-thread workgroups with static shares (k_pass)
-void launch_pass(hipStream_t s, int P, bool flush, bool percu, const PassArgs& g, int grid);
+// shadow (percu only): the initial and write-back passes also store the fp32 shadow g.S, and
+// the read-only passes run the certified fp32 search (k_pass_sh; same results, ~half the bytes)
+void launch_pass(hipStream_t s, int P, bool flush, bool percu, bool shadow, const PassArgs& g,
+                 int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:

@@ -36,6 +36,9 @@
 #ifndef TCI_PASS2_U
 #define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
 #endif
+#ifndef TCI_PASS_SH_U
+#define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (4 rows x 16-B fp32 loads per column)
+#endif
 #ifndef TCI_FLUSH_NT
 #define TCI_FLUSH_NT 0  // write-back pass stores non-temporal
 #endif
@@ -117,7 +120,7 @@ __device__ __forceinline__ void block_reduce_cand(CandR& c) {
 // only there, after every other workgroup has finished reading them.
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
-                             double* pivvals);
+                             double* pivvals, int64_t rk = -1, int64_t ck = -1);
 
 __device__ __forceinline__ void store_cand_sc1(Cand* dst, const CandR& c) {
     uint64_t* d = reinterpret_cast<uint64_t*>(dst);
@@ -185,6 +188,13 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     if (!last_s) return;
     // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
     constexpr int CPT = kMaxPassGrid / NT;
+    // the physical row / column at position selk (swapped by the commit): requested with the
+    // candidates, not after them
+    int64_t rk = -1, ck = -1;
+    if (threadIdx.x == 0) {
+        rk = sel.rowphys[sel.selk];
+        ck = sel.colphys[sel.selk];
+    }
     CandR cs[CPT];
 #pragma unroll
     for (int u = 0; u < CPT; ++u) {
@@ -199,7 +209,7 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     if (threadIdx.x == 0) {
         __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
-                     sel.colphys, sel.pivvals);
+                     sel.colphys, sel.pivvals, rk, ck);
 #if TCI_PASS_PROF
         __threadfence();
         PPROF(5);
@@ -453,24 +463,65 @@ constexpr int kP2Slices = kRowsPerTile / 128;              // 128-row slices of 
 constexpr int kP2Reps = kP2Threads / 64 / kP2Slices;        // waves per slice
 constexpr int kP2StageCols = 512;                           // columns staged at once
 static_assert(kP2StageCols <= kP2Threads, "one staged column per thread");
+constexpr int kShSlices = kRowsPerTile / 256;               // shadow search: 256-row slices
+constexpr int kShReps = kP2Threads / 64 / kShSlices;        // waves per slice
 
-template <int P, bool FLUSH>
-__global__ __launch_bounds__(kP2Threads) void k_pass2(
-    double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
-    double* __restrict__ Y, int64_t ldy, double* __restrict__ Lp, int64_t ldl,
-    double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand, int cb, int rev,
-    SelArgs sel) {
+// Kernel view of PassArgs.
+struct PassK {
+    double* A;
+    int64_t lda;
+    int m, n, k;
+    double* X;
+    int64_t ldx;
+    double* Y;
+    int64_t ldy;
+    double* Lp;
+    int64_t ldl;
+    double* Up;
+    int64_t ldu;
+    int leftorth;
+    Cand* cand;
+    int cb;
+    int rev;
+    float* S;  // fp32 shadow of the stale values (ld lds), or null
+    int64_t lds;
+};
+
+// LDS of a one-workgroup-per-CU pass: the staged columns' y's [local column][slot] in fp64 (and
+// fp32 for the shadow search), their positions, the per-slice chunk counters and the shadow
+// search's threshold (float bits; non-negative floats order like their bits).
+template <int PP>
+struct P2Lds {
+    double ys[kP2StageCols * PP];
+    float yf[kP2StageCols * PP];
+    int cpos[kP2StageCols];
+    int cnt[kP2Slices];
+    unsigned tau;
+    double xk[kRowsPerTile];  // shadow search: x_k of the tile's rows (exact examinations)
+};
+
+// Body of the exact pass (k_pass2). SH: also store the fp32 shadow S of the values this pass
+// leaves as the new stale ones (write-back passes) or reads unmodified (the initial pass, P = 0).
+// Returns false when the factorisation has already stopped.
+template <int P, bool FLUSH, bool SH>
+__device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
+                                           P2Lds<(P > 0 ? P : 1)>& L, CandR& best,
+                                           unsigned long long (&pt)[6]) {
     RrluState* st = sel.st;
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
-    PPROF(0);
+    double* __restrict__ A = g.A;
+    const int64_t lda = g.lda;
+    const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
+    double* __restrict__ X = g.X;
+    double* __restrict__ Y = g.Y;
+    const int64_t ldx = g.ldx, ldy = g.ldy;
     constexpr int U = TCI_PASS2_U;
     static_assert(U <= 8 && 8 % U == 0, "U must divide every column-tile width");
     constexpr int PP = P > 0 ? P : 1;
-    __shared__ double ys[kP2StageCols * PP];
-    __shared__ int cpos_s[kP2StageCols];
-    __shared__ int cnt[kP2Slices];
+    double* ys = L.ys;
+    int* cpos_s = L.cpos;
+    int* cnt = L.cnt;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slice = wave % kP2Slices, rep = wave / kP2Slices;
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
@@ -519,7 +570,7 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(
     const int nch0 = ntc > 0 ? min(G, ntc) * cb / U : 0;
     if (rep < nch0) load_chunk(0, rep, va);
     if (rep + kP2Reps < nch0) load_chunk(0, rep + kP2Reps, vb);
-    if (st->done) return;
+    if (st->done) return false;
     int a = 0, b = 0;
     double piv = 1.0;
     if (P > 0) {
@@ -549,16 +600,15 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(
             double* xs = X + (int64_t)(P - 1) * ldx;
             if (in0) {
                 xs[r0] = xk0;
-                Lp[r0 + (int64_t)k * ldl] = xk0;
+                g.Lp[r0 + (int64_t)k * g.ldl] = xk0;
             }
             if (in1) {
                 xs[r0 + 1] = xk1;
-                Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
+                g.Lp[r0 + 1 + (int64_t)k * g.ldl] = xk1;
             }
         }
     }
     PPROF(1);
-    CandR best = cand_none();
     const bool wact = __any(active);  // wave-uniform: the slice has rows in the trailing block
     for (int g0 = 0; g0 < ntc; g0 += G) {
         const int gn = min(G, ntc - g0);
@@ -587,7 +637,7 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(
                 ys[lc * PP + P - 1] = yk;
                 if (tr == 0) {
                     Y[(int64_t)(P - 1) * ldy + jst] = yk;
-                    Up[k + (int64_t)jst * ldu] = yk;
+                    g.Up[k + (int64_t)jst * g.ldu] = yk;
                 }
             }
         }
@@ -614,6 +664,15 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(
                     __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
                 } else {
                     *pa = v;
+                }
+            }
+            if constexpr (SH) {
+                if ((FLUSH || P == 0) && rowok) {
+                    float* ps = g.S + r0 + (int64_t)j * g.lds;
+                    if (pair)
+                        *reinterpret_cast<float2*>(ps) = make_float2((float)v.x, (float)v.y);
+                    else
+                        ps[0] = (float)v.x;
                 }
             }
             const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
@@ -644,8 +703,346 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(
             if (h1 < nch) load_chunk(g0, h1, vb);
         }
     }
+    return true;
+}
+
+template <int P, bool FLUSH, bool SH>
+__global__ __launch_bounds__(kP2Threads) void k_pass2(PassK g, SelArgs sel) {
+    __shared__ P2Lds<(P > 0 ? P : 1)> L;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
+    CandR best = cand_none();
+    if (!pass2_body<P, FLUSH, SH>(g, sel, L, best, pt)) return;
     PPROF(3);
-    pass_tail<kP2Threads>(best, sel, cand, pt, m, P, (int)FLUSH);
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, (int)FLUSH);
+}
+
+// ------------------------------------------------------------------ shadow search
+// A read-only pass must find the exact argmax of abs2 over the updated trailing block, but it
+// does not need every exact value: it needs a certificate. The write-back passes (and the
+// initial one) also store S = fl32(stale value) (4 B/element). A read-only pass then streams S
+// instead of the fp64 values and applies the P pending updates in fp32 (FMA) with fp32 copies of
+// x_s and y_s. With M_f = |pivot k-P+1| (every stale trailing value is bounded by it: that pivot
+// was the argmax over the block the last write-back left) and |x_s[i] y_s[j]| <= |pivot_s| (full
+// pivoting), the fp32 value w of every trailing element is within
+//     eps = (P + 3) 2^-23 (M_f + 2 sum_s |pivot_s|) + (P + 2) 2^-124
+// of the exact fp64 value v the reference computes (error analysis in DESIGN.md: conversions,
+// one rounding per FMA, subnormal flushes, plus the fp64 chain's own roundings, with a 2x margin).
+// Every lane keeps the maximum |w| of each chunk it streams; c - eps is a proven lower bound on
+// the block's max |v|, and the workgroup shares the best such bound (tau, LDS). A chunk whose
+// c + eps falls below tau cannot hold the argmax -- nor any element tied with it in abs2 (the
+// comparison keeps a 2^-20 relative margin for the fp32 roundings of c, eps and tau) -- and is
+// skipped; the others (the running maxima, a handful per workgroup) are re-read in fp64 and
+// examined exactly, in the reference's operation order, with the reference's tie order. The
+// workgroup's candidate is therefore exactly what the exact pass produces, and the pass reads
+// ~4 B/element instead of 8. NaN elements (never selected by the reference) stay NaN in fp32 and
+// drop out of the maxima. When the bound is not tight (eps >= 2^-10 |pivot k|, a rapidly decaying
+// block) or fp32 could overflow, the kernel runs the exact body instead (uniform decision).
+template <int P>
+__device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel, P2Lds<P>& L,
+                                             CandR& best, float eps, unsigned long long (&pt)[6]) {
+    RrluState* st = sel.st;
+    const int32_t* colpos = sel.colpos;
+    const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev;
+    const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy, lds = g.lds;
+    constexpr int U = TCI_PASS_SH_U;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slice = wave % kShSlices, rep = wave / kShSlices;
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const int tiles_c = (n + cb - 1) / cb;
+    const int nq = gridDim.x / tiles_r;
+    const int tr = blockIdx.x % tiles_r;
+    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    const int G = kP2StageCols / cb;
+    // four rows per lane: 16-B fp32 loads (lda, ldx and lds are multiples of 4, r0 too, so the
+    // four rows of a lane with r0 < m are inside the column)
+    const int r0 = tr * kRowsPerTile + slice * 256 + 4 * lane;
+    const int rb = r0 < m ? r0 : 0;
+    const float* const sbase = g.S + rb;
+    const int cbs = __builtin_ctz(cb);  // cb is 8 or 16
+    auto chunk_col = [&](int g0, int h) -> int {
+        const int it = g0 + ((h * U) >> cbs);
+        return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + ((h * U) & (cb - 1));
+    };
+    auto load_chunk = [&](int g0, int h, float4 (&v)[U]) {
+        const int j = chunk_col(g0, h);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = *reinterpret_cast<const float4*>(sbase + (int64_t)min(j + u, n - 1) * lds);
+    };
+    auto stage_col = [&](int g0) -> int {
+        const int gn = min(G, ntc - g0);
+        const int lc = threadIdx.x;
+        if (lc >= gn * cb) return -1;
+        const int it = g0 + (lc >> cbs);
+        return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
+    };
+    int rp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) rp[t] = r0 + t < m ? sel.rowpos[r0 + t] : -1;
+    const int lrow = slice * 256 + 4 * lane;  // the lane's first row within the tile
+    int jst = ntc > 0 ? stage_col(0) : -1;
+    int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+    float4 va[U], vb[U];
+    const int nch0 = ntc > 0 ? min(G, ntc) * cb / U : 0;
+    if (rep < nch0) load_chunk(0, rep, va);
+    if (rep + kShReps < nch0) load_chunk(0, rep + kShReps, vb);
+    if (st->done) return false;
+    const int a = (int)st->p, b = (int)st->q;
+    const double piv = st->pval;
+    // the pivot-row element of this thread's first staged column: requested together with the
+    // pivot column below (one memory round trip for both instead of two in sequence)
+    const double ypr0 = g.A[a + (int64_t)((jst >= 0 && jst < n) ? jst : 0) * lda];
+    unsigned inm = 0;  // bit t: row r0 + t is in the trailing block
+#pragma unroll
+    for (int t = 0; t < 4; ++t) inm |= (rp[t] > k ? 1u : 0u) << t;
+    const bool active = inm != 0;
+    // pending x's in fp32; x_k exact (fp64, kept for the exact examinations) and in fp32
+    typedef float f2v __attribute__((ext_vector_type(2)));  // packed pairs: v_pk_fma_f32
+    f2v xf[P][2];  // rows (0, 1) and (2, 3) of the lane
+    {
+        double xk[4];
+        const double2 c0 = *reinterpret_cast<const double2*>(g.A + rb + (int64_t)b * lda);
+        const double2 c1 = *reinterpret_cast<const double2*>(g.A + rb + 2 + (int64_t)b * lda);
+        xk[0] = c0.x;
+        xk[1] = c0.y;
+        xk[2] = c1.x;
+        xk[3] = c1.y;
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) {
+            const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rb);
+            const double2 u1 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rb + 2);
+            const double yv = g.Y[(int64_t)s * ldy + b];
+            const double xs[4] = {u0.x, u0.y, u1.x, u1.y};
+            xf[s][0] = f2v{(float)xs[0], (float)xs[1]};
+            xf[s][1] = f2v{(float)xs[2], (float)xs[3]};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xk[t] = __dsub_rn(xk[t], __dmul_rn(xs[t], yv));
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (g.leftorth) xk[t] = xk[t] / piv;
+        xf[P - 1][0] = f2v{(float)xk[0], (float)xk[1]};
+        xf[P - 1][1] = f2v{(float)xk[2], (float)xk[3]};
+        if (rep == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) L.xk[lrow + t] = xk[t];
+            if (q == 0) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (inm >> t & 1) {
+                        g.X[(int64_t)(P - 1) * ldx + r0 + t] = xk[t];
+                        g.Lp[r0 + t + (int64_t)k * g.ldl] = xk[t];
+                    }
+            }
+        }
+    }
+    PPROF(1);
+    const bool wact = __any(active);
+    const float margin = 0x1p-20f;
+    float tau = 0.0f;  // this lane's view of the workgroup's lower bound on the max |v|
+    // chunk h's maximum |w| over the lane's trailing-block elements
+    auto approx = [&](int h, const float4 (&v)[U]) -> float {
+        float cm[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int lc = h * U + u;
+            if (L.cpos[lc] <= k) continue;  // wave-uniform
+            f2v w01 = {v[u].x, v[u].y}, w23 = {v[u].z, v[u].w};
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const float y = L.yf[lc * P + s];
+                const f2v yy = {y, y};
+                w01 = __builtin_elementwise_fma(-xf[s][0], yy, w01);
+                w23 = __builtin_elementwise_fma(-xf[s][1], yy, w23);
+            }
+            cm[0] = fmaxf(cm[0], fabsf(w01.x));
+            cm[1] = fmaxf(cm[1], fabsf(w01.y));
+            cm[2] = fmaxf(cm[2], fabsf(w23.x));
+            cm[3] = fmaxf(cm[3], fabsf(w23.y));
+        }
+        float c = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (inm >> t & 1) c = fmaxf(c, cm[t]);
+        return c;
+    };
+    // exact examination of chunks e0 / e1 (< 0: none; the lane's four rows), as the exact pass
+    // does it. One call site and rolled loops: it runs for a handful of chunks per workgroup.
+    auto examine = [&](int g0, int e0, int e1) {
+#pragma unroll 1
+        for (int z = 0; z < 2; ++z) {
+            const int h = z ? e1 : e0;
+            if (h < 0) continue;
+            // addresses recomputed here from an opaque copy of the row index: otherwise they are
+            // shared with the start-up code's and kept live (in registers) across the whole pass
+            int rbx = rb;
+            asm volatile("" : "+v"(rbx));
+            const int j0 = chunk_col(g0, h);
+#pragma unroll 1
+            for (int u = 0; u < U; ++u) {
+                const int lc = h * U + u;
+                const int cp = L.cpos[lc];
+                if (cp <= k) continue;
+                const int j = j0 + u;
+                const double* pa = g.A + rbx + (int64_t)j * lda;
+                const double2 p0 = *reinterpret_cast<const double2*>(pa);
+                const double2 p1 = *reinterpret_cast<const double2*>(pa + 2);
+                double v[4] = {p0.x, p0.y, p1.x, p1.y};
+#pragma unroll 1
+                for (int s = 0; s < P - 1; ++s) {
+                    const double y = L.ys[lc * P + s];
+                    const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rbx);
+                    const double2 u1 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rbx + 2);
+                    v[0] = __dsub_rn(v[0], __dmul_rn(u0.x, y));
+                    v[1] = __dsub_rn(v[1], __dmul_rn(u0.y, y));
+                    v[2] = __dsub_rn(v[2], __dmul_rn(u1.x, y));
+                    v[3] = __dsub_rn(v[3], __dmul_rn(u1.y, y));
+                }
+                const double yk = L.ys[lc * P + P - 1];
+#pragma unroll 1
+                for (int t = 0; t < 4; ++t) {
+                    if (!(inm >> t & 1)) continue;
+                    const double vt = __dsub_rn(v[t], __dmul_rn(L.xk[lrow + t], yk));
+                    const double a2 = __dmul_rn(vt, vt);
+                    if (a2 >= best.v) cand_take(best, CandR{a2, vt, cp, sel.rowpos[r0 + t], j, r0 + t});
+                }
+            }
+        }
+    };
+    // fold chunk maximum c into the bounds; true when the chunk must be examined exactly
+    auto test = [&](float c) -> bool {
+        const float lb = fmaxf(c - eps, 0.0f);
+        const float ts = __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        tau = fmaxf(tau, ts);
+        if (lb > tau) {
+            tau = lb;
+            atomicMax(&L.tau, __float_as_uint(lb));
+        }
+        return c + eps >= tau - tau * margin;
+    };
+    for (int g0 = 0; g0 < ntc; g0 += G) {
+        const int gn = min(G, ntc - g0);
+        const int nch = gn * cb / U;
+        if (g0 > 0) {
+            jst = stage_col(g0);
+            cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+            if (wact) {
+                if (rep < nch) load_chunk(g0, rep, va);
+                if (rep + kShReps < nch) load_chunk(g0, rep + kShReps, vb);
+            }
+            __syncthreads();
+        }
+        if (jst >= 0) {
+            int lc = threadIdx.x;
+            asm volatile("" : "+v"(lc));  // staging addresses: not hoisted out of the group loop
+            L.cpos[lc] = cpst;
+            if (cpst > k) {
+                double yk = g0 == 0 ? ypr0 : g.A[a + (int64_t)jst * lda];
+#pragma unroll
+                for (int s = 0; s < P - 1; ++s) {
+                    const double ysv = g.Y[(int64_t)s * ldy + jst];
+                    L.ys[lc * P + s] = ysv;
+                    L.yf[lc * P + s] = (float)ysv;
+                    yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv));
+                }
+                if (!g.leftorth) yk = yk / piv;
+                L.ys[lc * P + P - 1] = yk;
+                L.yf[lc * P + P - 1] = (float)yk;
+                if (tr == 0) {
+                    g.Y[(int64_t)(P - 1) * ldy + jst] = yk;
+                    g.Up[k + (int64_t)jst * g.ldu] = yk;
+                }
+            }
+        }
+        if (threadIdx.x < kShSlices) L.cnt[threadIdx.x] = 2 * kShReps;
+        if (g0 == 0 && threadIdx.x == 0) L.tau = 0u;
+        __syncthreads();
+        if (g0 == 0) PPROF(2);
+        auto grab = [&]() -> int {
+            int h = 0;
+            if (lane == 0) h = atomicAdd(&L.cnt[slice], 1);
+            return __shfl(h, 0);
+        };
+        int h0 = rep, h1 = rep + kShReps;
+        int ex0 = -1, ex1 = -1;  // chunks to examine exactly
+        if (g0 == 0) {
+            // seed: the first two chunks of every wave set the workgroup's bound before any exact
+            // examination, so only chunks near the workgroup's maximum are ever re-read
+            float c0 = -1.0f, c1 = -1.0f;
+            const int e0 = h0, e1 = h1;
+            if (wact) {
+                if (h0 < nch) {
+                    c0 = approx(h0, va);
+                    h0 = grab();
+                    if (h0 < nch) load_chunk(g0, h0, va);
+                }
+                if (h1 < nch) {
+                    c1 = approx(h1, vb);
+                    h1 = grab();
+                    if (h1 < nch) load_chunk(g0, h1, vb);
+                }
+                float lb = fmaxf(fmaxf(c0, c1) - eps, 0.0f);
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) lb = fmaxf(lb, __shfl_xor(lb, off));
+                if (lane == 0) atomicMax(&L.tau, __float_as_uint(lb));
+            }
+            __syncthreads();
+            if (!wact) continue;
+            tau = __uint_as_float(L.tau);
+            if (c0 >= 0.0f && c0 + eps >= tau - tau * margin) ex0 = e0;
+            if (c1 >= 0.0f && c1 + eps >= tau - tau * margin) ex1 = e1;
+        } else if (!wact) {
+            continue;
+        }
+        // h0's values in va, h1's in vb; every grab returns a larger index than both
+        for (;;) {
+            if (ex0 >= 0 || ex1 >= 0) examine(g0, ex0, ex1);
+            ex0 = ex1 = -1;
+            if (h0 >= nch) break;
+            {
+                const float c = approx(h0, va);
+                const int e = h0;
+                h0 = grab();
+                if (h0 < nch) load_chunk(g0, h0, va);
+                if (test(c)) ex0 = e;
+            }
+            if (h1 < nch) {
+                const float c = approx(h1, vb);
+                const int e = h1;
+                h1 = grab();
+                if (h1 < nch) load_chunk(g0, h1, vb);
+                if (test(c)) ex1 = e;
+            }
+        }
+    }
+    return true;
+}
+
+template <int P>
+__global__ __launch_bounds__(kP2Threads) void k_pass_sh(PassK g, SelArgs sel) {
+    __shared__ P2Lds<P> L;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
+    // error bound of the fp32 search over pending pivots k-P+1 .. k (uniform)
+    const double* pv = sel.pivvals;
+    const double Mf = fabs(pv[g.k - P + 1]);
+    double sumM = 0.0;
+#pragma unroll
+    for (int s = 0; s < P; ++s) sumM += fabs(pv[g.k - P + 1 + s]);
+    const double mag = Mf + 2.0 * sumM;
+    const double epsd = (double)(P + 3) * 0x1p-23 * mag + (double)(P + 2) * 0x1p-124;
+    const bool shok = mag < 0x1p100 && epsd < 0x1p-10 * fabs(pv[g.k]);
+    CandR best = cand_none();
+    bool go;
+    if (shok)
+        go = pass_sh_body<P>(g, sel, L, best, (float)(epsd * (1.0 + 0x1p-20)), pt);
+    else
+        go = pass2_body<P, false, false>(g, sel, L, best, pt);
+    if (!go) return;
+    PPROF(3);
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, 0);
 }
 
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
@@ -661,30 +1058,40 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 }
 
 template <int P>
-static void launch_pass_p(hipStream_t s, bool flush, bool percu, const PassArgs& g, int grid) {
+static void launch_pass_p(hipStream_t s, bool flush, bool percu, bool shadow, const PassArgs& g,
+                          int grid) {
     const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals,
                       g.st,     g.ticket, g.reltol,  g.abstol,  g.selk};
+    if (percu) {
+        const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
+                      g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
+        if (shadow) {
+            if (flush || P == 0)
+                hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            else if constexpr (P > 0)
+                hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        } else if (flush) {
+            hipLaunchKernelGGL((k_pass2<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        } else {
+            hipLaunchKernelGGL((k_pass2<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        }
+        return;
+    }
 #define TCI_PASS_LAUNCH(KERN, NT)                                                                  \
     hipLaunchKernelGGL(KERN, dim3(grid), dim3(NT), 0, s, g.A, g.lda, g.m, g.n, g.k, g.X, g.ldx, g.Y, \
                        g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb, g.rev, sel)
-    if (percu) {
-        if (flush)
-            TCI_PASS_LAUNCH((k_pass2<P, true>), kP2Threads);
-        else
-            TCI_PASS_LAUNCH((k_pass2<P, false>), kP2Threads);
-    } else {
-        if (flush)
-            TCI_PASS_LAUNCH((k_pass<P, true>), kUpdThreads);
-        else
-            TCI_PASS_LAUNCH((k_pass<P, false>), kUpdThreads);
-    }
+    if (flush)
+        TCI_PASS_LAUNCH((k_pass<P, true>), kUpdThreads);
+    else
+        TCI_PASS_LAUNCH((k_pass<P, false>), kUpdThreads);
 #undef TCI_PASS_LAUNCH
 }
 
-void launch_pass(hipStream_t s, int P, bool flush, bool percu, const PassArgs& g, int grid) {
+void launch_pass(hipStream_t s, int P, bool flush, bool percu, bool shadow, const PassArgs& g,
+                 int grid) {
     switch (P) {
 #define TCI_PASS_CASE(p) \
-    case p: launch_pass_p<p>(s, flush, percu, g, grid); break;
+    case p: launch_pass_p<p>(s, flush, percu, shadow, g, grid); break;
         TCI_PASS_CASE(0) TCI_PASS_CASE(1) TCI_PASS_CASE(2) TCI_PASS_CASE(3) TCI_PASS_CASE(4)
         TCI_PASS_CASE(5) TCI_PASS_CASE(6) TCI_PASS_CASE(7) TCI_PASS_CASE(8) TCI_PASS_CASE(9)
         TCI_PASS_CASE(10) TCI_PASS_CASE(11) TCI_PASS_CASE(12) TCI_PASS_CASE(13) TCI_PASS_CASE(14)
@@ -701,7 +1108,7 @@ void launch_pass(hipStream_t s, int P, bool flush, bool percu, const PassArgs& g
 // the columns at k and q (swapcol!, :269-275). One thread.
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
-                             double* pivvals) {
+                             double* pivvals, int64_t rk, int64_t ck) {
     int pr = best.pr, pc = best.pc, rp = best.rpos, cp = best.cpos;
     double val = best.val;
     if (!(best.v >= 0.0)) {
@@ -726,13 +1133,13 @@ __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double rel
     st->np = k + 1;
     pivvals[k] = val;
     // swaprow!(k, rp): the physical row at position k moves to position rp
-    const int64_t rk = rowphys[k];
+    if (rk < 0) rk = rowphys[k];
     rowphys[k] = pr;
     rowphys[rp] = rk;
     rowpos[pr] = k;
     rowpos[rk] = rp;
     // swapcol!(k, cp)
-    const int64_t ck = colphys[k];
+    if (ck < 0) ck = colphys[k];
     colphys[k] = pc;
     colphys[cp] = ck;
     colpos[pc] = k;

@@ -53,6 +53,7 @@ SIGNATURES = {
     "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_small": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_mid": ([vp, C.c_int], C.c_int),
+    "tci_set_rrlu_shadow": ([vp, C.c_int], C.c_int),
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),

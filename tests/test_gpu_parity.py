@@ -16,14 +16,16 @@ pytestmark = pytest.mark.gpu
 T = pytest.importorskip("tci_amd")
 
 
-@pytest.fixture(scope="module", params=["default", "mid", "pipeline"])
+@pytest.fixture(scope="module", params=["default", "mid", "pipeline", "pipeline_exact"])
 def ctx(request):
-    """Every test runs three times: with the default size-based choice of rrLU path (one-workgroup
+    """Every test runs four times: with the default size-based choice of rrLU path (one-workgroup
     LDS kernel for small Pi, persistent grid for mid-size Pi, the pass pipeline above), with the
-    mid-size path for everything it fits, and with the pass pipeline forced for every size."""
+    mid-size path for everything it fits, and with the pass pipeline forced for every size, with
+    the certified fp32 shadow search (default) and without it (every pass reads fp64)."""
     c = T.Context(0)
     c.check(c.lib.tci_set_rrlu_small(c.h, int(request.param == "default")))
-    c.check(c.lib.tci_set_rrlu_mid(c.h, int(request.param != "pipeline")))
+    c.check(c.lib.tci_set_rrlu_mid(c.h, int(request.param not in ("pipeline", "pipeline_exact"))))
+    c.check(c.lib.tci_set_rrlu_shadow(c.h, int(request.param != "pipeline_exact")))
     yield c
     c.close()
 
