@@ -68,18 +68,67 @@ __device__ __forceinline__ void cand_take(CandR& a, const CandR& b) {
     if (cand_better(b.v, b.cpos, b.rpos, a.v, a.cpos, a.rpos)) a = b;
 }
 
+// Wave argmax of the candidates on DPP lane moves (VALU; ds_bpermute shuffles of all six fields
+// cost ~2 us per wave on the pass's critical path): (abs2, column position, row position, lane)
+// is reduced within rows of 16 lanes (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror), then across the four rows by readlane; the winning lane's fields are read last.
+// Candidate abs2 values are never NaN (the passes only take a2 >= best).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void dpp_take_cand(double& bv, unsigned& bc, unsigned& br, unsigned& bl) {
+    const uint64_t b = (uint64_t)__double_as_longlong(bv);
+    const uint64_t o = ((uint64_t)dpp_u32<CTRL>((unsigned)(b >> 32)) << 32) | dpp_u32<CTRL>((unsigned)b);
+    const double ov = __longlong_as_double((long long)o);
+    const unsigned oc = dpp_u32<CTRL>(bc), orr = dpp_u32<CTRL>(br), ol = dpp_u32<CTRL>(bl);
+    const bool better = (ov > bv) || (ov == bv && (oc < bc || (oc == bc && orr < br)));
+    bv = better ? ov : bv;
+    bc = better ? oc : bc;
+    br = better ? orr : br;
+    bl = better ? ol : bl;
+}
+
+__device__ __forceinline__ double readlane_dbl(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// every lane ends with the wave's winner
 __device__ __forceinline__ void wave_reduce_cand(CandR& c) {
+    double bv = c.v;
+    unsigned bc = (unsigned)c.cpos, br = (unsigned)c.rpos, bl = threadIdx.x & 63;
+    dpp_take_cand<0xb1>(bv, bc, br, bl);
+    dpp_take_cand<0x4e>(bv, bc, br, bl);
+    dpp_take_cand<0x141>(bv, bc, br, bl);
+    dpp_take_cand<0x140>(bv, bc, br, bl);
+    double v = readlane_dbl(bv, 0);
+    unsigned cc = (unsigned)__builtin_amdgcn_readlane((int)bc, 0);
+    unsigned rr = (unsigned)__builtin_amdgcn_readlane((int)br, 0);
+    unsigned ln = (unsigned)__builtin_amdgcn_readlane((int)bl, 0);
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        CandR o;
-        o.v = __shfl_xor(c.v, off);
-        o.val = __shfl_xor(c.val, off);
-        o.cpos = __shfl_xor(c.cpos, off);
-        o.rpos = __shfl_xor(c.rpos, off);
-        o.pc = __shfl_xor(c.pc, off);
-        o.pr = __shfl_xor(c.pr, off);
-        cand_take(c, o);
+    for (int r = 16; r < 64; r += 16) {
+        const double ov = readlane_dbl(bv, r);
+        const unsigned oc = (unsigned)__builtin_amdgcn_readlane((int)bc, r);
+        const unsigned orr = (unsigned)__builtin_amdgcn_readlane((int)br, r);
+        const unsigned ol = (unsigned)__builtin_amdgcn_readlane((int)bl, r);
+        const bool better = (ov > v) || (ov == v && (oc < cc || (oc == cc && orr < rr)));
+        v = better ? ov : v;
+        cc = better ? oc : cc;
+        rr = better ? orr : rr;
+        ln = better ? ol : ln;
     }
+    const int w = (int)ln;
+    c.v = v;
+    c.cpos = (int)cc;
+    c.rpos = (int)rr;
+    c.val = readlane_dbl(c.val, w);
+    c.pc = __builtin_amdgcn_readlane(c.pc, w);
+    c.pr = __builtin_amdgcn_readlane(c.pr, w);
 }
 
 __device__ __forceinline__ CandR cand_none() { return CandR{-1.0, 0.0, kBig, kBig, 0, 0}; }
