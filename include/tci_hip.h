@@ -45,7 +45,13 @@ extern "C" {
 #define TCI_F_QEXP 6     /* quantics x: p0 exp(-p1 x) + p2 exp(-p3 x)   (test_tensorci2.jl:65)  */
 #define TCI_F_TT 7       /* tensor-train evaluation (test_tensorci2.jl:477-502, TTCache as f)   */
 #define TCI_F_CP 8       /* f(x) = sum_k prod_t g[k][t][x_t]: CP-rank-K synthetic */
-/* GAUSSMIX and CP are sums of K separable terms: Pi is assembled as a rank-K fp64 MFMA GEMM.
+#define TCI_F_MPO 9      /* Contraction(A, B) of two 4-leg tensor trains (contraction.jl:60-575)  */
+/* GAUSSMIX, CP and MPO are sums of K separable terms: Pi is assembled as a rank-K fp64 MFMA GEMM
+ * (MPO: K = ra*rb at the cut, the factor rows are the left / right environments).
+ * MPO params: [N, per site t (ra, d1, d2, ra', rb, d3, rb', offA, offB), cores]: A_t is
+ * (ra, d1, d2, ra'), B_t is (rb, d2, d3, rb'), column-major at offA / offB past the 1 + 9N header;
+ * localdims[t] = d1 * d3 (fused index s1 + d1 (s3 - 1), contraction.jl:226-237); boundary bonds 1;
+ * every bond ra * rb <= 2048, every site rb*d2*ra' and ra*d2*rb' <= 8192 (TCI_ERR_ARG otherwise).
  * params: GAUSSMIX [K, a, centres (K x L, row-major), weights (K)];
  *         CP       [K, dmax, g (K x L x dmax, dmax fastest)] with dmax >= max(localdims). */
 

@@ -76,7 +76,7 @@ void orc_fill_uniform(double* a, i64 n, uint64_t seed, i64 offset) {
  * _batchevaluate_dispatch does (batcheval.jl:157-171). x is 1-based, length L. */
 enum {
     F_SUM = 0, F_LORENTZ = 1, F_TABLE = 2, F_GAUSS = 3, F_GAUSSMIX = 4,
-    F_QOSC = 5, F_QEXP = 6, F_TT = 7, F_CP = 8
+    F_QOSC = 5, F_QEXP = 6, F_TT = 7, F_CP = 8, F_MPO = 9
 };
 typedef struct {
     int kind;
@@ -91,6 +91,82 @@ static double quantics_x(const i32* x, int L) {
     uint64_t idx = 0;
     for (int t = 0; t < L; ++t) idx = (idx << 1) | (uint64_t)(x[t] - 1);
     return ldexp((double)idx, -L);
+}
+
+/* Contraction(A, B) at one point (contraction.jl:365-406): evaluate splits at midpoint = N / 2,
+ * the left environment of sites 1..midpoint (evaluateleft, :279-310, built with _extend_cache,
+ * :253-259: tmp1 = oldcache^T-contracted with a[:, i, :, :], then with b[:, :, j, :]), the right
+ * one of the rest (evaluateright, :323-354, the same on the mirrored cores), and
+ * sum(left .* right). p: [N, per site (ra, d1, d2, ra', rb, d3, rb', offA, offB), cores]. */
+static double mpo_eval(const double* p, const i32* x) {
+    int N = (int)p[0];
+    const double* data = p + 1 + 9 * N;
+    static double envL[4096], envR[4096], tmp[16384];
+    int mid = N / 2;
+    int la = 1, lb = 1, ra_ = 1, rb_ = 1;
+    envL[0] = 1.0;
+    for (int t = 0; t < mid; ++t) {
+        const double* q = p + 1 + 9 * t;
+        int ra = (int)q[0], d1 = (int)q[1], d2 = (int)q[2], ra2 = (int)q[3];
+        int rb = (int)q[4], d3 = (int)q[5], rb2 = (int)q[6];
+        const double* A = data + (i64)q[7];
+        const double* B = data + (i64)q[8];
+        int s1 = (x[t] - 1) % d1, s3 = (x[t] - 1) / d1;
+        /* tmp1[b, s2, a'] = sum_a old[a, b] a[a, s1, s2, a'] */
+        for (int a2 = 0; a2 < ra2; ++a2)
+            for (int s2 = 0; s2 < d2; ++s2)
+                for (int b = 0; b < rb; ++b) {
+                    double acc = 0.0;
+                    for (int a = 0; a < ra; ++a)
+                        acc = acc + envL[a + ra * b] * A[a + (i64)ra * (s1 + (i64)d1 * (s2 + (i64)d2 * a2))];
+                    tmp[b + rb * (s2 + d2 * a2)] = acc;
+                }
+        /* new[a', b'] = sum_{s2, b} tmp1[b, s2, a'] b[b, s2, s3, b'] */
+        for (int b2 = 0; b2 < rb2; ++b2)
+            for (int a2 = 0; a2 < ra2; ++a2) {
+                double acc = 0.0;
+                for (int s2 = 0; s2 < d2; ++s2)
+                    for (int b = 0; b < rb; ++b)
+                        acc = acc + tmp[b + rb * (s2 + d2 * a2)] * B[b + (i64)rb * (s2 + (i64)d2 * (s3 + (i64)d3 * b2))];
+                envL[a2 + ra2 * b2] = acc;
+            }
+        la = ra2;
+        lb = rb2;
+    }
+    envR[0] = 1.0;
+    for (int t = N - 1; t >= mid; --t) {
+        const double* q = p + 1 + 9 * t;
+        int ra = (int)q[0], d1 = (int)q[1], d2 = (int)q[2], ra2 = (int)q[3];
+        int rb = (int)q[4], d3 = (int)q[5], rb2 = (int)q[6];
+        const double* A = data + (i64)q[7];
+        const double* B = data + (i64)q[8];
+        int s1 = (x[t] - 1) % d1, s3 = (x[t] - 1) / d1;
+        /* tmp[a, s2, b'] = sum_a' a[a, s1, s2, a'] old[a', b'] */
+        for (int b2 = 0; b2 < rb2; ++b2)
+            for (int s2 = 0; s2 < d2; ++s2)
+                for (int a = 0; a < ra; ++a) {
+                    double acc = 0.0;
+                    for (int a2 = 0; a2 < ra2; ++a2)
+                        acc = acc + A[a + (i64)ra * (s1 + (i64)d1 * (s2 + (i64)d2 * a2))] * envR[a2 + ra2 * b2];
+                    tmp[a + ra * (s2 + d2 * b2)] = acc;
+                }
+        /* new[a, b] = sum_{b', s2} tmp[a, s2, b'] b[b, s2, s3, b'] */
+        for (int b = 0; b < rb; ++b)
+            for (int a = 0; a < ra; ++a) {
+                double acc = 0.0;
+                for (int b2 = 0; b2 < rb2; ++b2)
+                    for (int s2 = 0; s2 < d2; ++s2)
+                        acc = acc + tmp[a + ra * (s2 + d2 * b2)] * B[b + (i64)rb * (s2 + (i64)d2 * (s3 + (i64)d3 * b2))];
+                envR[a + ra * b] = acc;
+            }
+        ra_ = ra;
+        rb_ = rb;
+    }
+    (void)ra_;
+    (void)rb_;
+    double res = 0.0;
+    for (int e = 0; e < la * lb; ++e) res = res + envL[e] * envR[e];
+    return res;
 }
 
 static double feval(const orc_func* f, const i32* x) {
@@ -173,6 +249,8 @@ static double feval(const orc_func* f, const i32* x) {
         }
         return v[0];
     }
+    case F_MPO:
+        return mpo_eval(p, x);
     case F_CP: {
         /* CP-rank-K synthetic of SURVEY.md 8(d) (config 5): sum_k prod_t g[k][t][x_t];
          * p = [K, dmax, g (K x L x dmax, dmax fastest)] */

@@ -640,7 +640,7 @@ int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* lau
 int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
                     const int32_t* localdims, int32_t L, tci_func** out) {
     if (!c || !out) return TCI_ERR_ARG;
-    if (kind < TCI_F_SUM || kind > TCI_F_CP) return set_err(c, TCI_ERR_ARG, "unknown integrand kind");
+    if (kind < TCI_F_SUM || kind > TCI_F_MPO) return set_err(c, TCI_ERR_ARG, "unknown integrand kind");
     if (L < 1) return set_err(c, TCI_ERR_ARG, "L must be >= 1");
     if (L > 62 && (kind == TCI_F_QOSC || kind == TCI_F_QEXP))
         return set_err(c, TCI_ERR_ARG, "quantics integrands support at most 62 legs");
@@ -656,6 +656,35 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
             need = 2 + (int64_t)cpK * L * dmax;
         }
         if (nparams < need) return set_err(c, TCI_ERR_ARG, "params too short for K terms");
+    }
+    if (kind == TCI_F_MPO) {
+        // Contraction(A, B) (contraction.jl:121-152): matching lengths, shared index d2, bonds
+        if (nparams < 1 || !params || (int64_t)params[0] != L)
+            return set_err(c, TCI_ERR_ARG, "Tensor trains must have the same length.");
+        if (nparams < 1 + 9 * (int64_t)L) return set_err(c, TCI_ERR_ARG, "MPO params too short");
+        const int64_t hdr = 1 + 9 * (int64_t)L;
+        for (int t = 0; t < L; ++t) {
+            const double* q = params + 1 + 9 * t;
+            const int64_t ra = (int64_t)q[0], d1 = (int64_t)q[1], d2 = (int64_t)q[2], ra2 = (int64_t)q[3];
+            const int64_t rb = (int64_t)q[4], d3 = (int64_t)q[5], rb2 = (int64_t)q[6];
+            const int64_t offA = (int64_t)q[7], offB = (int64_t)q[8];
+            if (ra < 1 || d1 < 1 || d2 < 1 || ra2 < 1 || rb < 1 || d3 < 1 || rb2 < 1)
+                return set_err(c, TCI_ERR_ARG, "MPO: dimensions must be positive");
+            if (d1 * d3 != localdims[t]) return set_err(c, TCI_ERR_ARG, "MPO: localdims[t] must be d1 * d3");
+            if ((t == 0 && (ra != 1 || rb != 1)) || (t == L - 1 && (ra2 != 1 || rb2 != 1)))
+                return set_err(c, TCI_ERR_ARG, "MPO: boundary bond dimensions must be 1");
+            if (t + 1 < L) {
+                const double* nq = params + 1 + 9 * (t + 1);
+                if ((int64_t)nq[0] != ra2 || (int64_t)nq[4] != rb2)
+                    return set_err(c, TCI_ERR_ARG, "MPO: bond dimensions do not match");
+            }
+            if (ra * rb > tci::kMpoEnv || rb * d2 * ra2 > tci::kMpoTmp || ra * d2 * rb2 > tci::kMpoTmp)
+                return set_err(c, TCI_ERR_ARG, "MPO: bond dimensions exceed the environment kernel's LDS");
+            if (offA < 0 || offB < 0 || hdr + offA + ra * d1 * d2 * ra2 > nparams ||
+                hdr + offB + rb * d2 * d3 * rb2 > nparams)
+                return set_err(c, TCI_ERR_ARG, "MPO: cores outside params");
+            cpK = std::max<int32_t>(cpK, (int32_t)(ra * rb));
+        }
     }
     if (kind == TCI_F_TABLE) {
         int64_t cnt = 1;

@@ -4,6 +4,8 @@
 // Compiled with -ffp-contract=off: no multiply-add is fused unless written as such.
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "tci_internal.h"
@@ -283,11 +285,13 @@ void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t
 // per-row and per-column "state" (O((m+n)L)), then one pass that combines and writes
 // Pi[R + ldo*j] -- an HBM-write-bound stream. Other kinds evaluate directly per element.
 enum { F_SUM = 0, F_LORENTZ = 1, F_TABLE = 2, F_GAUSS = 3, F_GAUSSMIX = 4, F_QOSC = 5, F_QEXP = 6,
-       F_TT = 7, F_CP = 8 };
+       F_TT = 7, F_CP = 8, F_MPO = 9 };
 
 // Kinds that are a sum of K separable terms, f = sum_k rowfactor_k(I, c) * colfactor_k(J): Pi is
 // a rank-K product EL * ER^T, assembled by an fp64 MFMA GEMM (k_gemm_cp).
-__host__ __device__ __forceinline__ bool cp_kind(int kind) { return kind == F_GAUSSMIX || kind == F_CP; }
+__host__ __device__ __forceinline__ bool cp_kind(int kind) {
+    return kind == F_GAUSSMIX || kind == F_CP || kind == F_MPO;
+}
 
 __host__ __device__ __forceinline__ bool staged_kind(int kind) {
     return kind == F_SUM || kind == F_LORENTZ || kind == F_TABLE || kind == F_GAUSS ||
@@ -613,6 +617,120 @@ __global__ void k_cp_factors(FuncDev f, const int32_t* __restrict__ T, int cnt, 
     }
 }
 
+// ------------------------------------------------ MPO-MPO contraction (contraction.jl)
+// f = Contraction(A, B) (contraction.jl:60-152): f(x) = the product of A_t[:, s1, :, :] and
+// B_t[:, :, s3, :] over all sites, every inner index summed, with x_t the fused site index
+// s1 + d1 (s3 - 1) (_unfuse_idx / _fuse_idx, contraction.jl:226-237). For a split of the legs
+// into row legs and column legs, Pi[R, j] = sum_{a,b} Lenv_R[a, b] Renv_j[a, b]: the left and
+// right environments (evaluateleft / evaluateright, contraction.jl:279-354, with the centre leg
+// of batchevaluate folded into the rows, :483-575). So a contraction is a separable kind of K =
+// ra*rb terms at the cut: k_mpo_env computes the environments as the factor rows (batched small
+// contractions, one workgroup per row, intermediates in LDS) and the fp64 MFMA GEMM (k_gemm_cp*)
+// assembles Pi.
+// params: [N, per site t: ra, d1, d2, ra', rb, d3, rb', offA, offB, then the cores]; core A_t is
+// (ra, d1, d2, ra') and B_t (rb, d2, d3, rb'), column-major, at the given offsets past the header.
+struct MpoSite {
+    int ra, d1, d2, ra2, rb, d3, rb2;
+    int64_t offA, offB;
+};
+
+__device__ __forceinline__ MpoSite mpo_site(const double* p, int t) {
+    const double* q = p + 1 + 9 * t;
+    return MpoSite{(int)q[0], (int)q[1], (int)q[2], (int)q[3], (int)q[4],
+                   (int)q[5], (int)q[6], (int64_t)q[7], (int64_t)q[8]};
+}
+
+// Environment rows: R in [0, nrows * D) (i = R % nrows, centre c = R / nrows when M == 1). Left:
+// sites 0 .. nlegs-1 in order; right: sites t0 .. t0+nlegs-1 from the last one backwards. Writes
+// out[k * ld + R] for k < K4 (k = a + ra_cut * b; zero past the cut's ra * rb) and zeroes the
+// padding rows [nrows * D, ld).
+__global__ __launch_bounds__(256) void k_mpo_env(FuncDev f, const int32_t* __restrict__ T, int cnt,
+                                                 int nrows, int D, int M, int K4, int64_t ld, int t0,
+                                                 int right, double* __restrict__ out) {
+    __shared__ double env[kMpoEnv];
+    __shared__ double tmp[kMpoTmp];
+    const double* p = f.params;
+    const int N = (int)p[0];
+    const double* data = p + 1 + 9 * (int64_t)N;
+    const int nlegs = cnt + (M ? 1 : 0);
+    const int64_t rows = (int64_t)nrows * D;
+    for (int64_t e = rows * K4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ld * K4;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = (e - rows * K4) / (ld - rows), R = rows + (e - rows * K4) % (ld - rows);
+        out[k * ld + R] = 0.0;
+    }
+    for (int64_t R = blockIdx.x; R < rows; R += gridDim.x) {
+        const int i = (int)(R % nrows), c = (int)(R / nrows);
+        const int32_t* e = T + (int64_t)i * cnt;
+        if (threadIdx.x == 0) env[0] = 1.0;
+        int ea = 1, eb = 1;
+        __syncthreads();
+        for (int q = 0; q < nlegs; ++q) {
+            const int leg = right ? nlegs - 1 - q : q;
+            const int t = right ? t0 + leg : leg;
+            const int idx = (leg < cnt ? e[leg] : c + 1) - 1;
+            const MpoSite s = mpo_site(p, t);
+            const int s1 = idx % s.d1, s3 = idx / s.d1;
+            const double* A = data + s.offA;
+            const double* B = data + s.offB;
+            if (!right) {
+                // tmp[b, s2, a'] = sum_a env[a, b] A[a, s1, s2, a']   (_extend_cache, first step)
+                const int nt = s.rb * s.d2 * s.ra2;
+                for (int o = threadIdx.x; o < nt; o += blockDim.x) {
+                    const int b = o % s.rb, s2 = (o / s.rb) % s.d2, a2 = o / (s.rb * s.d2);
+                    const double* Ap = A + (int64_t)s.ra * (s1 + (int64_t)s.d1 * (s2 + (int64_t)s.d2 * a2));
+                    double acc = 0.0;
+                    for (int a = 0; a < s.ra; ++a) acc = acc + env[a + s.ra * b] * Ap[a];
+                    tmp[o] = acc;
+                }
+                __syncthreads();
+                // env[a', b'] = sum_{s2, b} tmp[b, s2, a'] B[b, s2, s3, b']   (second step)
+                const int ne = s.ra2 * s.rb2;
+                for (int o = threadIdx.x; o < ne; o += blockDim.x) {
+                    const int a2 = o % s.ra2, b2 = o / s.ra2;
+                    const double* Bp = B + (int64_t)s.rb * s.d2 * (s3 + (int64_t)s.d3 * b2);
+                    double acc = 0.0;
+                    for (int s2 = 0; s2 < s.d2; ++s2)
+                        for (int b = 0; b < s.rb; ++b)
+                            acc = acc + tmp[b + s.rb * (s2 + s.d2 * a2)] * Bp[b + (int64_t)s.rb * s2];
+                    env[o] = acc;
+                }
+                ea = s.ra2;
+                eb = s.rb2;
+            } else {
+                // tmp[a, s2, b'] = sum_a' A[a, s1, s2, a'] env[a', b']
+                const int nt = s.ra * s.d2 * s.rb2;
+                const int64_t sa = (int64_t)s.ra * s.d1 * s.d2;
+                for (int o = threadIdx.x; o < nt; o += blockDim.x) {
+                    const int a = o % s.ra, s2 = (o / s.ra) % s.d2, b2 = o / (s.ra * s.d2);
+                    const double* Ap = A + a + (int64_t)s.ra * (s1 + (int64_t)s.d1 * s2);
+                    double acc = 0.0;
+                    for (int a2 = 0; a2 < s.ra2; ++a2) acc = acc + Ap[sa * a2] * env[a2 + s.ra2 * b2];
+                    tmp[o] = acc;
+                }
+                __syncthreads();
+                // env[a, b] = sum_{b', s2} tmp[a, s2, b'] B[b, s2, s3, b']
+                const int ne = s.ra * s.rb;
+                for (int o = threadIdx.x; o < ne; o += blockDim.x) {
+                    const int a = o % s.ra, b = o / s.ra;
+                    double acc = 0.0;
+                    for (int b2 = 0; b2 < s.rb2; ++b2) {
+                        const double* Bp = B + b + (int64_t)s.rb * s.d2 * (s3 + (int64_t)s.d3 * b2);
+                        for (int s2 = 0; s2 < s.d2; ++s2)
+                            acc = acc + tmp[a + s.ra * (s2 + s.d2 * b2)] * Bp[(int64_t)s.rb * s2];
+                    }
+                    env[o] = acc;
+                }
+                ea = s.ra;
+                eb = s.rb;
+            }
+            __syncthreads();
+        }
+        for (int k = threadIdx.x; k < K4; k += blockDim.x) out[(int64_t)k * ld + R] = k < ea * eb ? env[k] : 0.0;
+        __syncthreads();
+    }
+}
+
 // Pi[R, j] = sum_k EL[k, R] * ER[k, j] on v_mfma_f64_16x16x4_f64: a wave owns a 32 x 32 tile
 // (2 x 2 MFMA blocks), a workgroup 4 waves (64 x 64). Operand lanes: A[row l&15][k l>>4],
 // B[k l>>4][col l&15]; result: col = l & 15, row = (l >> 4) + 4 * reg (cdna_hip_programming.md).
@@ -767,10 +885,17 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
         const int64_t ldR = cp_ld(mR), ldC = cp_ld(n);
         double* EL = reinterpret_cast<double*>(scratch);
         double* ER = EL + (int64_t)K4 * ldR;
-        hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldR * K4, 4096)), dim3(256), 0, s, f, I, nl, m,
-                           D, M, K, K4, ldR, 0, false, EL);
-        hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldC * K4, 4096)), dim3(256), 0, s, f, J, nr, n,
-                           1, 0, K, K4, ldC, f.L - nr, true, ER);
+        if (f.kind == F_MPO) {  // environments: one workgroup per row / column
+            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(mR, 1), 8192)), dim3(256),
+                               0, s, f, I, nl, m, D, M, K4, ldR, 0, 0, EL);
+            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(n, 1), 8192)), dim3(256),
+                               0, s, f, J, nr, n, 1, 0, K4, ldC, f.L - nr, 1, ER);
+        } else {
+            hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldR * K4, 4096)), dim3(256), 0, s, f, I, nl,
+                               m, D, M, K, K4, ldR, 0, false, EL);
+            hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldC * K4, 4096)), dim3(256), 0, s, f, J, nr,
+                               n, 1, 0, K, K4, ldC, f.L - nr, true, ER);
+        }
         if (mR >= 128 && n >= 128 && K4 >= 32)
             hipLaunchKernelGGL(k_gemm_cp_lds, dim3((unsigned)(ldR / 128), (unsigned)(ldC / 128)), dim3(256),
                                0, s, EL, ldR, ER, ldC, K4, mR, n, out, ldo, maxbits);

@@ -84,6 +84,10 @@ struct SelArgs {
     int selk;
 };
 
+// MPO-MPO contraction integrand (TCI_F_MPO): LDS limits of the environment kernel, in doubles
+constexpr int kMpoEnv = 2048;  // ra * rb at every bond
+constexpr int kMpoTmp = 8192;  // rb * d2 * ra' and ra * d2 * rb' at every site
+
 // Device view of an integrand (tci_func).
 struct FuncDev {
     int32_t kind;
@@ -92,7 +96,7 @@ struct FuncDev {
     const double* params;      // device
     int64_t nparams;
     const int64_t* strides;    // device, column-major strides for TCI_F_TABLE
-    int32_t cpK;               // number of separable terms (TCI_F_GAUSSMIX, TCI_F_CP), host copy
+    int32_t cpK;               // separable terms (TCI_F_GAUSSMIX, TCI_F_CP; TCI_F_MPO: max ra*rb), host copy
     int64_t ntab;              // TCI_F_LORENTZ: quotient table size (max sum of squares + 1), or 0
 };
 

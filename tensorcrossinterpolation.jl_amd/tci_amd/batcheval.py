@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _lib
 
-F_SUM, F_LORENTZ, F_TABLE, F_GAUSS, F_GAUSSMIX, F_QOSC, F_QEXP, F_TT, F_CP = range(9)
+F_SUM, F_LORENTZ, F_TABLE, F_GAUSS, F_GAUSSMIX, F_QOSC, F_QEXP, F_TT, F_CP, F_MPO = range(10)
 
 
 def _as_index_table(sets, width):

@@ -1,0 +1,215 @@
+"""Tensor-train operator contraction -- host-side mirror of src/contraction.jl.
+
+`Contraction(A, B)` (contraction.jl:60-152) is a BatchEvaluator{Float64} of the fused-index
+function x -> (A * B)[x] for two 4-leg tensor trains (MPOs). Its batch evaluation runs on the GPU
+(integrand kind TCI_F_MPO): the left / right environments of the row and column index sets
+(evaluateleft / evaluateright, contraction.jl:279-354) are batched small contractions in
+`k_mpo_env`, and Pi = Lenv . Renv^T is an fp64 MFMA GEMM -- the "TT-core contractions as batched
+small GEMMs" of the north star. `contract(A, B; algorithm="TCI")` (contraction.jl:692-732, 832-860)
+then runs crossinterpolate2 over it exactly like the reference.
+
+Cores follow the reference's layout: a 4-leg core is (left bond, s1, s2, right bond), a 3-leg core
+(left bond, s, right bond), as numpy arrays (Fortran order is not required; the values are copied).
+Float64 only (the reference also accepts ComplexF64).
+"""
+import numpy as np
+
+from . import _lib
+from .batcheval import F_MPO, GPUBatchEvaluator
+from .tensorci2 import crossinterpolate2, optfirstpivot
+
+
+def sitedims(tt):
+    """sitedims of a tensor train given as a list of cores: the legs between the two bonds."""
+    return [list(c.shape[1:-1]) for c in tt]
+
+
+def _check_pair(A, B):
+    """Contraction's constructor checks (contraction.jl:129-138) and contract_TCI's (:699-708)."""
+    if len(A) != len(B):
+        raise ValueError("Tensor trains must have the same length.")
+    for n in range(len(A)):
+        if A[n].ndim != 4 or B[n].ndim != 4:
+            raise ValueError("Contraction takes two 4-leg tensor trains (MPOs)")
+        if A[n].shape[2] != B[n].shape[1]:
+            raise ValueError(f"Tensor trains must share the identical index at n={n + 1}!")
+
+
+def _mpo_params(A, B):
+    """TCI_F_MPO params: [N, per site (ra, d1, d2, ra', rb, d3, rb', offA, offB), cores]."""
+    N = len(A)
+    hdr = []
+    blobs = []
+    off = 0
+    for a, b in zip(A, B):
+        a = np.asarray(a, np.float64)
+        b = np.asarray(b, np.float64)
+        offA = off
+        blobs.append(a.ravel(order="F"))
+        off += a.size
+        offB = off
+        blobs.append(b.ravel(order="F"))
+        off += b.size
+        hdr += [a.shape[0], a.shape[1], a.shape[2], a.shape[3], b.shape[0], b.shape[2], b.shape[3], offA, offB]
+    return np.concatenate([np.asarray([N] + hdr, np.float64)] + blobs)
+
+
+class Contraction(GPUBatchEvaluator):
+    """Contraction{Float64}(A, B) (contraction.jl:60-152): callable on fused multi-indices
+    (x_n = s1 + d1 (s3 - 1), _fuse_idx :235-237) and batch-evaluable on the GPU. `f`, the
+    optional elementwise post-processing of the reference, is not supported on the device."""
+
+    def __init__(self, A, B, ctx=None, f=None):
+        if f is not None:
+            raise NotImplementedError("Contraction(...; f) is not supported by the device evaluator")
+        _check_pair(A, B)
+        self.mpo = ([np.asarray(a, np.float64) for a in A], [np.asarray(b, np.float64) for b in B])
+        self.sitedims = [[a.shape[1], b.shape[2]] for a, b in zip(*self.mpo)]
+        localdims = [d1 * d3 for d1, d3 in self.sitedims]
+        super().__init__(F_MPO, _mpo_params(*self.mpo), localdims, ctx=ctx, name="contraction")
+
+    def __len__(self):
+        return len(self.mpo[0])
+
+    def _unfuse_idx(self, n, idx):
+        """_unfuse_idx (contraction.jl:226-228): fused 1-based idx -> (s1, s3)."""
+        d1 = self.sitedims[n][0]
+        return ((idx - 1) % d1 + 1, (idx - 1) // d1 + 1)
+
+    def _fuse_idx(self, n, ij):
+        """_fuse_idx (contraction.jl:235-237)."""
+        return ij[0] + self.sitedims[n][0] * (ij[1] - 1)
+
+    def evaluate_unfused(self, indexset):
+        """evaluate(obj, Vector{Tuple{Int,Int}}) (contraction.jl:385-406)."""
+        return self([self._fuse_idx(n, ij) for n, ij in enumerate(indexset)])
+
+
+def _findinitialpivots(f, localdims, nmaxpivots, rng):
+    """_findinitialpivots (contraction.jl:666-677): random starts improved by optfirstpivot, kept
+    when f is nonzero there. The reference draws with Julia's default_rng; here numpy's (the
+    stream cannot be reproduced)."""
+    pivots = []
+    for _ in range(nmaxpivots):
+        p = [int(rng.integers(1, d + 1)) for d in localdims]
+        p = optfirstpivot(f, localdims, p)
+        if abs(f(p)) == 0.0:
+            continue
+        pivots.append(p)
+    return pivots
+
+
+def _reshape_splitsites(t, legdims):
+    """_reshape_splitsites (contraction.jl:654-659): (chi, prod(legdims), chi') -> (chi, legdims..., chi')."""
+    return np.reshape(t, (t.shape[0],) + tuple(legdims) + (t.shape[-1],), order="F")
+
+
+def contract_TCI(A, B, initialpivots=10, f=None, seed=None, ctx=None, **kwargs):
+    """contract_TCI (contraction.jl:692-732): crossinterpolate2 over Contraction(A, B); returns
+    the 4-leg cores of the result. kwargs go to crossinterpolate2 (tolerance, maxbonddim, ...)."""
+    if len(A) != len(B):
+        raise ValueError("Cannot contract tensor trains with different length.")
+    if not all(A[i].shape[2] == B[i].shape[1] for i in range(len(A))):
+        raise ValueError("Cannot contract tensor trains with non-matching site dimensions.")
+    matrixproduct = Contraction(A, B, ctx=ctx, f=f)
+    localdims = matrixproduct.localdims
+    if isinstance(initialpivots, int):
+        initialpivots = _findinitialpivots(matrixproduct, localdims, initialpivots, np.random.default_rng(seed))
+        if not initialpivots:
+            raise RuntimeError("No initial pivots found.")
+    tci, ranks, errors = crossinterpolate2(matrixproduct, localdims, initialpivots, **kwargs)
+    return [_reshape_splitsites(t, d) for t, d in zip(tci.sitetensors, matrixproduct.sitedims)]
+
+
+def _contractsitetensors(a, b):
+    """_contractsitetensors (contraction.jl:591-602): (la, s1, s2, ra) x (lb, s2, s3, rb) ->
+    (la lb, s1, s3, ra rb) with the left index of A fastest in the fused bonds."""
+    ab = np.einsum("aijb,cjkd->acikbd", a, b)  # permutedims(ab, (1, 4, 2, 5, 3, 6))
+    return np.reshape(ab, (a.shape[0] * b.shape[0], a.shape[1], b.shape[2], a.shape[3] * b.shape[3]),
+                      order="F")
+
+
+def contract_naive(A, B, tolerance=0.0, maxbonddim=None):
+    """contract_naive (contraction.jl:616-637) without recompression: site-by-site products
+    (host; the bond dimensions multiply). tolerance / maxbonddim (SVD recompression) are not
+    supported."""
+    if tolerance > 0 or maxbonddim is not None:
+        raise NotImplementedError("contract_naive: SVD recompression is not part of this path")
+    _check_pair(A, B)
+    return [_contractsitetensors(np.asarray(a, np.float64), np.asarray(b, np.float64)) for a, b in zip(A, B)]
+
+
+def _as_mpo_left(tt):
+    """TensorTrain{4}(A, [(1, s...)]) for a 3-leg A on the left of an MPO (contraction.jl:870-877)."""
+    return [np.reshape(np.asarray(c, np.float64), (c.shape[0], 1, c.shape[1], c.shape[2]), order="F") for c in tt]
+
+
+def _as_mpo_right(tt):
+    """TensorTrain{4}(B, [(s..., 1)]) for a 3-leg B on the right of an MPO (contraction.jl:884-891)."""
+    return [np.reshape(np.asarray(c, np.float64), (c.shape[0], c.shape[1], 1, c.shape[2]), order="F") for c in tt]
+
+
+def _to_tt3(tt4):
+    """TensorTrain{3}(tt, prod.(sitedims(tt))): fuse the two site legs (first fastest)."""
+    return [np.reshape(c, (c.shape[0], c.shape[1] * c.shape[2], c.shape[3]), order="F") for c in tt4]
+
+
+def contract(A, B, algorithm="TCI", tolerance=1e-12, maxbonddim=None, f=None, **kwargs):
+    """contract(A, B; algorithm, tolerance, maxbonddim, f, kwargs...) (contraction.jl:832-891).
+    A, B: lists of cores; 4-leg x 4-leg gives an MPO, a 3-leg operand (MPS) gives an MPS.
+    algorithm: "TCI" (device path) or "naive"; "zipup" (LU/SVD recompression) is not part of this
+    path."""
+    if A and np.asarray(A[0]).ndim == 3:
+        return _to_tt3(contract(_as_mpo_left(A), B, algorithm, tolerance, maxbonddim, f, **kwargs))
+    if B and np.asarray(B[0]).ndim == 3:
+        return _to_tt3(contract(A, _as_mpo_right(B), algorithm, tolerance, maxbonddim, f, **kwargs))
+    if algorithm == "TCI":
+        kw = dict(kwargs)
+        kw["tolerance"] = tolerance
+        if maxbonddim is not None:
+            kw["maxbonddim"] = maxbonddim
+        return contract_TCI(A, B, f=f, **kw)
+    if algorithm == "naive":
+        if f is not None:
+            raise RuntimeError("Naive contraction implementation cannot contract matrix product with a function. "
+                               "Use algorithm=:TCI instead.")
+        return contract_naive(A, B)
+    if algorithm == "zipup":
+        raise NotImplementedError("contract(...; algorithm=:zipup) is not part of the TCI2 device path")
+    raise ValueError(f"Unknown algorithm {algorithm}.")
+
+
+def evaluate_tt(tt, idx):
+    """evaluate(tt, idx) (abstracttensortrain.jl:328-342) for 3-leg cores (1-based idx)."""
+    v = np.ones((1, 1))
+    for c, i in zip(tt, idx):
+        v = v @ c[:, int(i) - 1, :]
+    return float(v[0, 0])
+
+
+def tomat(tt4):
+    """The matrix of an MPO (rows: first site legs, first site fastest; test_contraction.jl:5-16)."""
+    d1 = [c.shape[1] for c in tt4]
+    d2 = [c.shape[2] for c in tt4]
+    out = np.zeros((int(np.prod(d1)), int(np.prod(d2))))
+    for i, ii in enumerate(np.ndindex(*d1[::-1])):
+        ii = ii[::-1]
+        for j, jj in enumerate(np.ndindex(*d2[::-1])):
+            jj = jj[::-1]
+            v = np.ones((1, 1))
+            for c, a, b in zip(tt4, ii, jj):
+                v = v @ c[:, a, b, :]
+            out[i, j] = v[0, 0]
+    return out
+
+
+def tovec(tt3):
+    """The vector of an MPS (first site fastest; test_contraction.jl:18-22)."""
+    d = [c.shape[1] for c in tt3]
+    out = np.zeros(int(np.prod(d)))
+    for i, ii in enumerate(np.ndindex(*d[::-1])):
+        out[i] = evaluate_tt(tt3, [x + 1 for x in ii[::-1]])
+    return out
+
+
+_ = _lib  # the device library is loaded through GPUBatchEvaluator

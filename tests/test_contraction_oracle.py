@@ -1,0 +1,115 @@
+"""CPU tests of the contraction path's oracle and host logic (contraction.jl).
+
+Pinned by the reference's own properties (test/test_contraction.jl): the contraction of two MPOs
+evaluates to the product of their matrices (`_tomat(ab) ≈ _tomat(a) * _tomat(b)`, :94), also for
+an MPO times an MPS (:175-176), on the reference's test shapes (N = 4, bonds [1,2,3,2,1], local
+dims 2 x 3 x 2). The reference draws complex random cores; Float64 cores here.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+T = pytest.importorskip("tci_amd")
+from tci_amd.contraction import (_as_mpo_right, _contractsitetensors, _mpo_params, contract_naive, tomat,  # noqa: E402
+                                 tovec)
+
+F_MPO = 9
+
+
+def gen_tto_tto(seed=0, N=4, bonds=(1, 2, 3, 2, 1), d1=2, d2=3, d3=2):
+    rng = np.random.default_rng(seed)
+    A = [rng.random((bonds[n], d1, d2, bonds[n + 1])) for n in range(N)]
+    B = [rng.random((bonds[n], d2, d3, bonds[n + 1])) for n in range(N)]
+    return A, B
+
+
+def fused_index_value(ref, x, d1s, d3s):
+    """(A * B)[x] for fused indices x_n = s1 + d1 (s3 - 1) (contraction.jl:226-237)."""
+    i = j = 0
+    si = sj = 1
+    for n, xn in enumerate(x):
+        s1, s3 = (xn - 1) % d1s[n], (xn - 1) // d1s[n]
+        i += s1 * si
+        j += s3 * sj
+        si *= d1s[n]
+        sj *= d3s[n]
+    return ref[i, j]
+
+
+def test_oracle_mpo_matches_matrix_product():
+    A, B = gen_tto_tto()
+    ref = tomat(A) @ tomat(B)
+    p = _mpo_params(A, B)
+    ld = [4] * 4
+    err = 0.0
+    for x in itertools.product(*[range(1, 5)] * 4):
+        err = max(err, abs(O.feval(F_MPO, p, ld, list(x)) - fused_index_value(ref, x, [2] * 4, [2] * 4)))
+    assert err <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("N", [1, 2, 5])
+def test_oracle_mpo_lengths(N):
+    bonds = [1] + [3] * (N - 1) + [1]
+    A, B = gen_tto_tto(seed=N, N=N, bonds=bonds, d1=2, d2=2, d3=3)
+    ref = tomat(A) @ tomat(B)
+    p = _mpo_params(A, B)
+    for x in itertools.product(*[range(1, 7)] * N):
+        assert O.feval(F_MPO, p, [6] * N, list(x)) == pytest.approx(
+            fused_index_value(ref, x, [2] * N, [3] * N), rel=1e-12, abs=1e-13)
+
+
+def test_oracle_batcheval_mpo_split():
+    """_batchevaluate_dispatch over the contraction: every (row legs, column legs) split."""
+    A, B = gen_tto_tto(seed=3)
+    p = _mpo_params(A, B)
+    ld = [4] * 4
+    rng = np.random.default_rng(7)
+    for nl in range(0, 5):
+        I = rng.integers(1, 5, size=(5, nl))
+        J = rng.integers(1, 5, size=(3, 4 - nl))
+        out, _ = O.batcheval(F_MPO, p, ld, I, J, 0)
+        for a in range(5):
+            for b in range(3):
+                x = list(I[a]) + list(J[b])
+                assert out[a, 0, b] == O.feval(F_MPO, p, ld, x)
+
+
+def test_contract_naive_is_matrix_product():
+    A, B = gen_tto_tto(seed=1)
+    ab = contract_naive(A, B)
+    assert [list(c.shape[1:3]) for c in ab] == [[2, 2]] * 4  # sitedims (test_contraction.jl:92)
+    np.testing.assert_allclose(tomat(ab), tomat(A) @ tomat(B), rtol=1e-12)
+
+
+def test_contractsitetensors_layout():
+    """_contractsitetensors (contraction.jl:591-602): fused bonds with A's index fastest."""
+    rng = np.random.default_rng(2)
+    a = rng.random((2, 3, 4, 5))
+    b = rng.random((3, 4, 2, 2))
+    c = _contractsitetensors(a, b)
+    assert c.shape == (6, 3, 2, 10)
+    for la, lb, s1, s3, ra, rb in itertools.product(range(2), range(3), range(3), range(2), range(5), range(2)):
+        want = sum(a[la, s1, s2, ra] * b[lb, s2, s3, rb] for s2 in range(4))
+        assert c[la + 2 * lb, s1, s3, ra + 5 * rb] == pytest.approx(want, rel=1e-14)
+
+
+def test_mpo_mps_naive():
+    rng = np.random.default_rng(4)
+    bonds = [1, 2, 3, 2, 1]
+    A = [rng.random((bonds[n], 3, 3, bonds[n + 1])) for n in range(4)]
+    b = [rng.random((bonds[n], 3, bonds[n + 1])) for n in range(4)]
+    ab = contract_naive(A, _as_mpo_right(b))
+    v = tovec([np.reshape(c, (c.shape[0], c.shape[1] * c.shape[2], c.shape[3]), order="F") for c in ab])
+    np.testing.assert_allclose(v, tomat(A) @ tovec(b), rtol=1e-12)
+
+
+def test_contract_argument_errors():
+    A, B = gen_tto_tto()
+    with pytest.raises(ValueError):
+        contract_naive(A[:3], B)
+    bad = [np.zeros((1, 2, 4, 1))] + B[1:]
+    with pytest.raises(ValueError):
+        contract_naive(A, bad)

@@ -1,0 +1,127 @@
+"""GPU parity of the contraction evaluator (TCI_F_MPO: k_mpo_env environments + fp64 MFMA GEMM)
+and of contract(A, B; algorithm=:TCI) (contraction.jl:483-575, 692-732, 832-891).
+
+Bars: batch evaluation within 1e-12 relative of the oracle (summation order of the environments
+and of the GEMM differs from the per-point chain); TCI2 over the contraction: ranks equal to the
+oracle's and errors within 1e-10 relative (north star); contract(...; :TCI) reproduces the
+matrix product of the operands (the reference's own test, test_contraction.jl:94, 175) within
+1e-10 relative to its largest entry.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_contraction_oracle import F_MPO, fused_index_value, gen_tto_tto
+
+pytestmark = pytest.mark.gpu
+
+T = pytest.importorskip("tci_amd")
+from tci_amd.contraction import _mpo_params, tomat, tovec  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+def relerr(a, b):
+    return np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(b).max(), 1e-300)
+
+
+@pytest.mark.parametrize("M", [0, 1])
+def test_batcheval_vs_oracle_every_split(ctx, M):
+    A, B = gen_tto_tto(seed=11)
+    f = T.Contraction(A, B, ctx=ctx)
+    p = _mpo_params(A, B)
+    rng = np.random.default_rng(5)
+    for nl in range(0, 5 - M):
+        I = rng.integers(1, 5, size=(7, nl)).astype(np.int32)
+        J = rng.integers(1, 5, size=(6, 4 - nl - M)).astype(np.int32)
+        got, mx = f.pi(I, J, M)
+        ref, rmx = O.batcheval(F_MPO, p, [4] * 4, I, J, M)
+        ref = ref.reshape(got.shape, order="F")
+        assert relerr(got, ref) <= 1e-12
+        assert mx == pytest.approx(rmx, rel=1e-12)
+
+
+def test_points_are_the_matrix_product(ctx):
+    A, B = gen_tto_tto(seed=12)
+    f = T.Contraction(A, B, ctx=ctx)
+    ref = tomat(A) @ tomat(B)
+    X = np.array(list(itertools.product(*[range(1, 5)] * 4)), np.int32)
+    got = f.points(X)
+    want = np.array([fused_index_value(ref, x, [2] * 4, [2] * 4) for x in X])
+    assert relerr(got, want) <= 1e-12
+
+
+def test_larger_bonds_vs_oracle(ctx):
+    """bond dimension 24 (K = 576 environment terms, the LDS-tiled MFMA GEMM), 10 sites."""
+    N, chi = 10, 24
+    bonds = [1] + [chi] * (N - 1) + [1]
+    A, B = gen_tto_tto(seed=13, N=N, bonds=bonds, d1=2, d2=2, d3=2)
+    f = T.Contraction(A, B, ctx=ctx)
+    p = _mpo_params(A, B)
+    rng = np.random.default_rng(6)
+    I = rng.integers(1, 5, size=(200, 5)).astype(np.int32)
+    J = rng.integers(1, 5, size=(150, 5)).astype(np.int32)
+    got, _ = f.pi(I, J, 0)
+    ref, _ = O.batcheval(F_MPO, p, [4] * N, I, J, 0)
+    assert relerr(got, ref.reshape(got.shape, order="F")) <= 1e-12
+
+
+def test_tci2_over_contraction_vs_oracle(ctx):
+    A, B = gen_tto_tto(seed=14)
+    f = T.Contraction(A, B, ctx=ctx)
+    p = _mpo_params(A, B)
+    piv = [T.optfirstpivot(f, f.localdims, [1] * 4)]
+    kw = dict(tolerance=1e-12, maxiter=8)
+    tci, ranks, errors = T.crossinterpolate2(f, f.localdims, piv, nsearchglobalpivot=0, **kw)
+    rt, rranks, rerrors = O.crossinterpolate2(F_MPO, p, [4] * 4, piv, **kw)
+    assert ranks == rranks
+    np.testing.assert_allclose(errors, rerrors, rtol=1e-10, atol=1e-14)
+
+
+def test_contract_tci_is_matrix_product(ctx):
+    """test_contraction.jl:86-98 (f = nothing, algorithm = :TCI)."""
+    A, B = gen_tto_tto(seed=15)
+    ab = T.contract(A, B, algorithm="TCI", seed=0, ctx=ctx)
+    assert [list(c.shape[1:3]) for c in ab] == [[2, 2]] * 4
+    ref = tomat(A) @ tomat(B)
+    assert relerr(tomat(ab), ref) <= 1e-10
+
+
+def test_contract_mpo_mps(ctx):
+    """test_contraction.jl:148-182: MPO x MPS and MPS x MPO."""
+    rng = np.random.default_rng(16)
+    bonds = [1, 2, 3, 2, 1]
+    A = [rng.random((bonds[n], 3, 3, bonds[n + 1])) for n in range(4)]
+    b = [rng.random((bonds[n], 3, bonds[n + 1])) for n in range(4)]
+    ab = T.contract(A, b, seed=0, ctx=ctx)
+    ba = T.contract(b, A, seed=0, ctx=ctx)
+    assert [c.shape[1] for c in ab] == [3] * 4
+    assert relerr(tovec(ab), tomat(A) @ tovec(b)) <= 1e-10
+    assert relerr(tovec(ba), tovec(b) @ tomat(A)) <= 1e-10
+
+
+def test_contract_naive_matches_tci(ctx):
+    A, B = gen_tto_tto(seed=17)
+    assert relerr(tomat(T.contract(A, B, algorithm="TCI", seed=1, ctx=ctx)),
+                  tomat(T.contract(A, B, algorithm="naive"))) <= 1e-10
+
+
+def test_contraction_argument_errors(ctx):
+    A, B = gen_tto_tto()
+    with pytest.raises(ValueError):
+        T.Contraction(A[:3], B, ctx=ctx)
+    with pytest.raises(ValueError):
+        T.contract(A, B, algorithm="bogus", ctx=ctx)
+    with pytest.raises(RuntimeError):
+        T.contract(A, B, algorithm="naive", f=lambda x: 2 * x)
+    big = 64  # ra * rb = 4096 > the environment kernel's 2048
+    A2, B2 = gen_tto_tto(seed=2, N=3, bonds=[1, big, big, 1], d1=2, d2=2, d3=2)
+    with pytest.raises(T.TCIArgumentError):
+        T.Contraction(A2, B2, ctx=ctx)
