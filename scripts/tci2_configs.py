@@ -73,6 +73,35 @@ def configs():
         return run("C5 scaled: 12d CP-rank-256 synthetic d=32 tol=1e-10 maxbonddim=256", f, [d] * L,
                    [p0], tolerance=1e-10, maxbonddim=256, maxiter=3, nsearchglobalpivot=0)
     out["C5_cp12d_K256"] = cp12
+
+    def cp12_full():
+        # config 5 as stated: CP-rank-1024 synthetic, 12 legs of d = 32, ranks up to 1024 (Pi up to
+        # 32768^2 = 8 GiB, rrLU at r = 1024); no separate warm-up (the kernels are those of C5 scaled)
+        rng = np.random.default_rng(2)
+        K, L, d = 1024, 12, 32
+        f = T.cp_function(0.5 + rng.random((K, L, d)))
+        p0 = T.optfirstpivot(f, [d] * L)
+        t0 = time.perf_counter()
+        tci, ranks, errors = T.crossinterpolate2(f, [d] * L, [p0], tolerance=1e-10, maxbonddim=1024,
+                                                 maxiter=3, nsearchglobalpivot=0)
+        wall = time.perf_counter() - t0
+        return {"config": "C5: 12d CP-rank-1024 synthetic d=32 tol=1e-10 maxbonddim=1024 maxiter=3",
+                "wall_s": round(wall, 3), "iterations": len(ranks), "ranks": ranks,
+                "final_error": errors[-1], "linkdims": tci.linkdims()}
+    out["C5_cp12d_K1024"] = cp12_full
+
+    def mpo_contract():
+        # contract(A, B; algorithm=:TCI) of two random MPOs, 20 sites, bonds 16, d = 2 x 2 x 2
+        rng = np.random.default_rng(5)
+        N, chi = 20, 8
+        bonds = [1] + [chi] * (N - 1) + [1]
+        A = [rng.standard_normal((bonds[n], 2, 2, bonds[n + 1])) / 2 for n in range(N)]
+        B = [rng.standard_normal((bonds[n], 2, 2, bonds[n + 1])) / 2 for n in range(N)]
+        f = T.Contraction(A, B)
+        p0 = T.optfirstpivot(f, f.localdims)
+        return run("contract(A, B; :TCI) of two 20-site MPOs, bond 8, d=2x2x2, tol=1e-10", f,
+                   f.localdims, [p0], tolerance=1e-10, maxbonddim=128, nsearchglobalpivot=0)
+    out["contract_mpo20"] = mpo_contract
     return out
 
 

@@ -50,19 +50,19 @@ __global__ void k_trsm_cols_upper(double* __restrict__ U, int64_t ldu, int n, in
     }
 }
 
-// Blocked form of both triangular solves for np <= kTrsmMaxNp: a workgroup keeps kTrsmRhs
-// right-hand sides (rows of L21 / columns of U12) x np in LDS and walks 16-column blocks from the
+// Blocked form of both triangular solves for np <= kTrsmMaxNp: a workgroup keeps RHS
+// right-hand sides (rows of L21 / columns of U12) x np in LDS (RHS = 32 up to np = 512, then 16
+// and 8, so that RHS x np doubles stay within 128 KiB) and walks 16-column blocks from the
 // right: solve the block's unit-triangular diagonal part per right-hand side, then subtract the
 // block's contribution from every column to its left in parallel (right-looking). Same
 // recurrence X[., j] = B[., j] - sum_{t > j} X[., t] coef(t, j) as the one-thread-per-row
 // kernels, in block order.
 //   LOWER (leftorth): X(r, j) = L[r + j ld], coef(t, j) = L[t + j ld]
 //   upper (!leftorth): X(c, j) = U[j + c ld], coef(t, j) = U[j + t ld]
-constexpr int kTrsmRhs = 32;
 constexpr int kTrsmBlk = 16;
-constexpr int kTrsmMaxNp = 512;
+constexpr int kTrsmMaxNp = 2048;
 
-template <bool LOWER>
+template <bool LOWER, int kTrsmRhs>
 __global__ __launch_bounds__(256) void k_trsm_blocked(double* __restrict__ Mx, int64_t ld, int rhs0,
                                                       int rhs1, int np) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -118,11 +118,18 @@ static void launch_trsm(hipStream_t s, double* Mx, int64_t ld, int rhs0, int rhs
                                rhs1, np);
         return;
     }
-    const size_t bytes = (size_t)kTrsmRhs * np * sizeof(double);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm_blocked<LOWER>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    hipLaunchKernelGGL(k_trsm_blocked<LOWER>, dim3((rhs1 - rhs0 + kTrsmRhs - 1) / kTrsmRhs), dim3(256),
-                       bytes, s, Mx, ld, rhs0, rhs1, np);
+    auto go = [&](auto kern, int rhs) {
+        const size_t bytes = (size_t)rhs * np * sizeof(double);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bytes);
+        hipLaunchKernelGGL(kern, dim3((rhs1 - rhs0 + rhs - 1) / rhs), dim3(256), bytes, s, Mx, ld, rhs0, rhs1, np);
+    };
+    if (np <= 512)
+        go(k_trsm_blocked<LOWER, 32>, 32);
+    else if (np <= 1024)
+        go(k_trsm_blocked<LOWER, 16>, 16);
+    else
+        go(k_trsm_blocked<LOWER, 8>, 8);
 }
 
 // left (m x np, ld m) scatter for leftorth: out[rowperm[i], j] = i < np ? (i==j) : X[i,j]

@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     const int G = kStageCols / cb;
     const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;  // this thread's two rows
     static_assert(U <= 8 && 8 % U == 0, "U must divide every column-tile width");
-    const bool rowok = r0 < m, pair = r0 + 1 < m;
+    const bool rowok = r0 < m;
     double* const base = A + r0;
     auto chunk_col = [&](int g0, int h) -> int {  // first (physical) column of chunk h
         const int it = g0 + (h * U) / cb;
@@ -448,8 +448,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
         if (g0 == 0) PPROF(2);
         if (!active) continue;
         // one column (local index lc, physical j): apply the P pending updates in order, write
-        // back if FLUSH, fold the block's rows into the running candidate. Rows outside the block
-        // are updated too (their values are never read again), which saves the selects.
+        // back if FLUSH (trailing rows only), fold the block's rows into the running candidate.
         auto column = [&](double2 v, int lc, int j) {
             const int cp = cpos_s[lc];
             if (cp <= k) return;  // pivoted column or past the last one: not in the trailing block
@@ -459,10 +458,12 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
                 v.x = __dsub_rn(v.x, __dmul_rn(x0[s], y));
                 v.y = __dsub_rn(v.y, __dmul_rn(x1[s], y));
             }
-            if (FLUSH) {
+            if (FLUSH && (in0 || in1)) {  // trailing rows only (see pass2_body)
                 double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
-                if (!pair) {
-                    pa->x = v.x;  // odd m: row m is the caller's padding, left untouched
+                if (!in1) {
+                    pa->x = v.x;
+                } else if (!in0) {
+                    pa->y = v.y;
                 } else if (TCI_FLUSH_NT) {
                     typedef double dv2 __attribute__((ext_vector_type(2)));
                     dv2 w = {v.x, v.y};
@@ -703,10 +704,16 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                 v.x = __dsub_rn(v.x, __dmul_rn(x0[s], y));
                 v.y = __dsub_rn(v.y, __dmul_rn(x1[s], y));
             }
-            if (FLUSH && rowok) {
+            // write back trailing rows only: a row outside the block keeps its stale value, which
+            // matters for pivot k's own row -- other workgroups read its stale values while
+            // staging y_k, concurrently with this store (a second staging group can start after
+            // the owner of that row has stored the group's columns)
+            if (FLUSH && (in0 || in1)) {
                 double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
-                if (!pair) {
+                if (!in1) {
                     pa->x = v.x;
+                } else if (!in0) {
+                    pa->y = v.y;
                 } else if (TCI_FLUSH_NT) {
                     typedef double dv2 __attribute__((ext_vector_type(2)));
                     dv2 w = {v.x, v.y};

@@ -73,6 +73,16 @@ def test_rrlu_random_bitwise(ctx, m, n, maxrank, leftorth):
     assert_lu_bitwise(lu, O.OracleLU(A, maxrank=maxrank, leftorthogonal=leftorth))
 
 
+@pytest.mark.parametrize("m,n,maxrank", [(8300, 9000, 40), (9000, 8300, 40)])
+def test_rrlu_two_staging_groups_bitwise(ctx, m, n, maxrank):
+    # 17 row tiles and more than 32 column tiles per workgroup: the pass stages its columns' y's in
+    # two groups, and write-back passes race with the second group's staging unless rows outside
+    # the trailing block (pivot k's own row) keep their stale values (regression: C5-size Pi)
+    A = O.fill_uniform(m * n, seed=m + n).reshape((m, n), order="F")
+    lu = T.rrlu(A, maxrank=maxrank, ctx=ctx)
+    assert_lu_bitwise(lu, O.OracleLU(A, maxrank=maxrank))
+
+
 @pytest.mark.parametrize("m,n", [(128, 128), (64, 256), (1, 4000), (4000, 1), (129, 127), (2, 2048)])
 def test_rrlu_small_path_limits_bitwise(ctx, m, n):
     # around the single-workgroup limits (m*n <= 16384, m + n <= 4096)
@@ -132,6 +142,19 @@ def test_luci_factors(ctx, kats, leftorth):
             assert np.array_equal(luci.pivoterrors(), ref.pivoterrors)
             np.testing.assert_allclose(luci.left(), ref.left, rtol=1e-12, atol=1e-12 * np.abs(ref.left).max())
             np.testing.assert_allclose(luci.right(), ref.right, rtol=1e-12, atol=1e-12 * np.abs(ref.right).max())
+
+
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_luci_factors_large_rank(ctx, leftorth):
+    # np beyond 512: the blocked triangular solves with 16 (np <= 1024) and 8 right-hand sides
+    A = O.fill_uniform(1400 * 1200, 12).reshape((1400, 1200), order="F")
+    for maxrank in (700, 1100):
+        luci = T.MatrixLUCI(A, maxrank=maxrank, leftorthogonal=leftorth, ctx=ctx)
+        ref = O.OracleLU(A, maxrank=maxrank, leftorthogonal=leftorth)
+        assert np.array_equal(luci.rowindices() - 1, ref.rowindices())
+        assert np.array_equal(luci.colindices() - 1, ref.colindices())
+        np.testing.assert_allclose(luci.left(), ref.left, rtol=1e-12, atol=1e-12 * np.abs(ref.left).max())
+        np.testing.assert_allclose(luci.right(), ref.right, rtol=1e-12, atol=1e-12 * np.abs(ref.right).max())
 
 
 KINDS = [
