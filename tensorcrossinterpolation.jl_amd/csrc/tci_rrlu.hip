@@ -131,6 +131,20 @@ __device__ __forceinline__ void wave_reduce_cand(CandR& c) {
     c.pr = __builtin_amdgcn_readlane(c.pr, w);
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8). The passes map a logical
+// index to (row tile, column set) row tile fastest, so with the raw blockIdx an XCD would only
+// ever see the row tiles congruent to it mod 8 -- the same offsets in every column, i.e. the same
+// subset of memory channels and its own L2 slice pattern (measured: even XCDs ended their
+// streaming 2-4 us after odd ones). Giving every XCD a contiguous range of logical indices spreads
+// all row tiles over every XCD.
+#ifndef TCI_XCD_SPREAD
+#define TCI_XCD_SPREAD 1
+#endif
+__device__ __forceinline__ int xcd_spread(int b, int G) {
+    if (!TCI_XCD_SPREAD || (G & 7)) return b;
+    return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 __device__ __forceinline__ CandR cand_none() { return CandR{-1.0, 0.0, kBig, kBig, 0, 0}; }
 
 // Block reduction; wave 0 ends with the winner.
@@ -329,8 +343,9 @@ __global__ __launch_bounds__(kUpdThreads) void k_pass(
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
     const int nq = gridDim.x / tiles_r;  // chunks per row tile (host: gridDim.x = tiles_r * nq)
-    const int tr = blockIdx.x % tiles_r;
-    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int tr = wid % tiles_r;
+    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
     // column tiles q, q + nq, q + 2 nq, ...: at any moment the grid streams one contiguous band
     // of nq column tiles (spread over every HBM channel), band after band
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
@@ -577,8 +592,9 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
     const int nq = gridDim.x / tiles_r;
-    const int tr = blockIdx.x % tiles_r;
-    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int tr = wid % tiles_r;
+    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
     const int G = kP2StageCols / cb;
     const int r0 = tr * kRowsPerTile + slice * 128 + 2 * lane;
@@ -807,8 +823,9 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
     const int nq = gridDim.x / tiles_r;
-    const int tr = blockIdx.x % tiles_r;
-    const int q = rev ? nq - 1 - blockIdx.x / tiles_r : blockIdx.x / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int tr = wid % tiles_r;
+    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
     const int G = kP2StageCols / cb;
     // four rows per lane: 16-B fp32 loads (lda, ldx and lds are multiples of 4, r0 too, so the
