@@ -73,7 +73,7 @@ def main():
                     help="diagnostic: no HIP events in the timed region (no roofline line)")
     ap.add_argument("--timing-stride", type=int, default=5,
                     help="time the rrLU pass of every s-th pivot with HIP events")
-    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "12")),
+    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "11")),
                     help="deferred-update depth of the rrLU (results are identical for every nb)")
     ap.add_argument("--no-shadow", action="store_true",
                     help="exact fp64 read-only passes instead of the certified fp32 shadow search")

@@ -37,7 +37,7 @@ struct tci_ctx {
     size_t capX = 0;
     double* ybuf = nullptr;
     size_t capY = 0;
-    int flush_every = 12;  // deferred-update depth nb (1 = write back every pivot; 12 measured best with the shadow search)
+    int flush_every = 11;  // deferred-update depth nb (1 = write back every pivot; 10-12 measured equal with the shadow search)
     int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int pass_percu = 1;    // one workgroup per CU, dynamic chunks (env TCI_PASS_PERCU=0: k_pass)

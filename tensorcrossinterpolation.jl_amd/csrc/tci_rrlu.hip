@@ -40,7 +40,7 @@
 #define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (4 rows x 16-B fp32 loads per column)
 #endif
 #ifndef TCI_FLUSH_NT
-#define TCI_FLUSH_NT 0  // write-back pass stores non-temporal
+#define TCI_FLUSH_NT 1  // write-back pass: fp64 stores non-temporal (the next pass reads the shadow, not them)
 #endif
 
 namespace tci {
