@@ -38,9 +38,7 @@ struct tci_ctx {
     double* ybuf = nullptr;
     size_t capY = 0;
     int flush_every = 11;  // deferred-update depth nb (1 = write back every pivot; 10-12 measured equal with the shadow search)
-    int pass_grid = 1024;  // workgroups of an rrLU pass (env TCI_PASS_GRID): 4 per CU, all resident
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
-    int pass_percu = 1;    // one workgroup per CU, dynamic chunks (env TCI_PASS_PERCU=0: k_pass)
     int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
     float* sbuf = nullptr; // its fp32 shadow of the matrix
     size_t capS = 0;
@@ -363,9 +361,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     g.abstol = abstol;
     g.ticket = c->ticket;
     g.selk = 0;
-    const bool percu = c->pass_percu && c->ncu > 0;
     // fp32 shadow for the certified search (4-row lanes need lda, lds multiples of 4)
-    const bool shadow = percu && c->shadow && lda % 4 == 0;
+    const bool shadow = c->shadow && lda % 4 == 0;
     g.S = nullptr;
     g.lds = 0;
     if (shadow) {
@@ -374,8 +371,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         g.S = c->sbuf;
     }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
-                                      percu ? std::min(c->ncu, kMaxGrid) : std::min(c->pass_grid, kMaxGrid));
-    tci::launch_pass(c->stream, 0, false, percu, shadow, g, grid);  // argmax of A, selects pivot 0
+                                      std::min(std::max(c->ncu, 1), kMaxGrid));
+    tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
     while (k < mr && !stopped) {
@@ -391,7 +388,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
             ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
-            tci::launch_pass(c->stream, P, flush, percu, shadow, g, grid);
+            tci::launch_pass(c->stream, P, flush, shadow, g, grid);
             ev_end(c, sampled);
             if (flush) t0 = kk + 1;
         }
@@ -534,9 +531,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     tci_ctx* c = new tci_ctx();
     c->device = device;
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
-    if (const char* e = getenv("TCI_PASS_GRID")) c->pass_grid = std::max(64, std::min(atoi(e), 2048));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
-    if (const char* e = getenv("TCI_PASS_PERCU")) c->pass_percu = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;

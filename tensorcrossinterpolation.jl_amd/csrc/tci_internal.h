@@ -7,10 +7,8 @@
 namespace tci {
 
 constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at most
-constexpr int kUpdThreads = 256;   // rrLU pass: 4 waves
 constexpr int kRowsPerTile = 512;  // 256 lanes x double2
 constexpr int kMaxCB = 16;         // rrLU pass: at most this many columns per tile (measured best)
-constexpr int kStageCols = 256;    // rrLU pass: columns whose y's a workgroup stages at once
 constexpr int kMaxPassGrid = 2048; // rrLU pass: at most this many workgroups (8 per CU)
 
 // Argmax candidate: abs2 value, the (current, pending-updated) value itself, its column and row
@@ -104,12 +102,10 @@ struct FuncDev {
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
-// percu: one 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2);
-// otherwise 256-thread workgroups with static shares (k_pass)
-// shadow (percu only): the initial and write-back passes also store the fp32 shadow g.S, and
+// One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).
+// shadow: the initial and write-back passes also store the fp32 shadow g.S, and
 // the read-only passes run the certified fp32 search (k_pass_sh; same results, ~half the bytes)
-void launch_pass(hipStream_t s, int P, bool flush, bool percu, bool shadow, const PassArgs& g,
-                 int grid);
+void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:

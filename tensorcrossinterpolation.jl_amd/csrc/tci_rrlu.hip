@@ -30,9 +30,6 @@
 
 #include "tci_internal.h"
 
-#ifndef TCI_PASS_U
-#define TCI_PASS_U 4  // columns per lane whose 16-B loads are in flight together (measured)
-#endif
 #ifndef TCI_PASS2_U
 #define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
 #endif
@@ -322,195 +319,6 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
         }
 #endif
     }
-}
-
-template <int P, bool FLUSH>
-__global__ __launch_bounds__(kUpdThreads) void k_pass(
-    double* __restrict__ A, int64_t lda, int m, int n, int k, double* __restrict__ X, int64_t ldx,
-    double* __restrict__ Y, int64_t ldy, double* __restrict__ Lp, int64_t ldl,
-    double* __restrict__ Up, int64_t ldu, int leftorth, Cand* __restrict__ cand, int cb, int rev,
-    SelArgs sel) {
-    RrluState* st = sel.st;
-    const int32_t* rowpos = sel.rowpos;
-    const int32_t* colpos = sel.colpos;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
-    PPROF(0);
-    constexpr int U = TCI_PASS_U;  // columns whose loads are in flight together
-    constexpr int PP = P > 0 ? P : 1;
-    // y_s of up to kStageCols of the workgroup's columns, [local column][slot]; slot P-1 = y_k
-    __shared__ double ys[kStageCols * PP];
-    __shared__ int cpos_s[kStageCols];
-    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
-    const int tiles_c = (n + cb - 1) / cb;
-    const int nq = gridDim.x / tiles_r;  // chunks per row tile (host: gridDim.x = tiles_r * nq)
-    const int wid = xcd_spread(blockIdx.x, gridDim.x);
-    const int tr = wid % tiles_r;
-    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
-    // column tiles q, q + nq, q + 2 nq, ...: at any moment the grid streams one contiguous band
-    // of nq column tiles (spread over every HBM channel), band after band
-    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
-    // The workgroup's columns stream in chunks of U (U divides cb: a chunk never straddles a
-    // tile), chunk h of a staging group covering local columns h*U .. h*U+U-1. Two chunks are in
-    // flight per lane (double-buffered registers). The stale values depend on nothing the pass
-    // derives, so the first two chunks are requested before the start-up chain (pivot, maps,
-    // pending vectors) and arrive while it runs.
-    const int G = kStageCols / cb;
-    const int r0 = tr * kRowsPerTile + 2 * threadIdx.x;  // this thread's two rows
-    static_assert(U <= 8 && 8 % U == 0, "U must divide every column-tile width");
-    const bool rowok = r0 < m;
-    double* const base = A + r0;
-    auto chunk_col = [&](int g0, int h) -> int {  // first (physical) column of chunk h
-        const int it = g0 + (h * U) / cb;
-        return (q + (rev ? ntc - 1 - it : it) * nq) * cb + (h * U) % cb;
-    };
-    auto load_chunk = [&](int g0, int h, double2 (&v)[U]) {
-        const int j = chunk_col(g0, h);
-#pragma unroll
-        for (int u = 0; u < U; ++u)  // past the last column: any valid address (never used)
-            v[u] = *reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
-    };
-    double2 va[U], vb[U];
-    if (rowok && ntc > 0) {
-        const int nch0 = min(G, ntc) * cb / U;
-        load_chunk(0, 0, va);
-        if (nch0 > 1) load_chunk(0, 1, vb);
-    }
-    if (st->done) return;
-    int a = 0, b = 0;
-    double piv = 1.0;
-    if (P > 0) {
-        a = (int)st->p;  // physical row / column of pivot k
-        b = (int)st->q;
-        piv = st->pval;
-    }
-    // this thread's rows' positions, pending x's and x_k
-    const int rp0 = rowok ? rowpos[r0] : -1;
-    const int rp1 = r0 + 1 < m ? rowpos[r0 + 1] : -1;
-    const bool in0 = rp0 > k, in1 = rp1 > k;
-    const bool active = in0 || in1;
-    double x0[PP], x1[PP];
-    if constexpr (P > 0) if (active) {
-        // x's of rows r0, r0 + 1 (ldx >= m + 1, so r0 + 1 is in bounds even past the last row)
-#pragma unroll
-        for (int s = 0; s < P - 1; ++s) {
-            const double2 u = *reinterpret_cast<const double2*>(X + (int64_t)s * ldx + r0);
-            x0[s] = u.x;
-            x1[s] = u.y;
-        }
-        const double2 cb2 = *reinterpret_cast<const double2*>(A + r0 + (int64_t)b * lda);
-        double xk0 = cb2.x, xk1 = cb2.y;
-#pragma unroll
-        for (int s = 0; s < P - 1; ++s) {
-            const double yv = Y[(int64_t)s * ldy + b];
-            xk0 = __dsub_rn(xk0, __dmul_rn(x0[s], yv));
-            xk1 = __dsub_rn(xk1, __dmul_rn(x1[s], yv));
-        }
-        if (leftorth) {
-            xk0 = xk0 / piv;
-            xk1 = xk1 / piv;
-        }
-        x0[P - 1] = xk0;
-        x1[P - 1] = xk1;
-        if (q == 0) {
-            double* xs = X + (int64_t)(P - 1) * ldx;
-            if (in0) {
-                xs[r0] = xk0;
-                Lp[r0 + (int64_t)k * ldl] = xk0;
-            }
-            if (in1) {
-                xs[r0 + 1] = xk1;
-                Lp[r0 + 1 + (int64_t)k * ldl] = xk1;
-            }
-        }
-    }
-    PPROF(1);
-    CandR best = cand_none();
-    // staging groups: the y's of G column tiles are staged at once (one barrier pair per group,
-    // usually one group per pass), then the group's tiles stream without barriers
-    for (int g0 = 0; g0 < ntc; g0 += G) {
-        const int gn = min(G, ntc - g0);
-        const int nch = gn * cb / U;
-        if (g0 > 0 && active) {
-            load_chunk(g0, 0, va);
-            if (nch > 1) load_chunk(g0, 1, vb);
-        }
-        __syncthreads();  // previous group's readers are done with ys / cpos_s
-        for (int lc = threadIdx.x; lc < gn * cb; lc += kUpdThreads) {
-            const int it = g0 + lc / cb;
-            const int j = (q + (rev ? ntc - 1 - it : it) * nq) * cb + lc % cb;
-            if (j >= n) {
-                cpos_s[lc] = -1;  // past the last column: skipped like a pivoted one
-                continue;
-            }
-            const int cp = colpos[j];
-            cpos_s[lc] = cp;
-            if (P > 0 && cp > k) {
-                double yk = A[a + (int64_t)j * lda];
-                for (int s = 0; s < P - 1; ++s) {
-                    const double ysv = Y[(int64_t)s * ldy + j];
-                    ys[lc * PP + s] = ysv;
-                    yk = __dsub_rn(yk, __dmul_rn(X[(int64_t)s * ldx + a], ysv));
-                }
-                if (!leftorth) yk = yk / piv;
-                ys[lc * PP + P - 1] = yk;
-                if (tr == 0) {
-                    Y[(int64_t)(P - 1) * ldy + j] = yk;
-                    Up[k + (int64_t)j * ldu] = yk;
-                }
-            }
-        }
-        __syncthreads();
-        if (g0 == 0) PPROF(2);
-        if (!active) continue;
-        // one column (local index lc, physical j): apply the P pending updates in order, write
-        // back if FLUSH (trailing rows only), fold the block's rows into the running candidate.
-        auto column = [&](double2 v, int lc, int j) {
-            const int cp = cpos_s[lc];
-            if (cp <= k) return;  // pivoted column or past the last one: not in the trailing block
-#pragma unroll
-            for (int s = 0; s < P; ++s) {
-                const double y = ys[lc * PP + s];
-                v.x = __dsub_rn(v.x, __dmul_rn(x0[s], y));
-                v.y = __dsub_rn(v.y, __dmul_rn(x1[s], y));
-            }
-            if (FLUSH && (in0 || in1)) {  // trailing rows only (see pass2_body)
-                double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
-                if (!in1) {
-                    pa->x = v.x;
-                } else if (!in0) {
-                    pa->y = v.y;
-                } else if (TCI_FLUSH_NT) {
-                    typedef double dv2 __attribute__((ext_vector_type(2)));
-                    dv2 w = {v.x, v.y};
-                    __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
-                } else {
-                    *pa = v;
-                }
-            }
-            // the full (value, column, row) comparison only matters when v >= best.v, which is
-            // rare once a large value has been seen: test that first (NaN fails it, as it should)
-            const double a0 = __dmul_rn(v.x, v.x), a1 = __dmul_rn(v.y, v.y);
-            if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
-                if (in0) cand_take(best, CandR{a0, v.x, cp, rp0, j, r0});
-                if (in1) cand_take(best, CandR{a1, v.y, cp, rp1, j, r0 + 1});
-            }
-        };
-        auto process = [&](int h, const double2 (&v)[U]) {
-            const int j = chunk_col(g0, h);
-#pragma unroll
-            for (int u = 0; u < U; ++u) column(v[u], h * U + u, j + u);
-        };
-        for (int h = 0; h < nch; h += 2) {
-            process(h, va);
-            if (h + 2 < nch) load_chunk(g0, h + 2, va);
-            if (h + 1 < nch) {
-                process(h + 1, vb);
-                if (h + 3 < nch) load_chunk(g0, h + 3, vb);
-            }
-        }
-    }
-    PPROF(3);
-    pass_tail<kUpdThreads>(best, sel, cand, pt, m, P, (int)FLUSH);
 }
 
 // ------------------------------------------------------------------ pass, one workgroup per CU
@@ -1131,40 +939,27 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 }
 
 template <int P>
-static void launch_pass_p(hipStream_t s, bool flush, bool percu, bool shadow, const PassArgs& g,
-                          int grid) {
+static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs& g, int grid) {
     const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals,
                       g.st,     g.ticket, g.reltol,  g.abstol,  g.selk};
-    if (percu) {
-        const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
-                      g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
-        if (shadow) {
-            if (flush || P == 0)
-                hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-            else if constexpr (P > 0)
-                hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-        } else if (flush) {
-            hipLaunchKernelGGL((k_pass2<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-        } else {
-            hipLaunchKernelGGL((k_pass2<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-        }
-        return;
+    const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
+                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
+    if (shadow) {
+        if (flush || P == 0)
+            hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        else if constexpr (P > 0)
+            hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+    } else if (flush) {
+        hipLaunchKernelGGL((k_pass2<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+    } else {
+        hipLaunchKernelGGL((k_pass2<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
     }
-#define TCI_PASS_LAUNCH(KERN, NT)                                                                  \
-    hipLaunchKernelGGL(KERN, dim3(grid), dim3(NT), 0, s, g.A, g.lda, g.m, g.n, g.k, g.X, g.ldx, g.Y, \
-                       g.ldy, g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb, g.rev, sel)
-    if (flush)
-        TCI_PASS_LAUNCH((k_pass<P, true>), kUpdThreads);
-    else
-        TCI_PASS_LAUNCH((k_pass<P, false>), kUpdThreads);
-#undef TCI_PASS_LAUNCH
 }
 
-void launch_pass(hipStream_t s, int P, bool flush, bool percu, bool shadow, const PassArgs& g,
-                 int grid) {
+void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid) {
     switch (P) {
 #define TCI_PASS_CASE(p) \
-    case p: launch_pass_p<p>(s, flush, percu, shadow, g, grid); break;
+    case p: launch_pass_p<p>(s, flush, shadow, g, grid); break;
         TCI_PASS_CASE(0) TCI_PASS_CASE(1) TCI_PASS_CASE(2) TCI_PASS_CASE(3) TCI_PASS_CASE(4)
         TCI_PASS_CASE(5) TCI_PASS_CASE(6) TCI_PASS_CASE(7) TCI_PASS_CASE(8) TCI_PASS_CASE(9)
         TCI_PASS_CASE(10) TCI_PASS_CASE(11) TCI_PASS_CASE(12) TCI_PASS_CASE(13) TCI_PASS_CASE(14)
