@@ -24,6 +24,18 @@ def configs():
     gm = np.concatenate([[8, 0.05], centres.ravel(), np.ones(8)]).tolist()
     g = 0.5 + np.random.default_rng(2).random((16, 6, 8))
     cp = np.concatenate([[16, 8], g.ravel()]).tolist()
+    # Contraction(A, B) of two 5-site MPOs (contraction.jl:60; TCI_F_MPO params, see
+    # tci_amd.contraction._mpo_params): bonds [1,3,4,4,3,1], d1 = d2 = d3 = 2
+    mrng = np.random.default_rng(4)
+    bonds = [1, 3, 4, 4, 3, 1]
+    A = [mrng.standard_normal((bonds[n], 2, 2, bonds[n + 1])) for n in range(5)]
+    B = [mrng.standard_normal((bonds[n], 2, 2, bonds[n + 1])) for n in range(5)]
+    hdr, blob, off = [5], [], 0
+    for a, b in zip(A, B):
+        hdr += [a.shape[0], 2, 2, a.shape[3], b.shape[0], 2, b.shape[3], off, off + a.size]
+        blob += a.ravel(order="F").tolist() + b.ravel(order="F").tolist()
+        off += a.size + b.size
+    mpo = [float(x) for x in hdr] + blob
     return [
         {"name": "C1_lorentz8d", "kind": 1, "params": [1.0], "localdims": [10] * 8, "initialpivots": None,
          "kw": {"tolerance": 1e-8}},
@@ -35,6 +47,8 @@ def configs():
          "initialpivots": [[1] + [2] * 39], "kw": {"tolerance": 1e-8}},
         {"name": "C5_cp6d_K16", "kind": 8, "params": cp, "localdims": [8] * 6, "initialpivots": [[1] * 6],
          "kw": {"tolerance": 1e-10}},
+        {"name": "contract_mpo5", "kind": 9, "params": mpo, "localdims": [4] * 5, "initialpivots": [[1] * 5],
+         "kw": {"tolerance": 1e-12}},
     ]
 
 
