@@ -16,6 +16,9 @@ import numpy as np
 
 from . import _lib
 from .batcheval import F_MPO, GPUBatchEvaluator
+from .matrixlu import left as lu_left
+from .matrixlu import npivots, right as lu_right, rrlu
+from .matrixluci import MatrixLUCI
 from .tensorci2 import crossinterpolate2, optfirstpivot
 
 
@@ -139,6 +142,53 @@ def contract_naive(A, B, tolerance=0.0, maxbonddim=None):
     return [_contractsitetensors(np.asarray(a, np.float64), np.asarray(b, np.float64)) for a, b in zip(A, B)]
 
 
+def _factorize(A, method, tolerance, maxbonddim, leftorthogonal=False, normalizeerror=True, ctx=None):
+    """_factorize (tensortrain.jl:219-271): :LU (rrlu on the device), :CI (MatrixLUCI on the
+    device) or :SVD (host LAPACK via numpy, truncated by the reference's rule)."""
+    reltol, abstol = (tolerance, 0.0) if normalizeerror else (1e-14, tolerance)
+    maxbonddim = int(min(maxbonddim, 2 ** 62))
+    if method == "LU":
+        lu = rrlu(A, maxrank=maxbonddim, reltol=reltol, abstol=abstol, leftorthogonal=leftorthogonal, ctx=ctx)
+        return lu_left(lu), lu_right(lu), npivots(lu)
+    if method == "CI":
+        ci = MatrixLUCI(A, maxrank=maxbonddim, reltol=reltol, abstol=abstol, leftorthogonal=leftorthogonal, ctx=ctx)
+        return ci.left(), ci.right(), ci.npivots()
+    if method == "SVD":
+        U, S, Vt = np.linalg.svd(A, full_matrices=False)
+        s2 = S ** 2
+        err = np.array([s2[n + 1:].sum() for n in range(len(S))])
+        nerr = err / s2.sum() if s2.sum() > 0 else err
+        first = lambda mask: int(np.argmax(mask)) + 1 if mask.any() else len(err)  # noqa: E731
+        trunci = min(first(err < abstol ** 2), first(nerr < reltol ** 2), maxbonddim)
+        if leftorthogonal:
+            return U[:, :trunci], S[:trunci, None] * Vt[:trunci, :], trunci
+        return U[:, :trunci] * S[None, :trunci], Vt[:trunci, :], trunci
+    raise RuntimeError("Not implemented yet.")
+
+
+def contract_zipup(A, B, tolerance=1e-12, method="SVD", maxbonddim=None, ctx=None):
+    """contract_zipup (contraction.jl:751-788): contract site by site from the left and factorize
+    the running tensor at every bond (:LU / :CI on the device, :SVD on the host)."""
+    if len(A) != len(B):
+        raise ValueError("Cannot contract tensor trains with different length.")
+    maxbonddim = 2 ** 62 if maxbonddim is None else maxbonddim
+    R = np.ones((1, 1, 1))
+    out = []
+    for n in range(len(A)):
+        a = np.asarray(A[n], np.float64)
+        b = np.asarray(B[n], np.float64)
+        RA = np.einsum("xyz,yijk->xzijk", R, a)          # _contract(R, A[n], (2,), (1,))
+        C = np.einsum("xzijk,zjlm->xilkm", RA, b)       # _contract(RA, B[n], (2,4), (1,2)), permuted
+        if n == len(A) - 1:
+            out.append(np.reshape(C, C.shape[:3] + (1,), order="F"))
+            break
+        Cm = np.reshape(C, (int(np.prod(C.shape[:3])), int(np.prod(C.shape[3:]))), order="F")
+        left, right, nb = _factorize(np.asfortranarray(Cm), method, tolerance, maxbonddim, ctx=ctx)
+        out.append(np.reshape(left, C.shape[:3] + (nb,), order="F"))
+        R = np.reshape(right, (nb,) + C.shape[3:], order="F")
+    return out
+
+
 def _as_mpo_left(tt):
     """TensorTrain{4}(A, [(1, s...)]) for a 3-leg A on the left of an MPO (contraction.jl:870-877)."""
     return [np.reshape(np.asarray(c, np.float64), (c.shape[0], 1, c.shape[1], c.shape[2]), order="F") for c in tt]
@@ -157,8 +207,8 @@ def _to_tt3(tt4):
 def contract(A, B, algorithm="TCI", tolerance=1e-12, maxbonddim=None, f=None, **kwargs):
     """contract(A, B; algorithm, tolerance, maxbonddim, f, kwargs...) (contraction.jl:832-891).
     A, B: lists of cores; 4-leg x 4-leg gives an MPO, a 3-leg operand (MPS) gives an MPS.
-    algorithm: "TCI" (device path) or "naive"; "zipup" (LU/SVD recompression) is not part of this
-    path."""
+    algorithm: "TCI" (device path), "naive" (host site products) or "zipup" (method="SVD" on the
+    host, "LU" / "CI" with the device rrLU)."""
     if A and np.asarray(A[0]).ndim == 3:
         return _to_tt3(contract(_as_mpo_left(A), B, algorithm, tolerance, maxbonddim, f, **kwargs))
     if B and np.asarray(B[0]).ndim == 3:
@@ -175,7 +225,10 @@ def contract(A, B, algorithm="TCI", tolerance=1e-12, maxbonddim=None, f=None, **
                                "Use algorithm=:TCI instead.")
         return contract_naive(A, B)
     if algorithm == "zipup":
-        raise NotImplementedError("contract(...; algorithm=:zipup) is not part of the TCI2 device path")
+        if f is not None:
+            raise RuntimeError("Zipup contraction implementation cannot contract matrix product with a function. "
+                               "Use algorithm=:TCI instead.")
+        return contract_zipup(A, B, tolerance=tolerance, maxbonddim=maxbonddim, **kwargs)
     raise ValueError(f"Unknown algorithm {algorithm}.")
 
 

@@ -113,3 +113,11 @@ def test_contract_argument_errors():
     bad = [np.zeros((1, 2, 4, 1))] + B[1:]
     with pytest.raises(ValueError):
         contract_naive(A, bad)
+
+
+def test_contract_zipup_svd_is_matrix_product():
+    """test_contraction.jl:185-189 (method = :SVD; host LAPACK, no device call)."""
+    from tci_amd.contraction import contract_zipup
+    A, B = gen_tto_tto(seed=5)
+    ab = contract_zipup(A, B, method="SVD")
+    np.testing.assert_allclose(tomat(ab), tomat(A) @ tomat(B), rtol=1e-10, atol=1e-12)

@@ -125,3 +125,17 @@ def test_contraction_argument_errors(ctx):
     A2, B2 = gen_tto_tto(seed=2, N=3, bonds=[1, big, big, 1], d1=2, d2=2, d3=2)
     with pytest.raises(T.TCIArgumentError):
         T.Contraction(A2, B2, ctx=ctx)
+
+
+@pytest.mark.parametrize("method", ["LU", "CI"])
+def test_contract_zipup_device_factorizations(ctx, method):
+    """test_contraction.jl:185-195: zip-up with the rrLU / MatrixLUCI factorizations (device)."""
+    A, B = gen_tto_tto(seed=18)
+    ab = T.contract(A, B, algorithm="zipup", method=method, ctx=ctx)
+    assert relerr(tomat(ab), tomat(A) @ tomat(B)) <= 1e-10
+    rng = np.random.default_rng(19)
+    bonds = [1, 2, 3, 2, 1]
+    A3 = [rng.random((bonds[n], 3, 3, bonds[n + 1])) for n in range(4)]
+    b = [rng.random((bonds[n], 3, bonds[n + 1])) for n in range(4)]
+    ab3 = T.contract(A3, b, algorithm="zipup", method=method, ctx=ctx)
+    assert relerr(tovec(ab3), tomat(A3) @ tovec(b)) <= 1e-10
