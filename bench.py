@@ -354,6 +354,34 @@ def extras(T, ctx):
     res["pi_cp_gemm"] = {"m": m, "n": n, "K": K, "L": L, "ms_device": round(kms / kn, 3), "TFLOPs": round(tfl, 2),
                          "mfma_f64_peak_measured_TFLOPs": round(peak.value, 2),
                          "frac_of_measured_peak": round(tfl / peak.value, 3)}
+    # Contraction of two MPOs (contraction.jl, TCI_F_MPO): 20 sites, bonds 32 (K = 1024 environment
+    # terms at the cut), d = 2 x 2 x 2; Pi 8192 x 8192 from 10 row legs and 10 column legs:
+    # environments (k_mpo_env) + the MFMA GEMM
+    N, chi = 20, 32
+    bonds = [1] + [chi] * (N - 1) + [1]
+    mrng = np.random.default_rng(5)
+    Am = [mrng.standard_normal((bonds[t], 2, 2, bonds[t + 1])) / chi ** 0.5 for t in range(N)]
+    Bm = [mrng.standard_normal((bonds[t], 2, 2, bonds[t + 1])) / chi ** 0.5 for t in range(N)]
+    fm = T.Contraction(Am, Bm, ctx=ctx)
+    Im = rng.integers(1, 5, (m, 10)).astype(np.int32)
+    Jm = rng.integers(1, 5, (n, 10)).astype(np.int32)
+    dm = T.DeviceMatrix(m, n, ctx=ctx)
+    for _ in range(2):
+        ctx.check(ctx.lib.tci_batcheval_d(ctx.h, fm.h, T._lib.ptr(Im), m, 10, T._lib.ptr(Jm), n, 10, 0, dm.ptr,
+                                          dm.ld, C.byref(mx)))
+    ctx.set_timing(True)
+    for _ in range(3):
+        ctx.check(ctx.lib.tci_batcheval_d(ctx.h, fm.h, T._lib.ptr(Im), m, 10, T._lib.ptr(Jm), n, 10, 0, dm.ptr,
+                                          dm.ld, C.byref(mx)))
+    kms, kn = ctx.kernel_stats(1)
+    ctx.set_timing(False)
+    dm.free()
+    env_flops = 2 * 2.0 * (m + n) * 10 * 2 * chi ** 3  # two contractions per site and environment
+    res["pi_mpo_contraction"] = {"m": m, "n": n, "sites": N, "bond": chi, "K": chi * chi,
+                                 "ms_device": round(kms / kn, 3),
+                                 "pi_rows_per_s_device": round(m / (kms / kn * 1e-3), 1),
+                                 "TFLOPs_env_plus_gemm": round((env_flops + 2.0 * m * n * chi * chi)
+                                                               / (kms / kn * 1e-3) / 1e12, 2)}
     # other rrLU configurations of SURVEY 8(d): config 2 (4096^2), right-orthogonal pivots, and a
     # 16384^2 matrix (2 GiB) for the scale curve
     res["rrlu_configs"] = []

@@ -125,10 +125,13 @@ struct tci_func {
     int64_t nparams = 0;
     int32_t cpK = 0;
     int64_t ntab = 0;
+    int32_t mpoEnv = 0, mpoTmp = 0;
     FuncDev view() const {
         FuncDev f;
         f.cpK = cpK;
         f.ntab = ntab;
+        f.mpoEnv = mpoEnv;
+        f.mpoTmp = mpoTmp;
         f.kind = kind;
         f.L = L;
         f.localdims = dld;
@@ -639,7 +642,7 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
     if (L < 1) return set_err(c, TCI_ERR_ARG, "L must be >= 1");
     if (L > 62 && (kind == TCI_F_QOSC || kind == TCI_F_QEXP))
         return set_err(c, TCI_ERR_ARG, "quantics integrands support at most 62 legs");
-    int32_t cpK = 0;
+    int32_t cpK = 0, mpoEnv = 0, mpoTmp = 0;
     if (kind == TCI_F_GAUSSMIX || kind == TCI_F_CP) {
         if (nparams < 2 || !params || params[0] < 0) return set_err(c, TCI_ERR_ARG, "params too short");
         cpK = (int32_t)params[0];
@@ -679,6 +682,10 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
                 hdr + offB + rb * d2 * d3 * rb2 > nparams)
                 return set_err(c, TCI_ERR_ARG, "MPO: cores outside params");
             cpK = std::max<int32_t>(cpK, (int32_t)(ra * rb));
+            // LDS of k_mpo_env: padded left environments (ra + 1) rb, right ones ra rb, and the
+            // intermediates (rb d2 + 1) ra' (left) / ra d2 rb' (right)
+            mpoEnv = std::max<int32_t>(mpoEnv, (int32_t)std::max((ra + 1) * rb, (ra2 + 1) * rb2));
+            mpoTmp = std::max<int32_t>(mpoTmp, (int32_t)std::max((rb * d2 + 1) * ra2, ra * d2 * rb2));
         }
     }
     if (kind == TCI_F_TABLE) {
@@ -690,6 +697,8 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
     f->ctx = c;
     f->kind = kind;
     f->cpK = cpK;
+    f->mpoEnv = mpoEnv;
+    f->mpoTmp = mpoTmp;
     if (kind == TCI_F_LORENTZ) {  // quotient table p0 / (s + 1) for every reachable s
         int64_t smax = 0;
         for (int t = 0; t < L; ++t) smax += (int64_t)localdims[t] * localdims[t];

@@ -651,11 +651,15 @@ __device__ __forceinline__ MpoSite mpo_site(const double* p, int t) {
 // sites 0 .. nlegs-1 in order; right: sites t0 .. t0+nlegs-1 from the last one backwards. Writes
 // out[k * ld + R] for k < K4 (k = a + ra_cut * b; zero past the cut's ra * rb) and zeroes the
 // padding rows [nrows * D, ld).
+// LDS layouts keep every inner-product read either broadcast or unit-stride across lanes (the
+// environments of the left chain padded to an odd leading dimension ra + 1, the intermediate to
+// rb*d2 + 1); the summation orders are those of the unpadded form.
 __global__ __launch_bounds__(256) void k_mpo_env(FuncDev f, const int32_t* __restrict__ T, int cnt,
                                                  int nrows, int D, int M, int K4, int64_t ld, int t0,
                                                  int right, double* __restrict__ out) {
-    __shared__ double env[kMpoEnv];
-    __shared__ double tmp[kMpoTmp];
+    extern __shared__ double smem_mpo[];
+    double* env = smem_mpo;              // f.mpoEnv doubles
+    double* tmp = smem_mpo + f.mpoEnv;   // f.mpoTmp doubles
     const double* p = f.params;
     const int N = (int)p[0];
     const double* data = p + 1 + 9 * (int64_t)N;
@@ -681,26 +685,28 @@ __global__ __launch_bounds__(256) void k_mpo_env(FuncDev f, const int32_t* __res
             const double* A = data + s.offA;
             const double* B = data + s.offB;
             if (!right) {
-                // tmp[b, s2, a'] = sum_a env[a, b] A[a, s1, s2, a']   (_extend_cache, first step)
-                const int nt = s.rb * s.d2 * s.ra2;
+                // tmp[b, s2, a'] = sum_a env[a, b] A[a, s1, s2, a']   (_extend_cache, first step);
+                // env[a, b] at a + (ra + 1) b, tmp[b, s2, a'] at b + rb s2 + (rb d2 + 1) a'
+                const int nt = s.rb * s.d2 * s.ra2, le = s.ra + 1, lt = s.rb * s.d2 + 1;
                 for (int o = threadIdx.x; o < nt; o += blockDim.x) {
                     const int b = o % s.rb, s2 = (o / s.rb) % s.d2, a2 = o / (s.rb * s.d2);
                     const double* Ap = A + (int64_t)s.ra * (s1 + (int64_t)s.d1 * (s2 + (int64_t)s.d2 * a2));
                     double acc = 0.0;
-                    for (int a = 0; a < s.ra; ++a) acc = acc + env[a + s.ra * b] * Ap[a];
-                    tmp[o] = acc;
+                    for (int a = 0; a < s.ra; ++a) acc = acc + env[a + le * b] * Ap[a];
+                    tmp[b + s.rb * s2 + lt * a2] = acc;
                 }
                 __syncthreads();
                 // env[a', b'] = sum_{s2, b} tmp[b, s2, a'] B[b, s2, s3, b']   (second step)
-                const int ne = s.ra2 * s.rb2;
+                const int ne = s.ra2 * s.rb2, le2 = s.ra2 + 1;
                 for (int o = threadIdx.x; o < ne; o += blockDim.x) {
                     const int a2 = o % s.ra2, b2 = o / s.ra2;
                     const double* Bp = B + (int64_t)s.rb * s.d2 * (s3 + (int64_t)s.d3 * b2);
+                    const double* tp = tmp + lt * a2;
                     double acc = 0.0;
                     for (int s2 = 0; s2 < s.d2; ++s2)
                         for (int b = 0; b < s.rb; ++b)
-                            acc = acc + tmp[b + s.rb * (s2 + s.d2 * a2)] * Bp[b + (int64_t)s.rb * s2];
-                    env[o] = acc;
+                            acc = acc + tp[b + s.rb * s2] * Bp[b + (int64_t)s.rb * s2];
+                    env[a2 + le2 * b2] = acc;
                 }
                 ea = s.ra2;
                 eb = s.rb2;
@@ -733,7 +739,10 @@ __global__ __launch_bounds__(256) void k_mpo_env(FuncDev f, const int32_t* __res
             }
             __syncthreads();
         }
-        for (int k = threadIdx.x; k < K4; k += blockDim.x) out[(int64_t)k * ld + R] = k < ea * eb ? env[k] : 0.0;
+        // factor row: k = a + ea * b (the left chain's environment is stored with ld ea + 1)
+        const int lde = right ? ea : ea + 1;
+        for (int k = threadIdx.x; k < K4; k += blockDim.x)
+            out[(int64_t)k * ld + R] = k < ea * eb ? env[k % ea + lde * (k / ea)] : 0.0;
         __syncthreads();
     }
 }
@@ -893,10 +902,13 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
         double* EL = reinterpret_cast<double*>(scratch);
         double* ER = EL + (int64_t)K4 * ldR;
         if (f.kind == F_MPO) {  // environments: one workgroup per row / column
-            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(mR, 1), 8192)), dim3(256),
-                               0, s, f, I, nl, m, D, M, K4, ldR, 0, 0, EL);
-            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(n, 1), 8192)), dim3(256),
-                               0, s, f, J, nr, n, 1, 0, K4, ldC, f.L - nr, 1, ER);
+            const size_t lds = 8 * ((size_t)f.mpoEnv + f.mpoTmp);
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mpo_env),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(mR, 1), 16384)),
+                               dim3(256), lds, s, f, I, nl, m, D, M, K4, ldR, 0, 0, EL);
+            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(n, 1), 16384)),
+                               dim3(256), lds, s, f, J, nr, n, 1, 0, K4, ldC, f.L - nr, 1, ER);
         } else {
             hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldR * K4, 4096)), dim3(256), 0, s, f, I, nl,
                                m, D, M, K, K4, ldR, 0, false, EL);

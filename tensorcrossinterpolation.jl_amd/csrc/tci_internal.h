@@ -96,6 +96,7 @@ struct FuncDev {
     const int64_t* strides;    // device, column-major strides for TCI_F_TABLE
     int32_t cpK;               // separable terms (TCI_F_GAUSSMIX, TCI_F_CP; TCI_F_MPO: max ra*rb), host copy
     int64_t ntab;              // TCI_F_LORENTZ: quotient table size (max sum of squares + 1), or 0
+    int32_t mpoEnv, mpoTmp;    // TCI_F_MPO: LDS (doubles) of the environment kernel's two buffers
 };
 
 // ---- rrLU (tci_rrlu.hip)
