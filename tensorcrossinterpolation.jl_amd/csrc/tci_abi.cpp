@@ -40,6 +40,7 @@ struct tci_ctx {
     int flush_every = 11;  // deferred-update depth nb (1 = write back every pivot; 10-12 measured equal with the shadow search)
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
+    int pass_gridx = 1;    // rrLU pass workgroups per CU (env TCI_PASS_GRIDX; 1 = all resident at once)
     float* sbuf = nullptr; // its fp32 shadow of the matrix
     size_t capS = 0;
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
@@ -374,7 +375,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         g.S = c->sbuf;
     }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
-                                      std::min(std::max(c->ncu, 1), kMaxGrid));
+                                      std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
     bool stopped = false;
@@ -536,6 +537,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
+    if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     {
