@@ -684,10 +684,10 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
                 hdr + offB + rb * d2 * d3 * rb2 > nparams)
                 return set_err(c, TCI_ERR_ARG, "MPO: cores outside params");
             cpK = std::max<int32_t>(cpK, (int32_t)(ra * rb));
-            // LDS of k_mpo_env: padded left environments (ra + 1) rb, right ones ra rb, and the
-            // intermediates (rb d2 + 1) ra' (left) / ra d2 rb' (right)
+            // LDS of k_mpo_env / k_mpo_env_mfma: environments (ra + 1) rb, intermediates
+            // (rb d2 + 1) ra' (left chain) / (ra d2 + 1) rb' (right chain)
             mpoEnv = std::max<int32_t>(mpoEnv, (int32_t)std::max((ra + 1) * rb, (ra2 + 1) * rb2));
-            mpoTmp = std::max<int32_t>(mpoTmp, (int32_t)std::max((rb * d2 + 1) * ra2, ra * d2 * rb2));
+            mpoTmp = std::max<int32_t>(mpoTmp, (int32_t)std::max((rb * d2 + 1) * ra2, (ra * d2 + 1) * rb2));
         }
     }
     if (kind == TCI_F_TABLE) {

@@ -747,6 +747,109 @@ __global__ __launch_bounds__(256) void k_mpo_env(FuncDev f, const int32_t* __res
     }
 }
 
+// The same environments with both per-site contractions on v_mfma_f64_16x16x4f64 (used when
+// the bonds are not tiny, cpK >= 64): every site is two small GEMMs whose operands come from LDS
+// (the environment, the intermediate) and from the L2-resident cores, 16 x 16 output tiles
+// spread over the 4 waves, zero-filled past the edges. Operand lanes: A[row l&15][k l>>4],
+// B[k l>>4][col l&15]; result: col = l & 15, row = (l >> 4) + 4 * reg. Environments of both
+// chains at a + (ra + 1) b; intermediates with leading dimensions rb*d2 + 1 (left) and
+// ra*d2 + 1 (right), so that lanes reading different rows hit different banks.
+typedef double mpo_dbl4 __attribute__((ext_vector_type(4)));
+
+template <class FA, class FB, class FS>
+__device__ __forceinline__ void mpo_mfma_gemm(int M, int N, int K, FA fa, FB fb, FS st) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int tm = (M + 15) >> 4, tn = (N + 15) >> 4;
+    for (int t = wave; t < tm * tn; t += nw) {  // wave-uniform
+        const int m0 = (t % tm) << 4, n0 = (t / tm) << 4;
+        const int r = m0 + (lane & 15), cc = n0 + (lane & 15), kq = lane >> 4;
+        mpo_dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < K; k0 += 4) {
+            const int k = k0 + kq;
+            const double a = (r < M && k < K) ? fa(r, k) : 0.0;
+            const double b = (k < K && cc < N) ? fb(k, cc) : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rr = m0 + (lane >> 4) + 4 * i;
+            if (rr < M && cc < N) st(rr, cc, acc[i]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mpo_env_mfma(FuncDev f, const int32_t* __restrict__ T, int cnt,
+                                                      int nrows, int D, int M, int K4, int64_t ld, int t0,
+                                                      int right, double* __restrict__ out) {
+    extern __shared__ double smem_mpo[];
+    double* env = smem_mpo;              // f.mpoEnv doubles
+    double* tmp = smem_mpo + f.mpoEnv;   // f.mpoTmp doubles
+    const double* p = f.params;
+    const int N = (int)p[0];
+    const double* data = p + 1 + 9 * (int64_t)N;
+    const int nlegs = cnt + (M ? 1 : 0);
+    const int64_t rows = (int64_t)nrows * D;
+    for (int64_t e = rows * K4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ld * K4;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = (e - rows * K4) / (ld - rows), R = rows + (e - rows * K4) % (ld - rows);
+        out[k * ld + R] = 0.0;
+    }
+    for (int64_t R = blockIdx.x; R < rows; R += gridDim.x) {
+        const int i = (int)(R % nrows), c = (int)(R / nrows);
+        const int32_t* e = T + (int64_t)i * cnt;
+        if (threadIdx.x == 0) env[0] = 1.0;
+        int ea = 1, eb = 1;
+        __syncthreads();
+        for (int q = 0; q < nlegs; ++q) {
+            const int leg = right ? nlegs - 1 - q : q;
+            const int t = right ? t0 + leg : leg;
+            const int idx = (leg < cnt ? e[leg] : c + 1) - 1;
+            const MpoSite s = mpo_site(p, t);
+            const int s1 = idx % s.d1, s3 = idx / s.d1;
+            const double* A = data + s.offA + (int64_t)s.ra * s1;           // A[a, s1, s2, a'] at a + ra d1 (s2 + d2 a')
+            const double* B = data + s.offB + (int64_t)s.rb * s.d2 * s3;    // B[b, s2, s3, b'] at b + rb s2 + rb d2 d3 b'
+            const int64_t sA = (int64_t)s.ra * s.d1, sB = (int64_t)s.rb * s.d2 * s.d3;
+            if (!right) {
+                const int le = s.ra + 1, lt = s.rb * s.d2 + 1, le2 = s.ra2 + 1, d2 = s.d2, rb = s.rb;
+                // tmp[b, s2, a'] = sum_a env[a, b] A[a, s1, s2, a']: rows b, columns n = s2 + d2 a'
+                mpo_mfma_gemm(
+                    s.rb, s.d2 * s.ra2, s.ra, [&](int b, int a) { return env[a + le * b]; },
+                    [&](int a, int n) { return A[a + sA * ((n % d2) + (int64_t)d2 * (n / d2))]; },
+                    [&](int b, int n, double v) { tmp[b + rb * (n % d2) + lt * (n / d2)] = v; });
+                __syncthreads();
+                // env[a', b'] = sum_{kk = b + rb s2} tmp[kk, a'] B[kk, s3, b']
+                mpo_mfma_gemm(
+                    s.ra2, s.rb2, s.rb * s.d2, [&](int a2, int kk) { return tmp[kk + lt * a2]; },
+                    [&](int kk, int b2) { return B[kk + sB * b2]; },
+                    [&](int a2, int b2, double v) { env[a2 + le2 * b2] = v; });
+                ea = s.ra2;
+                eb = s.rb2;
+            } else {
+                const int le2 = s.ra2 + 1, ra = s.ra, d2 = s.d2, lr = s.ra * s.d2 + 1, le = s.ra + 1;
+                // tmp[a, s2, b'] = sum_a' A[a, s1, s2, a'] env[a', b']: rows r = a + ra s2
+                mpo_mfma_gemm(
+                    s.ra * s.d2, s.rb2, s.ra2,
+                    [&](int r, int a2) { return A[(r % ra) + sA * ((r / ra) + (int64_t)d2 * a2)]; },
+                    [&](int a2, int b2) { return env[a2 + le2 * b2]; },
+                    [&](int r, int b2, double v) { tmp[r + lr * b2] = v; });
+                __syncthreads();
+                // env[a, b] = sum_{kk = s2 + d2 b'} tmp[a, s2, b'] B[b, s2, s3, b']
+                mpo_mfma_gemm(
+                    s.ra, s.rb, s.d2 * s.rb2,
+                    [&](int a, int kk) { return tmp[a + ra * (kk % d2) + lr * (kk / d2)]; },
+                    [&](int kk, int b) { return B[b + (int64_t)s.rb * (kk % d2) + sB * (kk / d2)]; },
+                    [&](int a, int b, double v) { env[a + le * b] = v; });
+                ea = s.ra;
+                eb = s.rb;
+            }
+            __syncthreads();
+        }
+        for (int k = threadIdx.x; k < K4; k += blockDim.x)
+            out[(int64_t)k * ld + R] = k < ea * eb ? env[k % ea + (ea + 1) * (k / ea)] : 0.0;
+        __syncthreads();
+    }
+}
+
 // Pi[R, j] = sum_k EL[k, R] * ER[k, j] on v_mfma_f64_16x16x4_f64: a wave owns a 32 x 32 tile
 // (2 x 2 MFMA blocks), a workgroup 4 waves (64 x 64). Operand lanes: A[row l&15][k l>>4],
 // B[k l>>4][col l&15]; result: col = l & 15, row = (l >> 4) + 4 * reg (cdna_hip_programming.md).
@@ -903,11 +1006,13 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
         double* ER = EL + (int64_t)K4 * ldR;
         if (f.kind == F_MPO) {  // environments: one workgroup per row / column
             const size_t lds = 8 * ((size_t)f.mpoEnv + f.mpoTmp);
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mpo_env),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(mR, 1), 16384)),
+            // tiny bonds: one thread per output entry; otherwise the per-site GEMMs on MFMA
+            auto kern = f.cpK >= 64 ? k_mpo_env_mfma : k_mpo_env;
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(mR, 1), 16384)),
                                dim3(256), lds, s, f, I, nl, m, D, M, K4, ldR, 0, 0, EL);
-            hipLaunchKernelGGL(k_mpo_env, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(n, 1), 16384)),
+            hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(std::max<int64_t>(n, 1), 16384)),
                                dim3(256), lds, s, f, J, nr, n, 1, 0, K4, ldC, f.L - nr, 1, ER);
         } else {
             hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldR * K4, 4096)), dim3(256), 0, s, f, I, nl,
