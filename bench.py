@@ -223,7 +223,7 @@ def main():
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 12, "shadow": True}  # the profiled command
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 11, "shadow": True}  # the profiled command
 
 
 def pmc_traffic(fam, m, n, r, nb, shadow):
