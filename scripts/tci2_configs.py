@@ -74,6 +74,16 @@ def configs():
                    [p0], tolerance=1e-10, maxbonddim=256, maxiter=3, nsearchglobalpivot=0)
     out["C5_cp12d_K256"] = cp12
 
+    def cp12_default():
+        # as C5 scaled, with the default global pivot search (site tensors solved every iteration)
+        rng = np.random.default_rng(2)
+        K, L, d = 256, 12, 32
+        f = T.cp_function(0.5 + rng.random((K, L, d)))
+        p0 = T.optfirstpivot(f, [d] * L)
+        return run("C5 scaled, default global pivot search", f, [d] * L, [p0], tolerance=1e-10,
+                   maxbonddim=256, maxiter=3, rng=np.random.default_rng(0))
+    out["C5_cp12d_K256_default"] = cp12_default
+
     def cp12_full():
         # config 5 as stated: CP-rank-1024 synthetic, 12 legs of d = 32, ranks up to 1024 (Pi up to
         # 32768^2 = 8 GiB, rrLU at r = 1024); no separate warm-up (the kernels are those of C5 scaled)

@@ -258,6 +258,23 @@ def test_sitetensor_solve(ctx):
     np.testing.assert_allclose(tens.reshape(ref.shape, order="F"), ref, rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("r,R", [(100, 1000), (300, 777), (600, 1201)])
+def test_sitetensor_solve_blocked(ctx, r, R):
+    # T = Pi1 * P^-1 (tensorci2.jl:620-627) with the LDS-blocked getrs (32 / 16 / 8 right-hand
+    # sides per workgroup, partial tiles included)
+    import ctypes as C
+    rng = np.random.default_rng(r + R)
+    P = rng.random((r, r)) + r * np.eye(r) * rng.choice([-1, 1], r)
+    Pi1 = rng.random((R, r))
+    T_ = np.zeros(R * r)
+    ctx.check(ctx.lib.tci_sitetensor_solve_h(ctx.h, T._lib.ptr(np.asfortranarray(P).ravel(order="F")), r,
+                                             T._lib.ptr(np.asfortranarray(Pi1).ravel(order="F")), R,
+                                             T._lib.ptr(T_)))
+    ref = O.sitetensor_solve(P, Pi1)
+    got = T_.reshape((R, r), order="F")
+    np.testing.assert_allclose(got, ref.reshape(got.shape, order="F"), rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
 # ------------------------------------------------------------------ TCI2
 def _compare_tci(tci, ranks, errors, rt, rranks, rerrors, rtol=1e-10, exact_f=True):
     """exact_f: integer-exact integrand (bitwise Pi) -> errors to 1e-10 relative of themselves;
