@@ -136,6 +136,16 @@ int tci_rrlu_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t 
                        int64_t* rowperm, int64_t* colperm, int64_t* npivot, double* lasterror,
                        double* pivoterrors);
 
+/* rrlu(A::Matrix{ComplexF64}) (matrixlu.jl:455-463; the _optimizerrlu! loop :346-396 on complex
+ * entries). A, L, U are ComplexF64 stored interleaved (re, im) column-major
+ * (Julia's layout): A is 2*lda*n doubles, L m x maxrank (ld m), U maxrank x n (ld ldu >= maxrank,
+ * counted in complex entries). pivoterrors: np + 1 values [abs.(diag(lu)); lu.error]
+ * (matrixlu.jl:799), NULL to skip. Same permutation / error conventions as tci_rrlu_h. */
+int tci_rrlu_c128_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
+                    int64_t* colperm, double* L, double* U, int64_t ldu, int64_t* npivot,
+                    double* lasterror, double* pivoterrors);
+
 /* ------------------------------------------------------------ MatrixLUCI
  * Replaces MatrixLUCI(A; kw...) + left/right/pivoterrors (matrixluci.jl:55-57, 161-311):
  * leftorth: left = colstimespivotinv (TRSM), right = rowmatrix (GEMM);

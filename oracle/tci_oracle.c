@@ -1136,3 +1136,161 @@ int orc_tci_evaluate(const orc_tci* t, const i32* idx, double* out) {
     free(v);
     return ORC_OK;
 }
+
+/* ============================================================ ComplexF64 rrLU
+ * rrlu(A::Matrix{ComplexF64}) -- the same _optimizerrlu! / addpivot! loop (matrixlu.jl:295-322,
+ * 346-396) on complex entries, stored interleaved (re, im) column-major like Julia's
+ * ComplexF64 arrays. Julia Base arithmetic the loop relies on (base/complex.jl, not under
+ * /root/reference; restated from its published algorithm, parity at the last-ulp level of the
+ * division and of abs unpinned):
+ *   abs2(z) = re*re + im*im;  z*w = (ac - bd, ad + bc) without fma;  a - b componentwise;
+ *   z / w   = Baudin & Smith robust division (the ComplexF64 method of `/`);
+ *   abs(z)  = hypot(re, im) (correctly rounded fma branch of Base.Math._hypot). */
+
+static void jl_cdiv2(double a, double b, double c, double d, double r, double t, double* out) {
+    if (r != 0) {
+        double br = b * r;
+        *out = (br != 0) ? (a + br) * t : a * t + (b * t) * r;
+    } else {
+        *out = (a + d * (b / c)) * t;
+    }
+}
+
+static void jl_cdiv1(double a, double b, double c, double d, double* p, double* q) {
+    double r = d / c;
+    double t = 1.0 / (c + d * r);
+    jl_cdiv2(a, b, c, d, r, t, p);
+    jl_cdiv2(b, -a, c, d, r, t, q);
+}
+
+void orc_cdiv(double a, double b, double c, double d, double* re, double* im) {
+    double absa = fabs(a), absb = fabs(b), ab = absa >= absb ? absa : absb;
+    double absc = fabs(c), absd = fabs(d), cd = absc >= absd ? absc : absd;
+    const double halfov = 0.5 * 1.7976931348623157e308;
+    const double twounE = 2.2250738585072014e-308 * 2.0 / 2.220446049250313e-16;
+    const double bs = 2.0 / (2.220446049250313e-16 * 2.220446049250313e-16);
+    double s = 1.0, p, q;
+    if (ab >= halfov) { a *= 0.5; b *= 0.5; s *= 2.0; }
+    if (cd >= halfov) { c *= 0.5; d *= 0.5; s *= 0.5; }
+    if (ab <= twounE) { a *= bs; b *= bs; s /= bs; }
+    if (cd <= twounE) { c *= bs; d *= bs; s *= bs; }
+    if (absd <= absc) {
+        jl_cdiv1(a, b, c, d, &p, &q);
+    } else {
+        jl_cdiv1(b, a, d, c, &p, &q);
+        q = -q;
+    }
+    *re = p * s;
+    *im = q * s;
+}
+
+double orc_hypot(double x, double y) {
+    if (isinf(x) || isinf(y)) return INFINITY;
+    double ax = fabs(x), ay = fabs(y);
+    if (ay > ax) { double t = ax; ax = ay; ay = t; }
+    if (isnan(ax) || isnan(ay)) return ax + ay;
+    if (ay <= ax * sqrt(2.220446049250313e-16 / 2)) return ax;
+    double scale = 2.220446049250313e-16 * sqrt(2.2250738585072014e-308);
+    if (ax > sqrt(1.7976931348623157e308 / 2)) {
+        ax *= scale; ay *= scale; scale = 1.0 / scale;
+    } else if (ay < sqrt(2.2250738585072014e-308)) {
+        ax /= scale; ay /= scale;
+    } else {
+        scale = 1.0;
+    }
+    double h = sqrt(fma(ax, ax, ay * ay));
+    double hsq = h * h, axsq = ax * ax;
+    h -= (fma(-ay, ay, hsq - axsq) + fma(h, h, -hsq) - fma(ax, ax, -axsq)) / (2 * h);
+    return h * scale;
+}
+
+/* _optimizerrlu! on ComplexF64 (matrixlu.jl:346-396); A interleaved m x n (ld m), copied.
+ * rowperm/colperm 0-based; L m x np, U np x n (interleaved, written for the np found; capacity
+ * maxrank); pivoterrs np + 1 values [abs.(diag(lu)); lu.error] (matrixlu.jl:799). */
+int orc_rrlu_c128(const double* A0, i64 m, i64 n, i64 maxrank, double reltol, double abstol,
+                  int leftorth, i64* rowperm, i64* colperm, double* L, double* U, i64* npivot,
+                  double* lasterr, double* pivoterrs) {
+    double* A = (double*)malloc(sizeof(double) * (size_t)(2 * m * n + 2));
+    if (!A) return fail(ORC_ERR_ALLOC, "allocation failed");
+    memcpy(A, A0, sizeof(double) * (size_t)(2 * m * n));
+#define RE(i, j) A[2 * ((i) + (j) * m)]
+#define IM(i, j) A[2 * ((i) + (j) * m) + 1]
+    for (i64 i = 0; i < m; ++i) rowperm[i] = i;
+    for (i64 j = 0; j < n; ++j) colperm[j] = j;
+    i64 mr = maxrank < m ? maxrank : m;
+    if (mr > n) mr = n;
+    double maxerror = 0.0, error = NAN;
+    i64 np = 0;
+    while (np < mr) {
+        i64 k = np, p = k, q = k;
+        double best = -INFINITY;  /* submatrixargmax(abs2, A, k) (matrixlu.jl:46-87, 133-135) */
+        for (i64 c = k; c < n; ++c)
+            for (i64 r = k; r < m; ++r) {
+                double v = RE(r, c) * RE(r, c) + IM(r, c) * IM(r, c);
+                if (v > best) { best = v; p = r; q = c; }
+            }
+        error = orc_hypot(RE(p, q), IM(p, q));
+        if ((error < reltol * maxerror || error < abstol) && np > 0) break;
+        maxerror = jl_max(maxerror, error);
+        /* addpivot!: swaprow!, swapcol!, normalise, rank-1 update (matrixlu.jl:295-322) */
+        i64 t;
+        t = rowperm[k]; rowperm[k] = rowperm[p]; rowperm[p] = t;
+        for (i64 j = 0; j < n; ++j) {
+            double a = RE(k, j), b = IM(k, j);
+            RE(k, j) = RE(p, j); IM(k, j) = IM(p, j);
+            RE(p, j) = a; IM(p, j) = b;
+        }
+        t = colperm[k]; colperm[k] = colperm[q]; colperm[q] = t;
+        for (i64 i = 0; i < m; ++i) {
+            double a = RE(i, k), b = IM(i, k);
+            RE(i, k) = RE(i, q); IM(i, k) = IM(i, q);
+            RE(i, q) = a; IM(i, q) = b;
+        }
+        const double pr = RE(k, k), pi = IM(k, k);
+        if (leftorth) {
+            for (i64 i = k + 1; i < m; ++i) orc_cdiv(RE(i, k), IM(i, k), pr, pi, &RE(i, k), &IM(i, k));
+        } else {
+            for (i64 j = k + 1; j < n; ++j) orc_cdiv(RE(k, j), IM(k, j), pr, pi, &RE(k, j), &IM(k, j));
+        }
+        for (i64 j = k + 1; j < n; ++j) {
+            const double yr = RE(k, j), yi = IM(k, j);
+            for (i64 i = k + 1; i < m; ++i) {
+                const double xr = RE(i, k), xi = IM(i, k);
+                const double zr = xr * yr - xi * yi, zi = xr * yi + xi * yr;
+                RE(i, j) = RE(i, j) - zr;
+                IM(i, j) = IM(i, j) - zi;
+            }
+        }
+        np += 1;
+    }
+    if (np >= (m < n ? m : n)) error = 0.0;
+    /* L = tril(A[:, 1:np]), U = triu(A[1:np, :]), NaN checks, unit diagonal (matrixlu.jl:372-388) */
+    int nan = 0;
+    for (i64 c = 0; c < np; ++c)
+        for (i64 r = 0; r < m; ++r) {
+            double a = r >= c ? RE(r, c) : 0.0, b = r >= c ? IM(r, c) : 0.0;
+            nan |= isnan(a) || isnan(b);
+            if (L) { L[2 * (r + c * m)] = a; L[2 * (r + c * m) + 1] = b; }
+        }
+    if (nan) { free(A); return fail(ORC_ERR_NAN, "lu.L contains NaNs"); }
+    for (i64 c = 0; c < n; ++c)
+        for (i64 r = 0; r < np; ++r) {
+            double a = r <= c ? RE(r, c) : 0.0, b = r <= c ? IM(r, c) : 0.0;
+            nan |= isnan(a) || isnan(b);
+            if (U) { U[2 * (r + c * np)] = a; U[2 * (r + c * np) + 1] = b; }
+        }
+    if (nan) { free(A); return fail(ORC_ERR_NAN, "lu.U contains NaNs"); }
+    for (i64 c = 0; c < np; ++c) {
+        if (pivoterrs) pivoterrs[c] = orc_hypot(RE(c, c), IM(c, c));
+        double* D = leftorth ? L : U;
+        i64 off = leftorth ? 2 * (c + c * m) : 2 * (c + c * np);
+        if (D) { D[off] = 1.0; D[off + 1] = 0.0; }
+    }
+    if (pivoterrs) pivoterrs[np] = error;
+#undef RE
+#undef IM
+    *npivot = np;
+    *lasterr = error;
+    free(A);
+    return ORC_OK;
+}

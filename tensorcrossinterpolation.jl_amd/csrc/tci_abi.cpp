@@ -97,6 +97,8 @@ struct tci_ctx {
     size_t capL = 0;
     double* dU = nullptr;
     size_t capU = 0;
+    char* cws = nullptr;  // ComplexF64 rrLU: state, candidates, pivot column / row buffers
+    size_t capCws = 0;
     // kernel timing (family 0: rrLU pass with write-back, 1: batch evaluation,
     //                2: rrLU read-only pass)
     bool timing = false;
@@ -579,7 +581,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
-    fr(c->dU);
+    fr(c->dU); fr(c->cws);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
@@ -805,6 +807,91 @@ int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
         HIPCHK(c, hipMemcpy2DAsync(U, ldu * sizeof(double), c->dU, np * sizeof(double),
                                    np * sizeof(double), n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
+                    int64_t* colperm, double* L, double* U, int64_t ldu, int64_t* npivot,
+                    double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
+        return set_err(c, TCI_ERR_ARG, "rrlu: invalid dimensions");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    if (U && ldu < std::max<int64_t>(mr, 1)) return set_err(c, TCI_ERR_ARG, "rrlu: ldu < maxrank");
+    const int64_t ld = std::max<int64_t>(m, 1);
+    const int mi = (int)m, ni = (int)n;
+    const int G = tci::crrlu_grid(mi, ni, 0);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t oSt = 0, oCand = al(sizeof(tci::CState)), oCol = oCand + al(sizeof(tci::CCand) * G);
+    const size_t oRow = oCol + al(16 * (size_t)std::max(mi, 1));
+    const size_t bytes = oRow + al(16 * (size_t)std::max(ni, 1));
+    int st;
+    if ((st = ensure(c, &c->cws, &c->capCws, bytes))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
+    if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * mr, 1))))) return st;
+    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(mr * n, 1))))) return st;
+    tci::CState* dst = reinterpret_cast<tci::CState*>(c->cws + oSt);
+    tci::launch_crrlu_init(c->stream, dst, c->rowperm, c->colperm, mi, ni);
+    HIPCHK(c, hipGetLastError());
+    double2* dA = reinterpret_cast<double2*>(c->dA);
+    if (m > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
+                                   c->stream));
+    tci::CStepArgs g{};
+    g.A = dA;
+    g.ld = ld;
+    g.m = mi;
+    g.n = ni;
+    g.mr = (int)mr;
+    g.leftorth = leftorth;
+    g.reltol = reltol;
+    g.abstol = abstol;
+    g.st = dst;
+    g.cand = reinterpret_cast<tci::CCand*>(c->cws + oCand);
+    g.colbuf = reinterpret_cast<double2*>(c->cws + oCol);
+    g.rowbuf = reinterpret_cast<double2*>(c->cws + oRow);
+    g.rowperm = c->rowperm;
+    g.colperm = c->colperm;
+    // one step per pivot; steps after the stop test fired return at once (st->done)
+    for (int t = 0; mr > 0 && t <= mr; ++t) {
+        g.t = t;
+        tci::launch_crrlu_step(c->stream, g);
+        HIPCHK(c, hipGetLastError());
+    }
+    tci::CState hs;
+    HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t np = hs.np;
+    double2* dL = reinterpret_cast<double2*>(c->dL);
+    double2* dU = reinterpret_cast<double2*>(c->dU);
+    double* dpe = reinterpret_cast<double*>(g.colbuf);  // free after the last step
+    if (np > 0) {
+        tci::launch_crrlu_extract(c->stream, dA, ld, mi, ni, (int)np, leftorth, dL, dU, np, dpe,
+                                  &dst->nan);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (hs.nan & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+        if (hs.nan & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    }
+    *npivot = np;
+    *lasterror = np >= std::min(m, n) ? 0.0 : hs.err;
+    if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    if (np > 0 && L)
+        HIPCHK(c, hipMemcpyAsync(L, dL, m * np * 16, hipMemcpyDeviceToHost, c->stream));
+    if (np > 0 && U)
+        HIPCHK(c, hipMemcpy2DAsync(U, ldu * 16, dU, np * 16, np * 16, n, hipMemcpyDeviceToHost,
+                                   c->stream));
+    if (np > 0 && pivoterrors)
+        HIPCHK(c, hipMemcpyAsync(pivoterrors, dpe, np * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (pivoterrors) pivoterrors[np] = *lasterror;
     return TCI_OK;
 }
 

@@ -106,6 +106,38 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).
 // shadow: the initial and write-back passes also store the fp32 shadow g.S, and
 // the read-only passes run the certified fp32 search (k_pass_sh; same results, ~half the bytes)
+// ComplexF64 rrLU (tci_rrlu_c128.hip): candidate, device state, one step's arguments
+struct CCand {
+    double v;  // abs2
+    int32_t col, row;
+};
+struct CState {
+    int64_t np;
+    int32_t done;
+    int32_t nan;
+    double maxerror;
+    double err;
+    double2 piv;
+};
+struct CStepArgs {
+    double2* A;
+    int64_t ld;
+    int m, n, t, mr, tiles_r, leftorth;
+    double reltol, abstol;
+    CState* st;
+    CCand* cand;
+    double2* colbuf;
+    double2* rowbuf;
+    int64_t* rowperm;
+    int64_t* colperm;
+};
+int crrlu_grid(int m, int n, int t);
+void launch_crrlu_init(hipStream_t s, CState* st, int64_t* rowperm, int64_t* colperm, int m, int n);
+void launch_crrlu_step(hipStream_t s, CStepArgs g);
+void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, int n, int np,
+                          int leftorth, double2* L, double2* U, int64_t ldu, double* pe,
+                          int* nanflag);
+
 void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);

@@ -1,0 +1,336 @@
+// tci_rrlu_c128.hip -- rrLU with full pivoting on ComplexF64 matrices (gfx950).
+//
+// rrlu(A::Matrix{ComplexF64}) runs the same _optimizerrlu! / addpivot! loop as the Float64 path
+// (matrixlu.jl:295-322, 346-396); SURVEY §8f rank 4. Entries are double2 (re, im) column-major,
+// Julia's ComplexF64 layout. Unlike the Float64 kernels (logical swaps, deferred updates,
+// certified fp32 shadow search) this path keeps the reference's physical row/column swaps: one
+// launch per pivot, each doing
+//   (1) the rank-1 update of pivot t-1 (normalised column/row from the published pivot
+//       column/row buffers, so no workgroup reads what another writes), complex multiply then
+//       subtract componentwise (matrixlu.jl:318; no fma: -ffp-contract=off),
+//   (2) the argmax of abs2 over the trailing block for pivot t (strict '>' in column-major order
+//       -> ties to the smallest column, then row; NaN never wins; matrixlu.jl:46-87),
+//   (3) in a one-workgroup launch of its own (no cross-XCD hand-off inside a kernel): the
+//       candidates' reduction, the stop test (matrixlu.jl:360-365), the row/column swap over the
+//       whole matrix (swaprow!/swapcol!, matrixlu.jl:254-275) and the publication of the new
+//       pivot column/row.
+// Per pivot that is one read+write of the trailing block (32 B/element) -- HBM-bound like the
+// Float64 rank-1 update (2x the bytes of the real case; 8 flops/element).
+// Julia Base arithmetic restated: ComplexF64 `/` is Baudin & Smith's robust division and
+// abs(z) = hypot(re, im) (base/complex.jl, base/math.jl; not under /root/reference), identical
+// to oracle/tci_oracle.c (orc_cdiv / orc_hypot) bit for bit.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "tci_internal.h"
+
+namespace tci {
+namespace {
+
+constexpr int kCTR = 64;      // rows per tile (one wave lane per row)
+constexpr int kCTC = 16;      // columns per tile (4 waves x 4 columns)
+constexpr int kCThreads = 256;
+
+__device__ inline bool cbetter(const CCand& b, const CCand& a) {
+    return b.v > a.v || (b.v == a.v && (b.col < a.col || (b.col == a.col && b.row < a.row)));
+}
+
+__device__ inline void jl_cdiv2(double a, double b, double c, double d, double r, double t,
+                                double* out) {
+    if (r != 0) {
+        double br = b * r;
+        *out = (br != 0) ? (a + br) * t : a * t + (b * t) * r;
+    } else {
+        *out = (a + d * (b / c)) * t;
+    }
+}
+
+__device__ inline double2 jl_cdiv(double2 z, double2 w) {
+    double a = z.x, b = z.y, c = w.x, d = w.y;
+    const double absa = fabs(a), absb = fabs(b), ab = absa >= absb ? absa : absb;
+    const double absc = fabs(c), absd = fabs(d), cd = absc >= absd ? absc : absd;
+    const double halfov = 0.5 * 1.7976931348623157e308;
+    const double twounE = 2.2250738585072014e-308 * 2.0 / 2.220446049250313e-16;
+    const double bs = 2.0 / (2.220446049250313e-16 * 2.220446049250313e-16);
+    double s = 1.0, p, q;
+    if (ab >= halfov) { a *= 0.5; b *= 0.5; s *= 2.0; }
+    if (cd >= halfov) { c *= 0.5; d *= 0.5; s *= 0.5; }
+    if (ab <= twounE) { a *= bs; b *= bs; s /= bs; }
+    if (cd <= twounE) { c *= bs; d *= bs; s *= bs; }
+    if (absd <= absc) {
+        const double r = d / c, t = 1.0 / (c + d * r);
+        jl_cdiv2(a, b, c, d, r, t, &p);
+        jl_cdiv2(b, -a, c, d, r, t, &q);
+    } else {
+        const double r = c / d, t = 1.0 / (d + c * r);
+        jl_cdiv2(b, a, d, c, r, t, &p);
+        jl_cdiv2(a, -b, d, c, r, t, &q);
+        q = -q;
+    }
+    return make_double2(p * s, q * s);
+}
+
+__device__ inline double jl_hypot(double x, double y) {
+    if (isinf(x) || isinf(y)) return INFINITY;
+    double ax = fabs(x), ay = fabs(y);
+    if (ay > ax) { double t = ax; ax = ay; ay = t; }
+    if (isnan(ax) || isnan(ay)) return ax + ay;
+    if (ay <= ax * sqrt(2.220446049250313e-16 / 2)) return ax;
+    double scale = 2.220446049250313e-16 * sqrt(2.2250738585072014e-308);
+    if (ax > sqrt(1.7976931348623157e308 / 2)) {
+        ax *= scale; ay *= scale; scale = 1.0 / scale;
+    } else if (ay < sqrt(2.2250738585072014e-308)) {
+        ax /= scale; ay /= scale;
+    } else {
+        scale = 1.0;
+    }
+    double h = sqrt(fma(ax, ax, ay * ay));
+    const double hsq = h * h, axsq = ax * ax;
+    h -= (fma(-ay, ay, hsq - axsq) + fma(h, h, -hsq) - fma(ax, ax, -axsq)) / (2 * h);
+    return h * scale;
+}
+
+__device__ inline double jl_maxd(double x, double y) {  // Base.max: NaN-propagating
+    if (x != x || y != y) return NAN;
+    return x > y ? x : y;
+}
+
+__device__ inline double2 cmul(double2 x, double2 y) {
+    return make_double2(x.x * y.x - x.y * y.y, x.x * y.y + x.y * y.x);
+}
+
+__device__ inline CCand shfl_cand(const CCand& c, int mask) {
+    CCand o;
+    o.v = __shfl_xor(c.v, mask);
+    o.col = __shfl_xor(c.col, mask);
+    o.row = __shfl_xor(c.row, mask);
+    return o;
+}
+
+// block-wide argmax; the result is valid in every thread
+__device__ CCand block_reduce(CCand c, CCand* sh) {
+    for (int mask = 32; mask >= 1; mask >>= 1) {
+        CCand o = shfl_cand(c, mask);
+        if (cbetter(o, c)) c = o;
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = c;
+    __syncthreads();
+    c = sh[0];
+    for (int i = 1; i < kCThreads / 64; ++i)
+        if (cbetter(sh[i], c)) c = sh[i];
+    return c;
+}
+
+__global__ void k_crrlu_init(CState* st, int64_t* rowperm, int64_t* colperm, int m, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        st->np = 0;
+        st->done = 0;
+        st->nan = 0;
+        st->maxerror = 0.0;
+        st->err = NAN;
+    }
+    if (i < m) rowperm[i] = i;  // 0-based here; the ABI returns them 1-based
+    if (i < n) colperm[i] = i;
+}
+
+__global__ __launch_bounds__(kCThreads) void k_crrlu_step(CStepArgs g) {
+    __shared__ double2 xs[kCTR];
+    __shared__ double2 ys[kCTC];
+    __shared__ CCand red[kCThreads / 64];
+    CState* st = g.st;
+    if (st->done) return;  // set by an earlier launch only
+    const int t = g.t;
+    const int tiles_r = g.tiles_r;
+    const int tr = blockIdx.x % tiles_r, tc = blockIdx.x / tiles_r;
+    const int r0 = t + tr * kCTR, c0 = t + tc * kCTC;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double2* A = g.A;
+    const int64_t ld = g.ld;
+
+    // (1) rank-1 update of pivot k = t - 1 from the published buffers
+    if (t > 0) {
+        const int k = t - 1;
+        const double2 piv = st->piv;
+        if (threadIdx.x < kCTR) {
+            const int i = r0 + threadIdx.x;
+            if (i < g.m) {
+                double2 x = g.colbuf[i];
+                if (g.leftorth) {
+                    x = jl_cdiv(x, piv);
+                    if (tc == 0) A[i + (int64_t)k * ld] = x;  // A[k+1:end, k] ./= A[k, k]
+                }
+                xs[threadIdx.x] = x;
+            }
+        } else if (threadIdx.x < kCTR + kCTC) {
+            const int j = c0 + threadIdx.x - kCTR;
+            if (j < g.n) {
+                double2 y = g.rowbuf[j];
+                if (!g.leftorth) {
+                    y = jl_cdiv(y, piv);
+                    if (tr == 0) A[k + (int64_t)j * ld] = y;  // A[k, k+1:end] ./= A[k, k]
+                }
+                ys[threadIdx.x - kCTR] = y;
+            }
+        }
+        __syncthreads();
+    }
+    CCand best{-INFINITY, INT32_MAX, INT32_MAX};
+    const int i = r0 + lane;
+    if (i < g.m) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int jl = w * 4 + cc;
+            const int j = c0 + jl;
+            if (j >= g.n) break;
+            double2* pa = A + i + (int64_t)j * ld;
+            double2 a = *pa;
+            if (t > 0) {
+                const double2 z = cmul(xs[lane], ys[jl]);
+                a.x = a.x - z.x;
+                a.y = a.y - z.y;
+                *pa = a;
+            }
+            const double v = a.x * a.x + a.y * a.y;
+            if (v > best.v) best = CCand{v, j, i};  // columns ascend: strict '>' keeps the first
+        }
+    }
+    if (t < g.mr) {
+        best = block_reduce(best, red);
+        if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
+    }
+}
+
+// (3) one workgroup (a launch of its own, so every store of the step above is visible):
+// reduce the candidates, stop test, swap, publish the new pivot column / row
+__global__ __launch_bounds__(kCThreads) void k_crrlu_select(CStepArgs g, int ncand) {
+    __shared__ CCand red[kCThreads / 64];
+    __shared__ int stop;
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t;
+    double2* A = g.A;
+    const int64_t ld = g.ld;
+    CCand c{-INFINITY, INT32_MAX, INT32_MAX};
+    for (int b = threadIdx.x; b < ncand; b += kCThreads) {
+        const CCand o = g.cand[b];
+        if (cbetter(o, c)) c = o;
+    }
+    c = block_reduce(c, red);
+    const int p = c.col == INT32_MAX ? t : c.row;
+    const int q = c.col == INT32_MAX ? t : c.col;
+    if (threadIdx.x == 0) {
+        const double2 a = A[p + (int64_t)q * ld];
+        const double err = jl_hypot(a.x, a.y);  // lu.error = abs(A[p, q])
+        st->err = err;
+        stop = (err < g.reltol * st->maxerror || err < g.abstol) && t > 0;
+        if (stop) {
+            st->done = 1;
+        } else {
+            st->maxerror = jl_maxd(st->maxerror, err);
+            st->np = t + 1;
+            int64_t tmp = g.rowperm[t]; g.rowperm[t] = g.rowperm[p]; g.rowperm[p] = tmp;
+            tmp = g.colperm[t]; g.colperm[t] = g.colperm[q]; g.colperm[q] = tmp;
+        }
+    }
+    __syncthreads();
+    if (stop) return;
+    // swaprow!(t, p) and swapcol!(t, q) over disjoint element sets; the 2x2 corner
+    // {t,p} x {t,q} by one thread: new[a, b] = old[sr(a), sc(b)]
+    for (int j = threadIdx.x; j < g.n; j += kCThreads) {
+        if (j == t || j == q) continue;
+        double2* pt = A + t + (int64_t)j * ld;
+        double2* pp = A + p + (int64_t)j * ld;
+        const double2 at = *pt, ap = *pp;
+        *pt = ap;
+        *pp = at;
+        g.rowbuf[j] = ap;
+    }
+    for (int r = threadIdx.x; r < g.m; r += kCThreads) {
+        if (r == t || r == p) continue;
+        double2* pt = A + r + (int64_t)t * ld;
+        double2* pq = A + r + (int64_t)q * ld;
+        const double2 at = *pt, aq = *pq;
+        *pt = aq;
+        *pq = at;
+        g.colbuf[r] = aq;
+    }
+    if (threadIdx.x == 0) {
+        const double2 o_tt = A[t + (int64_t)t * ld], o_tq = A[t + (int64_t)q * ld];
+        const double2 o_pt = A[p + (int64_t)t * ld], o_pq = A[p + (int64_t)q * ld];
+        A[t + (int64_t)t * ld] = o_pq;
+        A[t + (int64_t)q * ld] = o_pt;
+        A[p + (int64_t)t * ld] = o_tq;
+        A[p + (int64_t)q * ld] = o_tt;
+        // re-read: with p == t or q == t the four stores alias and the last one wins consistently
+        const double2 n_tt = A[t + (int64_t)t * ld];
+        g.rowbuf[t] = n_tt;
+        g.rowbuf[q] = A[t + (int64_t)q * ld];
+        g.colbuf[t] = n_tt;
+        g.colbuf[p] = A[p + (int64_t)t * ld];
+        st->piv = n_tt;
+    }
+}
+
+// L = tril(A[:, 1:np]), U = triu(A[1:np, :]), NaN flags (1: L, 2: U) before the unit diagonal
+// is set, pivot errors abs.(diag) (matrixlu.jl:372-388, 799)
+__global__ void k_crrlu_extract(const double2* A, int64_t ld, int m, int n, int np, int leftorth,
+                                double2* L, double2* U, int64_t ldu, double* pe, int* nanflag) {
+    const int64_t nl = (int64_t)m * np, nu = (int64_t)np * n;
+    int flag = 0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nl + nu;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nl) {
+            const int r = (int)(e % m), c = (int)(e / m);
+            double2 a = r >= c ? A[r + (int64_t)c * ld] : make_double2(0.0, 0.0);
+            if (isnan(a.x) || isnan(a.y)) flag |= 1;
+            if (r == c && leftorth) a = make_double2(1.0, 0.0);
+            if (L) L[e] = a;
+            if (r == c && pe) pe[c] = jl_hypot(A[r + (int64_t)c * ld].x, A[r + (int64_t)c * ld].y);
+        } else {
+            const int64_t f = e - nl;
+            const int r = (int)(f % np), c = (int)(f / np);
+            double2 a = r <= c ? A[r + (int64_t)c * ld] : make_double2(0.0, 0.0);
+            if (isnan(a.x) || isnan(a.y)) flag |= 2;
+            if (r == c && !leftorth) a = make_double2(1.0, 0.0);
+            if (U) U[r + (int64_t)c * ldu] = a;
+        }
+    }
+    if (flag) atomicOr(nanflag, flag);
+}
+
+}  // namespace
+
+int crrlu_grid(int m, int n, int t) {
+    const int tr = m - t > 0 ? (m - t + kCTR - 1) / kCTR : 1;
+    const int tc = n - t > 0 ? (n - t + kCTC - 1) / kCTC : 1;
+    return tr * tc;
+}
+
+void launch_crrlu_init(hipStream_t s, CState* st, int64_t* rowperm, int64_t* colperm, int m,
+                       int n) {
+    const int N = m > n ? m : n;
+    k_crrlu_init<<<(N + 255) / 256 + 1, 256, 0, s>>>(st, rowperm, colperm, m, n);
+}
+
+void launch_crrlu_step(hipStream_t s, CStepArgs g) {
+    g.tiles_r = g.m - g.t > 0 ? (g.m - g.t + kCTR - 1) / kCTR : 1;
+    const int grid = crrlu_grid(g.m, g.n, g.t);
+    k_crrlu_step<<<grid, kCThreads, 0, s>>>(g);
+    if (g.t < g.mr) k_crrlu_select<<<1, kCThreads, 0, s>>>(g, grid);
+}
+
+void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, int n, int np,
+                          int leftorth, double2* L, double2* U, int64_t ldu, double* pe,
+                          int* nanflag) {
+    const int64_t tot = (int64_t)m * np + (int64_t)np * n;
+    int grid = (int)((tot + 255) / 256);
+    if (grid < 1) grid = 1;
+    if (grid > 4096) grid = 4096;
+    k_crrlu_extract<<<grid, 256, 0, s>>>(A, ld, m, n, np, leftorth, L, U, ldu, pe, nanflag);
+}
+
+}  // namespace tci

@@ -47,8 +47,11 @@ class rrLU:
 
 
 def rrlu(A, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True, ctx=None):
-    """rrlu(A; maxrank, reltol, abstol, leftorthogonal) (matrixlu.jl:455-463). A is not modified."""
+    """rrlu(A; maxrank, reltol, abstol, leftorthogonal) (matrixlu.jl:455-463). A is not modified.
+    Float64 and ComplexF64 (complex128) matrices, like the reference's rrLU{T}."""
     ctx = ctx or _lib.context()
+    if np.iscomplexobj(A):
+        return _rrlu_c128(A, maxrank, reltol, abstol, leftorthogonal, ctx)
     A = np.asarray(A, dtype=np.float64)
     if A.ndim != 2:
         raise ValueError("A must be a matrix")
@@ -70,6 +73,33 @@ def rrlu(A, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True, ct
     # U was written with leading dimension max(mr, 1)
     Um = U[: max(mr, 1) * n].reshape((max(mr, 1), n), order="F")[:k, :].copy()
     return rrLU(rowperm[:m].copy(), colperm[:n].copy(), Lm, Um, leftorthogonal, k, err.value)
+
+
+def _rrlu_c128(A, maxrank, reltol, abstol, leftorthogonal, ctx):
+    """rrLU{ComplexF64}: tci_rrlu_c128_h (interleaved re/im, Julia's ComplexF64 layout)."""
+    A = np.asarray(A, dtype=np.complex128)
+    if A.ndim != 2:
+        raise ValueError("A must be a matrix")
+    m, n = A.shape
+    Af = np.asfortranarray(A)
+    mr = int(max(min(int(maxrank), m, n), 0))
+    rowperm = np.zeros(max(m, 1), np.int64)
+    colperm = np.zeros(max(n, 1), np.int64)
+    L = np.zeros(max(m * mr, 1), np.complex128)
+    U = np.zeros(max(mr, 1) * max(n, 1), np.complex128)
+    pe = np.zeros(mr + 1)
+    npv = C.c_int64()
+    err = C.c_double()
+    ctx.check(ctx.lib.tci_rrlu_c128_h(ctx.h, _lib.ptr(Af), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
+                                      float(reltol), float(abstol), int(bool(leftorthogonal)),
+                                      _lib.ptr(rowperm), _lib.ptr(colperm), _lib.ptr(L), _lib.ptr(U),
+                                      max(mr, 1), C.byref(npv), C.byref(err), _lib.ptr(pe)))
+    k = npv.value
+    Lm = L[: m * k].reshape((m, k), order="F").copy()
+    Um = U[: max(mr, 1) * n].reshape((max(mr, 1), n), order="F")[:k, :].copy()
+    lu = rrLU(rowperm[:m].copy(), colperm[:n].copy(), Lm, Um, leftorthogonal, k, err.value)
+    lu.device_pivoterrors = pe[: k + 1].copy()
+    return lu
 
 
 def rrlu_(A, **kw):
@@ -118,7 +148,11 @@ def npivots(lu):
 
 
 def pivoterrors(lu):
-    """pivoterrors(lu) (matrixlu.jl:799-801): [abs.(diag(lu)); lu.error]."""
+    """pivoterrors(lu) (matrixlu.jl:799-801): [abs.(diag(lu)); lu.error]. For ComplexF64 the
+    device computes abs (Julia's hypot) next to the factorisation."""
+    pe = getattr(lu, "device_pivoterrors", None)
+    if pe is not None:
+        return pe.copy()
     return np.concatenate([np.abs(diag(lu)), [lu.error]])
 
 

@@ -75,6 +75,12 @@ def lib():
         L.orc_tci_bonderrors.argtypes = [C.c_void_p, f64p]
         L.orc_tci_sitetensor.argtypes = [C.c_void_p, C.c_int, f64p]
         L.orc_tci_evaluate.argtypes = [C.c_void_p, i32p, C.POINTER(C.c_double)]
+        L.orc_rrlu_c128.argtypes = [f64p, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double,
+                                    C.c_int, i64p, i64p, f64p, f64p, C.POINTER(C.c_int64),
+                                    C.POINTER(C.c_double), f64p]
+        L.orc_cdiv.argtypes = [C.c_double] * 4 + [C.POINTER(C.c_double)] * 2
+        L.orc_hypot.argtypes = [C.c_double, C.c_double]
+        L.orc_hypot.restype = C.c_double
         _lib = L
     return _lib
 
@@ -100,6 +106,41 @@ def submatrixargmax(A, rows, cols, f="abs2"):
     _check(lib().orc_submatrixargmax(flat, A.shape[0], A.shape[0], A.shape[1], r, len(r), c, len(c),
                                      1 if f == "abs2" else 0, C.byref(mr), C.byref(mc)))
     return mr.value, mc.value
+
+
+def cdiv(z, w):
+    """Julia's ComplexF64 `/` as restated in the oracle (Baudin-Smith robust division)."""
+    re, im = C.c_double(), C.c_double()
+    lib().orc_cdiv(z.real, z.imag, w.real, w.imag, C.byref(re), C.byref(im))
+    return complex(re.value, im.value)
+
+
+class OracleLUc:
+    """rrlu(A::Matrix{ComplexF64}) restatement (matrixlu.jl:346-396 on complex entries)."""
+
+    def __init__(self, A, maxrank=None, reltol=1e-14, abstol=0.0, leftorthogonal=True):
+        A = np.asarray(A, dtype=np.complex128)
+        m, n = A.shape
+        maxrank = min(m, n) if maxrank is None else int(maxrank)
+        mr = max(min(maxrank, m, n), 0)
+        flat = np.ascontiguousarray(A.ravel(order="F")).view(np.float64)
+        rp = np.zeros(max(m, 1), np.int64)
+        cp = np.zeros(max(n, 1), np.int64)
+        L = np.zeros(max(m * mr, 1), np.complex128)
+        U = np.zeros(max(mr * n, 1), np.complex128)
+        pe = np.zeros(mr + 1)
+        npv, err = C.c_int64(), C.c_double()
+        _check(lib().orc_rrlu_c128(flat, m, n, maxrank, reltol, abstol, int(leftorthogonal), rp, cp,
+                                   L.view(np.float64), U.view(np.float64), C.byref(npv),
+                                   C.byref(err), pe))
+        k = npv.value
+        self.m, self.n, self.npivot, self.error = m, n, k, err.value
+        self.leftorthogonal = leftorthogonal
+        self.rowpermutation = rp[:m].copy()
+        self.colpermutation = cp[:n].copy()
+        self.L = L[: m * k].reshape((m, k), order="F")
+        self.U = U[: k * n].reshape((k, n), order="F")
+        self.pivoterrors = pe[: k + 1].copy()
 
 
 class OracleLU:

@@ -1,0 +1,118 @@
+"""GPU parity of the ComplexF64 rrLU (tci_rrlu_c128_h, tci_rrlu_c128.hip) with the CPU oracle
+(orc_rrlu_c128): bit-exact permutations, L, U, npivot, lu.error and pivot errors -- the device
+restates Julia's complex division / abs exactly like the oracle, and the update keeps the
+reference's multiply-then-subtract (matrixlu.jl:318)."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+T = pytest.importorskip("tci_amd")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+def assert_c_bitwise(lu, ref):
+    assert lu.npivot == ref.npivot
+    assert np.array_equal(lu.rowpermutation - 1, ref.rowpermutation)
+    assert np.array_equal(lu.colpermutation - 1, ref.colpermutation)
+    assert np.array_equal(lu.L, ref.L)
+    assert np.array_equal(lu.U, ref.U)
+    assert (lu.error == ref.error) or (np.isnan(lu.error) and np.isnan(ref.error))
+    pe = T.pivoterrors(lu)
+    assert np.array_equal(pe[:-1], ref.pivoterrors[:-1])
+
+
+def crand(rng, m, n):
+    return rng.random((m, n)) - 0.5 + 1j * (rng.random((m, n)) - 0.5)
+
+
+@pytest.mark.parametrize("shape,kw", [
+    ((7, 5), {}),
+    ((30, 40), {}),
+    ((100, 80), {"maxrank": 20}),
+    ((257, 300), {"maxrank": 64}),
+    ((65, 17), {"reltol": 1e-3}),
+    ((1, 9), {}),
+    ((9, 1), {}),
+])
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_crrlu_random_bitwise(ctx, shape, kw, leftorth):
+    A = crand(np.random.default_rng(shape[0] * 7 + shape[1]), *shape)
+    lu = T.rrlu(A, leftorthogonal=leftorth, ctx=ctx, **kw)
+    ref = O.OracleLUc(A, leftorthogonal=leftorth, **kw)
+    assert_c_bitwise(lu, ref)
+
+
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_crrlu_lorentz_ties_bitwise(ctx, leftorth):
+    # Pi of the complex Lorentzian coeff / (1 + sum v^2) (test_tensorci2.jl:246-249): values
+    # depend on sum v^2 only -> many exact abs2 ties, resolved in column-major order
+    d = 6
+    I = np.array(list(np.ndindex(d, d))) + 1
+    J = np.array(list(np.ndindex(d, d))) + 1
+    s = (I ** 2).sum(1)[:, None] + (J ** 2).sum(1)[None, :]
+    A = (0.5 - 1.0j) / (s + 1.0)
+    for kw in ({}, {"maxrank": 5}, {"reltol": 1e-8}):
+        lu = T.rrlu(A, leftorthogonal=leftorth, ctx=ctx, **kw)
+        ref = O.OracleLUc(A, leftorthogonal=leftorth, **kw)
+        assert_c_bitwise(lu, ref)
+
+
+def test_crrlu_rank_deficient_and_abstol(ctx):
+    rng = np.random.default_rng(3)
+    B = crand(rng, 120, 4) @ crand(rng, 4, 90)
+    for kw in ({"reltol": 1e-12}, {"abstol": 1e-3}, {"reltol": 0.0, "abstol": 0.0}):
+        lu = T.rrlu(B, ctx=ctx, **kw)
+        ref = O.OracleLUc(B, **kw)
+        assert_c_bitwise(lu, ref)
+    assert T.rrlu(B, reltol=1e-12, ctx=ctx).npivot == 4
+
+
+def test_crrlu_argmax_kat(kats, ctx):
+    k = kats["argmax_complex_3x6"]
+    Z = np.array(k["re"], float) + 1j * np.array(k["im"], float)
+    lu = T.rrlu(Z, maxrank=1, ctx=ctx)
+    flat = (np.abs(Z) ** 2).ravel(order="F")
+    i = int(np.argmax(flat))
+    assert (lu.rowpermutation[0], lu.colpermutation[0]) == (i % 3 + 1, i // 3 + 1)
+
+
+def test_crrlu_nan_and_empty(ctx):
+    A = np.ones((4, 4), complex) + np.eye(4)
+    A[2, 0] = complex(np.nan, 0)
+    with pytest.raises(O.OracleError, match="lu.L contains NaNs"):
+        O.OracleLUc(A)
+    with pytest.raises(T.TCIError, match="lu.L contains NaNs"):
+        T.rrlu(A, ctx=ctx)
+    lu = T.rrlu(np.zeros((0, 5), complex), ctx=ctx)
+    assert lu.npivot == 0 and lu.error == 0.0
+    # an all-zero matrix: 0/0 in the normalisation -> NaN in L, like the Float64 reference
+    Z = np.zeros((6, 4), complex)
+    with pytest.raises(O.OracleError, match="lu.L contains NaNs"):
+        O.OracleLUc(Z)
+    with pytest.raises(T.TCIError, match="lu.L contains NaNs"):
+        T.rrlu(Z, ctx=ctx)
+    # one row: no normalisation below the pivot, rank 1
+    r = np.array([[0.0, 2.0 - 1.0j, 0.5j]])
+    assert_c_bitwise(T.rrlu(r, ctx=ctx), O.OracleLUc(r))
+
+
+def test_crrlu_large_identity(ctx):
+    # a size with many workgroups per step; the oracle checks the first pivots bitwise and the
+    # factorisation identity covers the rest
+    rng = np.random.default_rng(11)
+    A = crand(rng, 1500, 1300)
+    lu = T.rrlu(A, maxrank=48, ctx=ctx)
+    ref = O.OracleLUc(A, maxrank=48)
+    assert_c_bitwise(lu, ref)
+    P = A[lu.rowpermutation - 1][:, lu.colpermutation - 1]
+    k = lu.npivot
+    np.testing.assert_allclose(lu.L[:k] @ lu.U[:, :k], P[:k, :k], rtol=0, atol=1e-12)
