@@ -118,6 +118,7 @@ struct CState {
     double maxerror;
     double err;
     double2 piv;
+    int32_t p, q;  // accepted pivot (physical row / column)
 };
 struct CStepArgs {
     double2* A;

@@ -3,17 +3,17 @@
 // rrlu(A::Matrix{ComplexF64}) runs the same _optimizerrlu! / addpivot! loop as the Float64 path
 // (matrixlu.jl:295-322, 346-396); SURVEY §8f rank 4. Entries are double2 (re, im) column-major,
 // Julia's ComplexF64 layout. Unlike the Float64 kernels (logical swaps, deferred updates,
-// certified fp32 shadow search) this path keeps the reference's physical row/column swaps: one
-// launch per pivot, each doing
+// certified fp32 shadow search) this path keeps the reference's physical row/column swaps; per
+// pivot:
 //   (1) the rank-1 update of pivot t-1 (normalised column/row from the published pivot
 //       column/row buffers, so no workgroup reads what another writes), complex multiply then
 //       subtract componentwise (matrixlu.jl:318; no fma: -ffp-contract=off),
 //   (2) the argmax of abs2 over the trailing block for pivot t (strict '>' in column-major order
 //       -> ties to the smallest column, then row; NaN never wins; matrixlu.jl:46-87),
-//   (3) in a one-workgroup launch of its own (no cross-XCD hand-off inside a kernel): the
-//       candidates' reduction, the stop test (matrixlu.jl:360-365), the row/column swap over the
-//       whole matrix (swaprow!/swapcol!, matrixlu.jl:254-275) and the publication of the new
-//       pivot column/row.
+//   (3) in launches of their own (no cross-XCD hand-off inside a kernel): the candidates'
+//       reduction and stop test (matrixlu.jl:360-365) in one 1024-thread workgroup, then the
+//       row/column swap over the whole matrix (swaprow!/swapcol!, matrixlu.jl:254-275), one
+//       thread per row / column, publishing the new pivot column / row.
 // Per pivot that is one read+write of the trailing block (32 B/element) -- HBM-bound like the
 // Float64 rank-1 update (2x the bytes of the real case; 8 flops/element).
 // Julia Base arithmetic restated: ComplexF64 `/` is Baudin & Smith's robust division and
@@ -29,8 +29,10 @@ namespace tci {
 namespace {
 
 constexpr int kCTR = 64;      // rows per tile (one wave lane per row)
-constexpr int kCTC = 16;      // columns per tile (4 waves x 4 columns)
+constexpr int kCTC = 32;      // columns per tile (4 waves x 8 columns)
 constexpr int kCThreads = 256;
+constexpr int kCW = kCTC / (kCThreads / 64);  // columns per wave
+constexpr int kRThreads = 1024;               // candidate reduction
 
 __device__ inline bool cbetter(const CCand& b, const CCand& a) {
     return b.v > a.v || (b.v == a.v && (b.col < a.col || (b.col == a.col && b.row < a.row)));
@@ -109,6 +111,7 @@ __device__ inline CCand shfl_cand(const CCand& c, int mask) {
 }
 
 // block-wide argmax; the result is valid in every thread
+template <int NT>
 __device__ CCand block_reduce(CCand c, CCand* sh) {
     for (int mask = 32; mask >= 1; mask >>= 1) {
         CCand o = shfl_cand(c, mask);
@@ -119,7 +122,7 @@ __device__ CCand block_reduce(CCand c, CCand* sh) {
     if ((threadIdx.x & 63) == 0) sh[w] = c;
     __syncthreads();
     c = sh[0];
-    for (int i = 1; i < kCThreads / 64; ++i)
+    for (int i = 1; i < NT / 64; ++i)
         if (cbetter(sh[i], c)) c = sh[i];
     return c;
 }
@@ -182,8 +185,8 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step(CStepArgs g) {
     const int i = r0 + lane;
     if (i < g.m) {
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int jl = w * 4 + cc;
+        for (int cc = 0; cc < kCW; ++cc) {
+            const int jl = w * kCW + cc;
             const int j = c0 + jl;
             if (j >= g.n) break;
             double2* pa = A + i + (int64_t)j * ld;
@@ -199,66 +202,81 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step(CStepArgs g) {
         }
     }
     if (t < g.mr) {
-        best = block_reduce(best, red);
+        best = block_reduce<kCThreads>(best, red);
         if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
     }
 }
 
-// (3) one workgroup (a launch of its own, so every store of the step above is visible):
-// reduce the candidates, stop test, swap, publish the new pivot column / row
-__global__ __launch_bounds__(kCThreads) void k_crrlu_select(CStepArgs g, int ncand) {
-    __shared__ CCand red[kCThreads / 64];
-    __shared__ int stop;
+// (3a) one workgroup (a launch of its own, so every store of the step is visible): reduce the
+// candidates, stop test (matrixlu.jl:360-365), permutation swap; the winner goes to st->p/q
+__global__ __launch_bounds__(kRThreads) void k_crrlu_reduce(CStepArgs g, int ncand) {
+    __shared__ CCand red[kRThreads / 64];
     CState* st = g.st;
     if (st->done) return;
     const int t = g.t;
-    double2* A = g.A;
-    const int64_t ld = g.ld;
     CCand c{-INFINITY, INT32_MAX, INT32_MAX};
-    for (int b = threadIdx.x; b < ncand; b += kCThreads) {
+    int b = threadIdx.x;
+    for (; b + 7 * kRThreads < ncand; b += 8 * kRThreads) {  // 8 independent loads in flight
+        CCand o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = g.cand[b + u * kRThreads];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (cbetter(o[u], c)) c = o[u];
+    }
+    for (; b < ncand; b += kRThreads) {
         const CCand o = g.cand[b];
         if (cbetter(o, c)) c = o;
     }
-    c = block_reduce(c, red);
-    const int p = c.col == INT32_MAX ? t : c.row;
-    const int q = c.col == INT32_MAX ? t : c.col;
+    c = block_reduce<kRThreads>(c, red);  // (v, col, row) is a total order: any order reduces
     if (threadIdx.x == 0) {
-        const double2 a = A[p + (int64_t)q * ld];
+        const int p = c.col == INT32_MAX ? t : c.row;  // nothing beat -Inf (all NaN): (k, k)
+        const int q = c.col == INT32_MAX ? t : c.col;
+        const double2 a = g.A[p + (int64_t)q * g.ld];
         const double err = jl_hypot(a.x, a.y);  // lu.error = abs(A[p, q])
         st->err = err;
-        stop = (err < g.reltol * st->maxerror || err < g.abstol) && t > 0;
-        if (stop) {
+        if ((err < g.reltol * st->maxerror || err < g.abstol) && t > 0) {
             st->done = 1;
         } else {
             st->maxerror = jl_maxd(st->maxerror, err);
             st->np = t + 1;
+            st->p = p;
+            st->q = q;
             int64_t tmp = g.rowperm[t]; g.rowperm[t] = g.rowperm[p]; g.rowperm[p] = tmp;
             tmp = g.colperm[t]; g.colperm[t] = g.colperm[q]; g.colperm[q] = tmp;
         }
     }
-    __syncthreads();
-    if (stop) return;
-    // swaprow!(t, p) and swapcol!(t, q) over disjoint element sets; the 2x2 corner
-    // {t,p} x {t,q} by one thread: new[a, b] = old[sr(a), sc(b)]
-    for (int j = threadIdx.x; j < g.n; j += kCThreads) {
-        if (j == t || j == q) continue;
+}
+
+// (3b) swaprow!(t, p) and swapcol!(t, q) (matrixlu.jl:254-275) over disjoint element sets, one
+// thread per column (row swap), per row (column swap) and one for the 2x2 corner
+// {t,p} x {t,q}: new[a, b] = old[sr(a), sc(b)]; publishes the new pivot column / row
+__global__ void k_crrlu_swap(CStepArgs g) {
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t, p = st->p, q = st->q;
+    double2* A = g.A;
+    const int64_t ld = g.ld;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < g.n) {
+        const int j = e;
+        if (j == t || j == q) return;
         double2* pt = A + t + (int64_t)j * ld;
         double2* pp = A + p + (int64_t)j * ld;
         const double2 at = *pt, ap = *pp;
         *pt = ap;
         *pp = at;
         g.rowbuf[j] = ap;
-    }
-    for (int r = threadIdx.x; r < g.m; r += kCThreads) {
-        if (r == t || r == p) continue;
+    } else if (e < g.n + g.m) {
+        const int r = e - g.n;
+        if (r == t || r == p) return;
         double2* pt = A + r + (int64_t)t * ld;
         double2* pq = A + r + (int64_t)q * ld;
         const double2 at = *pt, aq = *pq;
         *pt = aq;
         *pq = at;
         g.colbuf[r] = aq;
-    }
-    if (threadIdx.x == 0) {
+    } else if (e == g.n + g.m) {
         const double2 o_tt = A[t + (int64_t)t * ld], o_tq = A[t + (int64_t)q * ld];
         const double2 o_pt = A[p + (int64_t)t * ld], o_pq = A[p + (int64_t)q * ld];
         A[t + (int64_t)t * ld] = o_pq;
@@ -320,7 +338,10 @@ void launch_crrlu_step(hipStream_t s, CStepArgs g) {
     g.tiles_r = g.m - g.t > 0 ? (g.m - g.t + kCTR - 1) / kCTR : 1;
     const int grid = crrlu_grid(g.m, g.n, g.t);
     k_crrlu_step<<<grid, kCThreads, 0, s>>>(g);
-    if (g.t < g.mr) k_crrlu_select<<<1, kCThreads, 0, s>>>(g, grid);
+    if (g.t < g.mr) {
+        k_crrlu_reduce<<<1, kRThreads, 0, s>>>(g, grid);
+        k_crrlu_swap<<<(g.m + g.n + 256) / 256, 256, 0, s>>>(g);
+    }
 }
 
 void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, int n, int np,
