@@ -382,6 +382,29 @@ def extras(T, ctx):
                                  "pi_rows_per_s_device": round(m / (kms / kn * 1e-3), 1),
                                  "TFLOPs_env_plus_gemm": round((env_flops + 2.0 * m * n * chi * chi)
                                                                / (kms / kn * 1e-3) / 1e12, 2)}
+    # ComplexF64 rrLU (K8): 8192^2 r = 256, device-resident, U[0,1) re and im
+    mc = nc = 8192
+    rc = 256
+    Ac = T.DeviceMatrix(2 * mc, nc, ctx=ctx)  # interleaved (re, im): complex ld = Ac.ld / 2
+    Ac.fill_uniform(seed=0)
+    Wc = T.DeviceMatrix(2 * mc, nc, ctx=ctx)
+    npv, errc = C.c_int64(), C.c_double()
+    walls = []
+    for rep in range(3):
+        Wc.copy_from(Ac)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.check(ctx.lib.tci_rrlu_c128_inplace_d(ctx.h, Wc.ptr, mc, nc, Wc.ld // 2, rc, 1e-14, 0.0, 1,
+                                                  None, None, C.byref(npv), C.byref(errc), None))
+        walls.append(time.perf_counter() - t0)
+    Ac.free()
+    Wc.free()
+    kk = np.arange(1, npv.value + 1, dtype=np.float64)
+    elc = float(((mc - kk) * (nc - kk)).sum())
+    tc = min(walls[1:])
+    res["rrlu_c128"] = {"m": mc, "n": nc, "r": int(npv.value), "ms": round(tc * 1e3, 2),
+                        "complex_GFLOPs": round(8 * elc / tc / 1e9, 1),
+                        "algorithmic_GBps": round(32 * elc / tc / 1e9, 1)}
     # other rrLU configurations of SURVEY 8(d): config 2 (4096^2), right-orthogonal pivots, and a
     # 16384^2 matrix (2 GiB) for the scale curve
     res["rrlu_configs"] = []

@@ -146,6 +146,14 @@ int tci_rrlu_c128_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t
                     int64_t* colperm, double* L, double* U, int64_t ldu, int64_t* npivot,
                     double* lasterror, double* pivoterrors);
 
+/* rrlu! of a ComplexF64 device matrix (interleaved, ld lda >= m, 16-byte aligned), clobbered as
+ * the work matrix; permutations (NULL to skip), npivot, lu.error and the np + 1 pivot errors
+ * (NULL to skip) to the host, with the NaN checks of matrixlu.jl:376-381. */
+int tci_rrlu_c128_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
+                            int64_t maxrank, double reltol, double abstol, int leftorth,
+                            int64_t* rowperm, int64_t* colperm, int64_t* npivot,
+                            double* lasterror, double* pivoterrors);
+
 /* ------------------------------------------------------------ MatrixLUCI
  * Replaces MatrixLUCI(A; kw...) + left/right/pivoterrors (matrixluci.jl:55-57, 161-311):
  * leftorth: left = colstimespivotinv (TRSM), right = rowmatrix (GEMM);

@@ -810,18 +810,11 @@ int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
     return TCI_OK;
 }
 
-int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
-                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
-                    int64_t* colperm, double* L, double* U, int64_t ldu, int64_t* npivot,
-                    double* lasterror, double* pivoterrors) {
-    if (!c || !npivot || !lasterror || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
-    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
-        return set_err(c, TCI_ERR_ARG, "rrlu: invalid dimensions");
-    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
-    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
-    if (mr < 0) mr = 0;
-    if (U && ldu < std::max<int64_t>(mr, 1)) return set_err(c, TCI_ERR_ARG, "rrlu: ldu < maxrank");
-    const int64_t ld = std::max<int64_t>(m, 1);
+// ComplexF64 rrLU on a device matrix (double2, ld >= m): steps, then np / lu.error to the host;
+// the pivot column buffer holds the pivot errors afterwards when want_pe
+static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t n, int64_t mr,
+                        double reltol, double abstol, int leftorth, int64_t* np_out,
+                        double* err_out, tci::CState** st_out, double2** colbuf_out) {
     const int mi = (int)m, ni = (int)n;
     const int G = tci::crrlu_grid(mi, ni, 0);
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -830,18 +823,11 @@ int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
     const size_t bytes = oRow + al(16 * (size_t)std::max(ni, 1));
     int st;
     if ((st = ensure(c, &c->cws, &c->capCws, bytes))) return st;
-    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
-    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * mr, 1))))) return st;
-    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(mr * n, 1))))) return st;
     tci::CState* dst = reinterpret_cast<tci::CState*>(c->cws + oSt);
     tci::launch_crrlu_init(c->stream, dst, c->rowperm, c->colperm, mi, ni);
     HIPCHK(c, hipGetLastError());
-    double2* dA = reinterpret_cast<double2*>(c->dA);
-    if (m > 0 && n > 0)
-        HIPCHK(c, hipMemcpy2DAsync(dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
-                                   c->stream));
     tci::CStepArgs g{};
     g.A = dA;
     g.ld = ld;
@@ -866,21 +852,60 @@ int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
     tci::CState hs;
     HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int64_t np = hs.np;
+    *np_out = hs.np;
+    *err_out = hs.np >= std::min(m, n) ? 0.0 : hs.err;
+    *st_out = dst;
+    *colbuf_out = g.colbuf;
+    return TCI_OK;
+}
+
+// L / U extraction with the NaN checks of matrixlu.jl:376-381 (pivot errors into pe)
+static int crrlu_extract(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t n, int64_t np,
+                         int leftorth, double2* dL, double2* dU, double* pe, tci::CState* dst) {
+    if (np <= 0) return TCI_OK;
+    tci::launch_crrlu_extract(c->stream, dA, ld, (int)m, (int)n, (int)np, leftorth, dL, dU, np, pe,
+                              &dst->nan);
+    HIPCHK(c, hipGetLastError());
+    tci::CState hs;
+    HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (hs.nan & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+    if (hs.nan & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    return TCI_OK;
+}
+
+int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
+                    int64_t* colperm, double* L, double* U, int64_t ldu, int64_t* npivot,
+                    double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
+        return set_err(c, TCI_ERR_ARG, "rrlu: invalid dimensions");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    if (U && ldu < std::max<int64_t>(mr, 1)) return set_err(c, TCI_ERR_ARG, "rrlu: ldu < maxrank");
+    const int64_t ld = std::max<int64_t>(m, 1);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * mr, 1))))) return st;
+    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(mr * n, 1))))) return st;
+    double2* dA = reinterpret_cast<double2*>(c->dA);
+    if (m > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
+                                   c->stream));
+    int64_t np;
+    double err;
+    tci::CState* dst;
+    double2* colbuf;
+    if ((st = crrlu_device(c, dA, ld, m, n, mr, reltol, abstol, leftorth, &np, &err, &dst, &colbuf)))
+        return st;
     double2* dL = reinterpret_cast<double2*>(c->dL);
     double2* dU = reinterpret_cast<double2*>(c->dU);
-    double* dpe = reinterpret_cast<double*>(g.colbuf);  // free after the last step
-    if (np > 0) {
-        tci::launch_crrlu_extract(c->stream, dA, ld, mi, ni, (int)np, leftorth, dL, dU, np, dpe,
-                                  &dst->nan);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (hs.nan & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
-        if (hs.nan & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
-    }
+    double* dpe = reinterpret_cast<double*>(colbuf);  // free after the last step
+    if ((st = crrlu_extract(c, dA, ld, m, n, np, leftorth, dL, dU, dpe, dst))) return st;
     *npivot = np;
-    *lasterror = np >= std::min(m, n) ? 0.0 : hs.err;
+    *lasterror = err;
     if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
     if (np > 0 && L)
         HIPCHK(c, hipMemcpyAsync(L, dL, m * np * 16, hipMemcpyDeviceToHost, c->stream));
@@ -892,6 +917,45 @@ int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
                                  c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (pivoterrors) pivoterrors[np] = *lasterror;
+    return TCI_OK;
+}
+
+int tci_rrlu_c128_inplace_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda,
+                            int64_t maxrank, double reltol, double abstol, int leftorth,
+                            int64_t* rowperm, int64_t* colperm, int64_t* npivot,
+                            double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror || (m > 0 && n > 0 && !d_A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
+        return set_err(c, TCI_ERR_ARG, "rrlu: invalid dimensions");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    if (reinterpret_cast<uintptr_t>(d_A) % 16)
+        return set_err(c, TCI_ERR_ARG, "rrlu: device matrix must be 16-byte aligned");
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    int64_t np;
+    double err;
+    tci::CState* dst;
+    double2* colbuf;
+    double2* dA = reinterpret_cast<double2*>(d_A);
+    int st;
+    if ((st = crrlu_device(c, dA, lda, m, n, mr, reltol, abstol, leftorth, &np, &err, &dst, &colbuf)))
+        return st;
+    // NaN checks need L / U: extract into the context's buffers
+    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * np, 1))))) return st;
+    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(np * n, 1))))) return st;
+    double* dpe = reinterpret_cast<double*>(colbuf);
+    if ((st = crrlu_extract(c, dA, lda, m, n, np, leftorth, reinterpret_cast<double2*>(c->dL),
+                            reinterpret_cast<double2*>(c->dU), dpe, dst)))
+        return st;
+    *npivot = np;
+    *lasterror = err;
+    if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    if (np > 0 && pivoterrors) {
+        HIPCHK(c, hipMemcpyAsync(pivoterrors, dpe, np * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (pivoterrors) pivoterrors[np] = err;
     return TCI_OK;
 }
 

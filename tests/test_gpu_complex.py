@@ -116,3 +116,29 @@ def test_crrlu_large_identity(ctx):
     P = A[lu.rowpermutation - 1][:, lu.colpermutation - 1]
     k = lu.npivot
     np.testing.assert_allclose(lu.L[:k] @ lu.U[:, :k], P[:k, :k], rtol=0, atol=1e-12)
+
+
+def test_crrlu_inplace_device_matches_host(ctx):
+    import ctypes as C
+    rng = np.random.default_rng(21)
+    m, n = 300, 260
+    A = np.asfortranarray(crand(rng, m, n))
+    ref = O.OracleLUc(A, maxrank=40)
+    p = C.c_void_p()
+    ctx.check(ctx.lib.tci_malloc_d(ctx.h, C.byref(p), A.nbytes))
+    try:
+        ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, p, T._lib.ptr(A), A.nbytes))
+        rp = np.zeros(m, np.int64)
+        cp = np.zeros(n, np.int64)
+        pe = np.zeros(41)
+        npv, err = C.c_int64(), C.c_double()
+        ctx.check(ctx.lib.tci_rrlu_c128_inplace_d(ctx.h, p, m, n, m, 40, 1e-14, 0.0, 1, T._lib.ptr(rp),
+                                                  T._lib.ptr(cp), C.byref(npv), C.byref(err),
+                                                  T._lib.ptr(pe)))
+    finally:
+        ctx.lib.tci_free_d(ctx.h, p)
+    assert npv.value == ref.npivot
+    assert np.array_equal(rp - 1, ref.rowpermutation)
+    assert np.array_equal(cp - 1, ref.colpermutation)
+    assert err.value == ref.error
+    assert np.array_equal(pe, ref.pivoterrors)
