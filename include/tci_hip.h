@@ -164,6 +164,13 @@ int tci_luci_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda,
                double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
                double* pivoterrors, double* left, double* right, int64_t* npivot);
 
+/* MatrixLUCI{ComplexF64} (matrixluci.jl:55-57, 161-311) on top of the ComplexF64 rrLU:
+ * left m x np, right np x n, interleaved (re, im) column-major; otherwise as tci_luci_h. */
+int tci_luci_c128_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowidx,
+                    int64_t* colidx, double* pivoterrors, double* left, double* right,
+                    int64_t* npivot);
+
 /* --------------------------------------------------------- 2-site update
  * Replaces the :full branch of updatepivots! (tensorci2.jl:842-928) with Pi kept on the device:
  * Pi = f(rows x cols) -> maxabs -> rrLU -> pivot rows/cols -> (optionally) MatrixLUCI factors.

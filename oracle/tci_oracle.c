@@ -1294,3 +1294,94 @@ int orc_rrlu_c128(const double* A0, i64 m, i64 n, i64 maxrank, double reltol, do
     free(A);
     return ORC_OK;
 }
+
+/* MatrixLUCI{ComplexF64} left/right factors (matrixluci.jl:161-283) from orc_rrlu_c128's L / U,
+ * the same loops as luci_left / luci_right above on complex entries (multiply without fma,
+ * sequential sums, orc_cdiv for the divisions). left m x np, right np x n, interleaved;
+ * rowidx / colidx: the np pivot rows / columns (0-based). */
+int orc_luci_c128(const double* A, i64 m, i64 n, i64 maxrank, double reltol, double abstol,
+                  int leftorth, i64* rowidx, i64* colidx, double* pivoterrs, double* left,
+                  double* right, i64* npivot) {
+    i64 mr = maxrank < m ? maxrank : m;
+    if (mr > n) mr = n;
+    if (mr < 0) mr = 0;
+    i64* rp = (i64*)malloc(sizeof(i64) * (size_t)(m + 1));
+    i64* cp = (i64*)malloc(sizeof(i64) * (size_t)(n + 1));
+    double* L = (double*)malloc(sizeof(double) * (size_t)(2 * m * mr + 2));
+    double* U = (double*)malloc(sizeof(double) * (size_t)(2 * mr * n + 2));
+    if (!rp || !cp || !L || !U) {
+        free(rp); free(cp); free(L); free(U);
+        return fail(ORC_ERR_ALLOC, "allocation failed");
+    }
+    i64 np;
+    double err;
+    int st = orc_rrlu_c128(A, m, n, maxrank, reltol, abstol, leftorth, rp, cp, L, U, &np, &err,
+                           pivoterrs);
+    if (st) { free(rp); free(cp); free(L); free(U); return st; }
+    *npivot = np;
+    for (i64 k = 0; k < np; ++k) { rowidx[k] = rp[k]; colidx[k] = cp[k]; }
+#define LR(i, j) L[2 * ((i) + (j) * m)]
+#define LI(i, j) L[2 * ((i) + (j) * m) + 1]
+#define UR(i, j) U[2 * ((i) + (j) * np)]
+#define UI(i, j) U[2 * ((i) + (j) * np) + 1]
+    if (left) {
+        for (i64 i = 0; i < m; ++i) {
+            double* o = left + 2 * rp[i];
+            for (i64 j = np - 1; j >= 0; --j) {
+                double sr = 0.0, si = 0.0;
+                if (leftorth) {  /* [I; L21 / LowerTriangular(L11)] */
+                    if (i < np) { sr = (i == j); si = 0.0; }
+                    else {
+                        sr = LR(i, j); si = LI(i, j);
+                        for (i64 t = j + 1; t < np; ++t) {
+                            const double xr = o[2 * (t * m)], xi = o[2 * (t * m) + 1];
+                            sr = sr - (xr * LR(t, j) - xi * LI(t, j));
+                            si = si - (xr * LI(t, j) + xi * LR(t, j));
+                        }
+                        orc_cdiv(sr, si, LR(j, j), LI(j, j), &sr, &si);
+                    }
+                } else {  /* colmatrix: L * U11 */
+                    for (i64 t = 0; t < np; ++t) {
+                        sr = sr + (LR(i, t) * UR(t, j) - LI(i, t) * UI(t, j));
+                        si = si + (LR(i, t) * UI(t, j) + LI(i, t) * UR(t, j));
+                    }
+                }
+                o[2 * (j * m)] = sr;
+                o[2 * (j * m) + 1] = si;
+            }
+        }
+    }
+    if (right) {
+        for (i64 c = 0; c < n; ++c) {
+            double* o = right + 2 * np * cp[c];
+            for (i64 a = np - 1; a >= 0; --a) {
+                double sr = 0.0, si = 0.0;
+                if (!leftorth) {  /* [I, UpperTriangular(U11) \ U12] */
+                    if (c < np) { sr = (a == c); si = 0.0; }
+                    else {
+                        sr = UR(a, c); si = UI(a, c);
+                        for (i64 t = a + 1; t < np; ++t) {
+                            const double xr = o[2 * t], xi = o[2 * t + 1];
+                            sr = sr - (UR(a, t) * xr - UI(a, t) * xi);
+                            si = si - (UR(a, t) * xi + UI(a, t) * xr);
+                        }
+                        orc_cdiv(sr, si, UR(a, a), UI(a, a), &sr, &si);
+                    }
+                } else {  /* rowmatrix: L11 * U */
+                    for (i64 t = 0; t < np; ++t) {
+                        sr = sr + (LR(a, t) * UR(t, c) - LI(a, t) * UI(t, c));
+                        si = si + (LR(a, t) * UI(t, c) + LI(a, t) * UR(t, c));
+                    }
+                }
+                o[2 * a] = sr;
+                o[2 * a + 1] = si;
+            }
+        }
+    }
+#undef LR
+#undef LI
+#undef UR
+#undef UI
+    free(rp); free(cp); free(L); free(U);
+    return ORC_OK;
+}

@@ -920,6 +920,59 @@ int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
     return TCI_OK;
 }
 
+int tci_luci_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowidx,
+                    int64_t* colidx, double* pivoterrors, double* left, double* right,
+                    int64_t* npivot) {
+    if (!c || !npivot || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
+        return set_err(c, TCI_ERR_ARG, "MatrixLUCI: invalid dimensions");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    const int64_t ld = std::max<int64_t>(m, 1);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * mr, 1))))) return st;
+    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(mr * n, 1))))) return st;
+    double2* dA = reinterpret_cast<double2*>(c->dA);
+    if (m > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
+                                   c->stream));
+    int64_t np;
+    double err;
+    tci::CState* dst;
+    double2* colbuf;
+    if ((st = crrlu_device(c, dA, ld, m, n, mr, reltol, abstol, leftorth, &np, &err, &dst, &colbuf)))
+        return st;
+    double2* dL = reinterpret_cast<double2*>(c->dL);
+    double2* dU = reinterpret_cast<double2*>(c->dU);
+    double* dpe = reinterpret_cast<double*>(colbuf);
+    if ((st = crrlu_extract(c, dA, ld, m, n, np, leftorth, dL, dU, dpe, dst))) return st;
+    *npivot = np;
+    if (np > 0 && (st = fetch_perms(c, rowidx, colidx, rowidx ? np : 0, colidx ? np : 0))) return st;
+    if (np > 0 && pivoterrors) {
+        HIPCHK(c, hipMemcpyAsync(pivoterrors, dpe, np * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (pivoterrors) pivoterrors[np] = err;
+    if (np > 0 && (left || right)) {
+        if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(2 * m * np)))) return st;
+        if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(2 * np * n)))) return st;
+        tci::launch_cluci_factors(c->stream, dL, dU, (int)m, (int)n, (int)np, leftorth, c->rowperm,
+                                  c->colperm, left ? reinterpret_cast<double2*>(c->dF1) : nullptr,
+                                  right ? reinterpret_cast<double2*>(c->dF2) : nullptr);
+        HIPCHK(c, hipGetLastError());
+        if (left)
+            HIPCHK(c, hipMemcpyAsync(left, c->dF1, m * np * 16, hipMemcpyDeviceToHost, c->stream));
+        if (right)
+            HIPCHK(c, hipMemcpyAsync(right, c->dF2, np * n * 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return TCI_OK;
+}
+
 int tci_rrlu_c128_inplace_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda,
                             int64_t maxrank, double reltol, double abstol, int leftorth,
                             int64_t* rowperm, int64_t* colperm, int64_t* npivot,

@@ -139,6 +139,9 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
                           int leftorth, double2* L, double2* U, int64_t ldu, double* pe,
                           int* nanflag);
 
+void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,
+                          int leftorth, const int64_t* rowperm, const int64_t* colperm,
+                          double2* left, double2* right);
 void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);

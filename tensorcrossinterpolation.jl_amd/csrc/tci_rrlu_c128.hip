@@ -320,6 +320,71 @@ __global__ void k_crrlu_extract(const double2* A, int64_t ld, int m, int n, int 
     if (flag) atomicOr(nanflag, flag);
 }
 
+// MatrixLUCI{ComplexF64} factors (matrixluci.jl:161-283), one thread per output row (left) /
+// column (right) with the oracle's loop order: TRSM rows solved last column first, GEMM sums in
+// ascending t. L: m x np (ld m, unit diagonal if leftorth), U: np x n (ld np).
+__global__ void k_cluci_left(const double2* __restrict__ L, const double2* __restrict__ U, int m,
+                             int np, int leftorth, const int64_t* __restrict__ rowperm,
+                             double2* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double2* o = out + rowperm[i];
+    for (int j = np - 1; j >= 0; --j) {
+        double2 s = make_double2(0.0, 0.0);
+        if (leftorth) {  // [I; L21 / LowerTriangular(L11)]
+            if (i < np) {
+                s.x = (i == j) ? 1.0 : 0.0;
+            } else {
+                s = L[i + (int64_t)j * m];
+                for (int t = j + 1; t < np; ++t) {
+                    const double2 z = cmul(o[(int64_t)t * m], L[t + (int64_t)j * m]);
+                    s.x = s.x - z.x;
+                    s.y = s.y - z.y;
+                }
+                s = jl_cdiv(s, L[j + (int64_t)j * m]);
+            }
+        } else {  // colmatrix: L * U11
+            for (int t = 0; t < np; ++t) {
+                const double2 z = cmul(L[i + (int64_t)t * m], U[t + (int64_t)j * np]);
+                s.x = s.x + z.x;
+                s.y = s.y + z.y;
+            }
+        }
+        o[(int64_t)j * m] = s;
+    }
+}
+
+__global__ void k_cluci_right(const double2* __restrict__ L, const double2* __restrict__ U, int m,
+                              int n, int np, int leftorth, const int64_t* __restrict__ colperm,
+                              double2* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double2* o = out + (int64_t)np * colperm[c];
+    for (int a = np - 1; a >= 0; --a) {
+        double2 s = make_double2(0.0, 0.0);
+        if (!leftorth) {  // [I, UpperTriangular(U11) \ U12]
+            if (c < np) {
+                s.x = (a == c) ? 1.0 : 0.0;
+            } else {
+                s = U[a + (int64_t)c * np];
+                for (int t = a + 1; t < np; ++t) {
+                    const double2 z = cmul(U[a + (int64_t)t * np], o[t]);
+                    s.x = s.x - z.x;
+                    s.y = s.y - z.y;
+                }
+                s = jl_cdiv(s, U[a + (int64_t)a * np]);
+            }
+        } else {  // rowmatrix: L11 * U
+            for (int t = 0; t < np; ++t) {
+                const double2 z = cmul(L[a + (int64_t)t * m], U[t + (int64_t)c * np]);
+                s.x = s.x + z.x;
+                s.y = s.y + z.y;
+            }
+        }
+        o[a] = s;
+    }
+}
+
 }  // namespace
 
 int crrlu_grid(int m, int n, int t) {
@@ -352,6 +417,13 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
     if (grid < 1) grid = 1;
     if (grid > 4096) grid = 4096;
     k_crrlu_extract<<<grid, 256, 0, s>>>(A, ld, m, n, np, leftorth, L, U, ldu, pe, nanflag);
+}
+
+void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,
+                          int leftorth, const int64_t* rowperm, const int64_t* colperm,
+                          double2* left, double2* right) {
+    if (left) k_cluci_left<<<(m + 63) / 64, 64, 0, s>>>(L, U, m, np, leftorth, rowperm, left);
+    if (right) k_cluci_right<<<(n + 63) / 64, 64, 0, s>>>(L, U, m, n, np, leftorth, colperm, right);
 }
 
 }  // namespace tci

@@ -17,16 +17,19 @@ class MatrixLUCI:
 
     def __init__(self, A, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True, ctx=None):
         ctx = ctx or _lib.context()
-        A = np.asfortranarray(np.asarray(A, dtype=np.float64))
+        cplx = np.iscomplexobj(A)  # MatrixLUCI{ComplexF64}: tci_luci_c128_h
+        dt = np.complex128 if cplx else np.float64
+        A = np.asfortranarray(np.asarray(A, dtype=dt))
         m, n = A.shape
         mr = int(max(min(int(maxrank), m, n), 0))
         rowidx = np.zeros(max(mr, 1), np.int64)
         colidx = np.zeros(max(mr, 1), np.int64)
         pe = np.zeros(mr + 1)
-        lf = np.zeros(max(m * mr, 1))
-        rf = np.zeros(max(mr * n, 1))
+        lf = np.zeros(max(m * mr, 1), dt)
+        rf = np.zeros(max(mr * n, 1), dt)
         npv = C.c_int64()
-        ctx.check(ctx.lib.tci_luci_h(ctx.h, _lib.ptr(A), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
+        entry = ctx.lib.tci_luci_c128_h if cplx else ctx.lib.tci_luci_h
+        ctx.check(entry(ctx.h, _lib.ptr(A), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
                                      float(reltol), float(abstol), int(bool(leftorthogonal)),
                                      _lib.ptr(rowidx), _lib.ptr(colidx), _lib.ptr(pe), _lib.ptr(lf),
                                      _lib.ptr(rf), C.byref(npv)))

@@ -78,6 +78,8 @@ def lib():
         L.orc_rrlu_c128.argtypes = [f64p, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double,
                                     C.c_int, i64p, i64p, f64p, f64p, C.POINTER(C.c_int64),
                                     C.POINTER(C.c_double), f64p]
+        L.orc_luci_c128.argtypes = [f64p, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double,
+                                    C.c_int, i64p, i64p, f64p, f64p, f64p, C.POINTER(C.c_int64)]
         L.orc_cdiv.argtypes = [C.c_double] * 4 + [C.POINTER(C.c_double)] * 2
         L.orc_hypot.argtypes = [C.c_double, C.c_double]
         L.orc_hypot.restype = C.c_double
@@ -141,6 +143,26 @@ class OracleLUc:
         self.L = L[: m * k].reshape((m, k), order="F")
         self.U = U[: k * n].reshape((k, n), order="F")
         self.pivoterrors = pe[: k + 1].copy()
+
+
+def luci_c128(A, maxrank=None, reltol=1e-14, abstol=0.0, leftorthogonal=True):
+    """MatrixLUCI{ComplexF64} restatement -> (rowidx, colidx 0-based, pivoterrors, left, right)."""
+    A = np.asarray(A, dtype=np.complex128)
+    m, n = A.shape
+    maxrank = min(m, n) if maxrank is None else int(maxrank)
+    mr = max(min(maxrank, m, n), 0)
+    flat = np.ascontiguousarray(A.ravel(order="F")).view(np.float64)
+    ri = np.zeros(max(mr, 1), np.int64)
+    ci = np.zeros(max(mr, 1), np.int64)
+    pe = np.zeros(mr + 1)
+    lf = np.zeros(max(m * mr, 1), np.complex128)
+    rf = np.zeros(max(mr * n, 1), np.complex128)
+    npv = C.c_int64()
+    _check(lib().orc_luci_c128(flat, m, n, maxrank, reltol, abstol, int(leftorthogonal), ri, ci, pe,
+                               lf.view(np.float64), rf.view(np.float64), C.byref(npv)))
+    k = npv.value
+    return (ri[:k].copy(), ci[:k].copy(), pe[: k + 1].copy(), lf[: m * k].reshape((m, k), order="F"),
+            rf[: k * n].reshape((k, n), order="F"))
 
 
 class OracleLU:

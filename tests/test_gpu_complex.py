@@ -142,3 +142,18 @@ def test_crrlu_inplace_device_matches_host(ctx):
     assert np.array_equal(cp - 1, ref.colpermutation)
     assert err.value == ref.error
     assert np.array_equal(pe, ref.pivoterrors)
+
+
+@pytest.mark.parametrize("shape,kw", [((30, 24), {"maxrank": 10}), ((30, 24), {}), ((200, 150), {"maxrank": 40}),
+                                      ((90, 300), {"reltol": 1e-6})])
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_cluci_factors_bitwise(ctx, shape, kw, leftorth):
+    A = crand(np.random.default_rng(shape[0] + shape[1]), *shape)
+    luci = T.MatrixLUCI(A, leftorthogonal=leftorth, ctx=ctx, **kw)
+    ri, ci, pe, left, right = O.luci_c128(A, leftorthogonal=leftorth, **kw)
+    assert luci.npivots() == len(ri)
+    assert np.array_equal(luci.rowindices() - 1, ri)
+    assert np.array_equal(luci.colindices() - 1, ci)
+    assert np.array_equal(luci.pivoterrors(), pe)
+    assert np.array_equal(luci.left(), left)
+    assert np.array_equal(luci.right(), right)

@@ -88,3 +88,18 @@ def test_cdiv_and_hypot_restatements():
         assert O.lib().orc_hypot(x, y) == pytest.approx(math.hypot(x, y), rel=2.3e-16)
     assert O.lib().orc_hypot(float("inf"), float("nan")) == float("inf")
     assert math.isnan(O.lib().orc_hypot(1.0, float("nan")))
+
+
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_complex_luci_cross_interpolation(leftorth):
+    # MatrixLUCI property (test_matrixluci.jl:6-74): left * right reproduces A exactly on the
+    # pivot rows and columns, and A itself at full rank
+    rng = np.random.default_rng(8)
+    A = rng.random((30, 24)) - 0.5 + 1j * (rng.random((30, 24)) - 0.5)
+    ri, ci, pe, left, right = O.luci_c128(A, maxrank=10, leftorthogonal=leftorth)
+    assert len(ri) == 10
+    approx = left @ right
+    np.testing.assert_allclose(approx[ri, :], A[ri, :], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(approx[:, ci], A[:, ci], rtol=0, atol=1e-13)
+    ri, ci, pe, left, right = O.luci_c128(A, leftorthogonal=leftorth)
+    np.testing.assert_allclose(left @ right, A, rtol=0, atol=1e-13)
