@@ -184,6 +184,24 @@ int tci_update_pivots_h(tci_ctx* ctx, const tci_func* f, const int32_t* rows, in
                         int64_t* rowidx, int64_t* colidx, double* pivoterrors, int64_t* npivot,
                         double* maxabs, double* left, double* right);
 
+/* Batch evaluation of the ComplexF64 evaluator (cre + i cim) * f (see below): out is the
+ * (m * D) x n complex result, interleaved, ld m * D (NULL: only max|.| is returned). */
+int tci_batcheval_c128_h(tci_ctx* ctx, const tci_func* f, double cre, double cim,
+                         const int32_t* I, int64_t m, int32_t nl, const int32_t* J, int64_t n,
+                         int32_t nr, int32_t M, double* out, double* maxabs);
+
+/* The 2-site update for a ComplexF64 evaluator f_c(x) = (cre + i cim) * f(x) over a real device
+ * integrand f (the complex Lorentzian of test_tensorci2.jl:246-249 is coeff * TCI_F_LORENTZ):
+ * Pi on the device, max|Pi| (abs = hypot), complex rrLU, pivots, and with want_factors the
+ * MatrixLUCI{ComplexF64} factors (left m x np, right np x n, interleaved). Otherwise as
+ * tci_update_pivots_h. */
+int tci_update_pivots_c128_h(tci_ctx* ctx, const tci_func* f, double cre, double cim,
+                             const int32_t* rows, int64_t m, int32_t nl, const int32_t* cols,
+                             int64_t n, int32_t nr, int64_t maxrank, double reltol, double abstol,
+                             int leftorth, int want_factors, int64_t* rowidx, int64_t* colidx,
+                             double* pivoterrors, int64_t* npivot, double* maxabs, double* left,
+                             double* right);
+
 /* ---------------------------------------------------- site-tensor solve
  * Replaces setsitetensor!(tci, f, b) (tensorci2.jl:599-629): Pi1 = f(Iset_b x d x Jset_b),
  * P = f(Iset_{b+1} x Jset_b), T = Pi1 * P^-1 (partial-pivot LU of P^T, like getrf/getrs).

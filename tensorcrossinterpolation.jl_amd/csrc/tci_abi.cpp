@@ -99,6 +99,8 @@ struct tci_ctx {
     size_t capU = 0;
     char* cws = nullptr;  // ComplexF64 rrLU: state, candidates, pivot column / row buffers
     size_t capCws = 0;
+    double* dRe = nullptr;  // ComplexF64 2-site update: real values of f before the scaling
+    size_t capRe = 0;
     // kernel timing (family 0: rrLU pass with write-back, 1: batch evaluation,
     //                2: rrLU read-only pass)
     bool timing = false;
@@ -581,7 +583,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
-    fr(c->dU); fr(c->cws);
+    fr(c->dU); fr(c->cws); fr(c->dRe);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
@@ -920,25 +922,17 @@ int tci_rrlu_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
     return TCI_OK;
 }
 
-int tci_luci_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
-                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowidx,
-                    int64_t* colidx, double* pivoterrors, double* left, double* right,
-                    int64_t* npivot) {
-    if (!c || !npivot || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
-    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
-        return set_err(c, TCI_ERR_ARG, "MatrixLUCI: invalid dimensions");
-    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+// MatrixLUCI{ComplexF64} of the complex matrix already in c->dA (ld = max(m, 1))
+static int cluci_core(tci_ctx* c, int64_t m, int64_t n, int64_t maxrank, double reltol,
+                      double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
+                      double* pivoterrors, double* left, double* right, int64_t* npivot) {
     int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
     if (mr < 0) mr = 0;
     const int64_t ld = std::max<int64_t>(m, 1);
     int st;
-    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
     if ((st = ensure(c, &c->dL, &c->capL, (size_t)(2 * std::max<int64_t>(m * mr, 1))))) return st;
     if ((st = ensure(c, &c->dU, &c->capU, (size_t)(2 * std::max<int64_t>(mr * n, 1))))) return st;
     double2* dA = reinterpret_cast<double2*>(c->dA);
-    if (m > 0 && n > 0)
-        HIPCHK(c, hipMemcpy2DAsync(dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
-                                   c->stream));
     int64_t np;
     double err;
     tci::CState* dst;
@@ -971,6 +965,86 @@ int tci_luci_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     return TCI_OK;
+}
+
+int tci_luci_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowidx,
+                    int64_t* colidx, double* pivoterrors, double* left, double* right,
+                    int64_t* npivot) {
+    if (!c || !npivot || (m > 0 && n > 0 && !A)) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || (m > 0 && n > 0 && lda < m))
+        return set_err(c, TCI_ERR_ARG, "MatrixLUCI: invalid dimensions");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    const int64_t ld = std::max<int64_t>(m, 1);
+    int st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    if (m > 0 && n > 0)
+        HIPCHK(c, hipMemcpy2DAsync(c->dA, ld * 16, A, lda * 16, m * 16, n, hipMemcpyHostToDevice,
+                                   c->stream));
+    return cluci_core(c, m, n, maxrank, reltol, abstol, leftorth, rowidx, colidx, pivoterrors, left,
+                      right, npivot);
+}
+
+int tci_batcheval_c128_h(tci_ctx* c, const tci_func* f, double cre, double cim,
+                         const int32_t* I, int64_t m, int32_t nl, const int32_t* J, int64_t n,
+                         int32_t nr, int32_t M, double* out, double* maxabs) {
+    if (!c || !f || !maxabs) return TCI_ERR_ARG;
+    if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    const int64_t D = M ? f->localdims[nl] : 1;
+    const int64_t mR = m * D;
+    const int64_t ld = std::max<int64_t>(mR, 1);
+    if (mR > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int st;
+    if ((st = ensure(c, &c->dRe, &c->capRe, (size_t)(round_up(ld, 2) * std::max<int64_t>(n, 1)))))
+        return st;
+    double mxr = 0.0;
+    if ((st = tci_batcheval_d(c, f, I, m, nl, J, n, nr, M, c->dRe, round_up(ld, 2), &mxr))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    tci::launch_c128_scale(c->stream, c->dRe, round_up(ld, 2), (int)mR, (int)n, cre, cim,
+                           reinterpret_cast<double2*>(c->dA), ld, c->maxbits);
+    HIPCHK(c, hipGetLastError());
+    if (out && mR > 0 && n > 0)
+        HIPCHK(c, hipMemcpyAsync(out, c->dA, mR * n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double mx;
+    memcpy(&mx, c->hmaxbits, sizeof mx);
+    *maxabs = (mR > 0 && n > 0) ? mx : 0.0;
+    return TCI_OK;
+}
+
+int tci_update_pivots_c128_h(tci_ctx* c, const tci_func* f, double cre, double cim,
+                             const int32_t* rows, int64_t m, int32_t nl, const int32_t* cols,
+                             int64_t n, int32_t nr, int64_t maxrank, double reltol, double abstol,
+                             int leftorth, int want_factors, int64_t* rowidx, int64_t* colidx,
+                             double* pivoterrors, int64_t* npivot, double* maxabs, double* left,
+                             double* right) {
+    if (!c || !f || !npivot || !maxabs) return TCI_ERR_ARG;
+    if (nl + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    const int64_t ld = std::max<int64_t>(m, 1);
+    int st;
+    // real values of f on the device, then Pi = coeff * f and max|Pi| (hypot) into c->dA
+    if ((st = ensure(c, &c->dRe, &c->capRe, (size_t)(round_up(ld, 2) * std::max<int64_t>(n, 1)))))
+        return st;
+    double mxr = 0.0;
+    if ((st = tci_batcheval_d(c, f, rows, m, nl, cols, n, nr, 0, c->dRe, round_up(ld, 2), &mxr)))
+        return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    tci::launch_c128_scale(c->stream, c->dRe, round_up(ld, 2), (int)m, (int)n, cre, cim,
+                           reinterpret_cast<double2*>(c->dA), ld, c->maxbits);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double mx;
+    memcpy(&mx, c->hmaxbits, sizeof mx);
+    *maxabs = (m > 0 && n > 0) ? mx : 0.0;
+    return cluci_core(c, m, n, maxrank, reltol, abstol, leftorth, rowidx, colidx, pivoterrors,
+                      want_factors ? left : nullptr, want_factors ? right : nullptr, npivot);
 }
 
 int tci_rrlu_c128_inplace_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda,

@@ -139,6 +139,8 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
                           int leftorth, double2* L, double2* U, int64_t ldu, double* pe,
                           int* nanflag);
 
+void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int n, double cre,
+                       double cim, double2* out, int64_t ldo, unsigned long long* maxbits);
 void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,
                           int leftorth, const int64_t* rowperm, const int64_t* colperm,
                           double2* left, double2* right);

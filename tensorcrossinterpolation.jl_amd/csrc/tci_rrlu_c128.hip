@@ -385,6 +385,29 @@ __global__ void k_cluci_right(const double2* __restrict__ L, const double2* __re
     }
 }
 
+// Pi = coeff * f (ComplexF64 evaluator over a real device integrand) and max|Pi| (Julia's abs =
+// hypot; NaN propagates through the bit-pattern max like Base.max, util.jl:34-43)
+__global__ void k_c128_scale(const double* __restrict__ re, int64_t ldr, int m, int n, double cre,
+                             double cim, double2* __restrict__ out, int64_t ldo,
+                             unsigned long long* maxbits) {
+    const int64_t tot = (int64_t)m * n;
+    double mx = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(e % m), j = (int)(e / m);
+        const double x = re[i + (int64_t)j * ldr];
+        const double2 z = make_double2(cre * x, cim * x);
+        out[i + (int64_t)j * ldo] = z;
+        const double a = jl_hypot(z.x, z.y);
+        mx = (a != a || a > mx) ? a : mx;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double v = __shfl_xor(mx, o);
+        mx = (v != v || v > mx) ? v : mx;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
+}
+
 }  // namespace
 
 int crrlu_grid(int m, int n, int t) {
@@ -417,6 +440,15 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
     if (grid < 1) grid = 1;
     if (grid > 4096) grid = 4096;
     k_crrlu_extract<<<grid, 256, 0, s>>>(A, ld, m, n, np, leftorth, L, U, ldu, pe, nanflag);
+}
+
+void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int n, double cre,
+                       double cim, double2* out, int64_t ldo, unsigned long long* maxbits) {
+    const int64_t tot = (int64_t)m * n;
+    int grid = (int)((tot + 255) / 256);
+    if (grid < 1) grid = 1;
+    if (grid > 8192) grid = 8192;
+    k_c128_scale<<<grid, 256, 0, s>>>(re, ldr, m, n, cre, cim, out, ldo, maxbits);
 }
 
 void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,

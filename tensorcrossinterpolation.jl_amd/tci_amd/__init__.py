@@ -4,7 +4,7 @@ Host-side mirror of the reference's API for the path this package replaces (rrlu
 batch evaluation / TensorCI2 / crossinterpolate2); all compute runs in libtci_hip.so (gfx950).
 """
 from ._lib import Context, TCIArgumentError, TCIDeviceError, TCIError, context, load
-from .batcheval import (F_CP, F_GAUSS, F_GAUSSMIX, F_LORENTZ, F_MPO, F_QEXP, F_QOSC, F_SUM, F_TABLE, F_TT,
+from .batcheval import (ComplexScaledEvaluator, F_CP, F_GAUSS, F_GAUSSMIX, F_LORENTZ, F_MPO, F_QEXP, F_QOSC, F_SUM, F_TABLE, F_TT,
                         GPUBatchEvaluator, cp_function, gauss, gaussmix, lorentz, quantics_bits,
                         quantics_exp, quantics_osc, sum_, table, tensortrain_function)
 from .contraction import Contraction, contract, contract_naive, contract_TCI

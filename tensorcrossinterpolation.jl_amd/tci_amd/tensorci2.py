@@ -404,7 +404,7 @@ class TensorCI2:
         v = np.ones((1, 1))
         for p, i in enumerate(idx):
             v = v @ self.sitetensors[p][:, int(i) - 1, :]
-        return float(v[0, 0])
+        return complex(v[0, 0]) if np.iscomplexobj(v) else float(v[0, 0])
 
     def evaluate_many(self, X, ctx=None):
         """evaluate at every row of X in one device call (tci_tt_evaluate_h): the batched
@@ -454,6 +454,9 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
     """One fused device call: Pi = f(rows x cols), maxabs, rrLU, pivots, MatrixLUCI factors.
     An evaluator that is not a GPUBatchEvaluator (e.g. a ShardedBatchEvaluator) supplies Pi
     through its pi() method; the factorisation then runs on this process's GPU."""
+    if getattr(f, "is_complex", False):
+        return _update_pivots_c128(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                                   want_left, want_right)
     if not hasattr(f, "h"):
         return _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                       want_left, want_right)
@@ -475,6 +478,39 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
                                           int(bool(leftorth)), int(bool(want_factors)), _lib.ptr(rowidx),
                                           _lib.ptr(colidx), _lib.ptr(pe), C.byref(npv), C.byref(mx),
                                           _lib.ptr(left), _lib.ptr(right)))
+    k = npv.value
+    res = {"rowidx": rowidx[:k].copy(), "colidx": colidx[:k].copy(), "pivoterrors": pe[: k + 1].copy(),
+           "maxabs": mx.value, "npivot": k}
+    if left is not None:
+        res["left"] = left[: m * k].reshape((m, k), order="F")
+    if right is not None:
+        res["right"] = right[: k * n].reshape((k, n), order="F")
+    return res
+
+
+def _update_pivots_c128(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                        want_left, want_right):
+    """The 2-site update of a ComplexF64 evaluator: Pi, max|Pi|, complex rrLU and MatrixLUCI
+    factors in one device call (tci_update_pivots_c128_h)."""
+    ctx = f.ctx
+    rows = np.ascontiguousarray(rows, np.int32)
+    cols = np.ascontiguousarray(cols, np.int32)
+    m, nl = rows.shape
+    n, nr = cols.shape
+    mr = int(max(min(int(maxrank), m, n), 0))
+    rowidx = np.zeros(max(mr, 1), np.int64)
+    colidx = np.zeros(max(mr, 1), np.int64)
+    pe = np.zeros(mr + 1)
+    npv = C.c_int64()
+    mx = C.c_double()
+    left = np.zeros(max(m * mr, 1), np.complex128) if (want_factors and want_left) else None
+    right = np.zeros(max(mr * n, 1), np.complex128) if (want_factors and want_right) else None
+    ctx.check(ctx.lib.tci_update_pivots_c128_h(ctx.h, f.f.h, f.coeff.real, f.coeff.imag, _lib.ptr(rows), m, nl,
+                                               _lib.ptr(cols), n, nr, int(min(maxrank, INT64_MAX)),
+                                               float(reltol), float(abstol), int(bool(leftorth)),
+                                               int(bool(want_factors)), _lib.ptr(rowidx), _lib.ptr(colidx),
+                                               _lib.ptr(pe), C.byref(npv), C.byref(mx), _lib.ptr(left),
+                                               _lib.ptr(right)))
     k = npv.value
     res = {"rowidx": rowidx[:k].copy(), "colidx": colidx[:k].copy(), "pivoterrors": pe[: k + 1].copy(),
            "maxabs": mx.value, "npivot": k}
@@ -532,6 +568,12 @@ def _sitetensor_generic(f, Ib, Jb, Inext, solve):
 
 def sitetensor_device(f, Ib, Jb, Inext, solve=True):
     """T = Pi1 * P^-1 (tensorci2.jl:599-629) on the device; returns (T or None, max|Pi1|)."""
+    if getattr(f, "is_complex", False):
+        if solve and Inext is not None:
+            raise NotImplementedError("ComplexF64 site-tensor solve (setsitetensor! with P^-1) is not "
+                                      "implemented on the device; run with nsearchglobalpivot=0")
+        Pi1, mx = f.pi(Ib, Jb, 1, want_values=solve)
+        return (np.asfortranarray(Pi1) if solve else None), mx
     if not hasattr(f, "h"):
         return _sitetensor_generic(f, Ib, Jb, Inext, solve)
     ctx = f.ctx

@@ -2,6 +2,8 @@
 (orc_rrlu_c128): bit-exact permutations, L, U, npivot, lu.error and pivot errors -- the device
 restates Julia's complex division / abs exactly like the oracle, and the update keeps the
 reference's multiply-then-subtract (matrixlu.jl:318)."""
+import itertools
+
 import numpy as np
 import pytest
 
@@ -157,3 +159,50 @@ def test_cluci_factors_bitwise(ctx, shape, kw, leftorth):
     assert np.array_equal(luci.pivoterrors(), pe)
     assert np.array_equal(luci.left(), left)
     assert np.array_equal(luci.right(), right)
+
+
+# --- ComplexF64 TCI2: the reference's "Lorentz MPS with ValueType=ComplexF64" testset
+# (test_tensorci2.jl:246-339, pivotsearch=:full), with nsearchglobalpivot=0. Its
+# assertions are properties (rank equality, pivoterror bound, evaluate == f), kept as stated.
+
+def _clorentz(ctx, coeff=0.5 - 1.0j, n=5):
+    return T.ComplexScaledEvaluator(coeff, T.lorentz([10] * n, ctx=ctx))
+
+
+def test_complex_evaluator_values(ctx):
+    f = _clorentz(ctx)
+    X = np.array([[1, 1, 1, 1, 1], [2, 9, 10, 5, 7], [10, 10, 10, 10, 10]], np.int32)
+    v = f.points(X)
+    ref = (0.5 - 1.0j) * (1.0 / (1.0 + (X.astype(float) ** 2).sum(1)))
+    np.testing.assert_allclose(v, ref, rtol=1e-15)
+    Pi, mx = f.pi(X[:, :2], X[:, 2:], 0)
+    assert Pi.shape == (3, 3) and mx == pytest.approx(np.abs(Pi).max(), rel=1e-15)
+
+
+def test_complex_tci2_lorentz(ctx):
+    f = _clorentz(ctx)
+    tci2, ranks2, errors2 = T.crossinterpolate2(f, [10] * 5, [[1] * 5], tolerance=1e-8, maxiter=8,
+                                                sweepstrategy="forward", nsearchglobalpivot=0)
+    tci3, ranks3, errors3 = T.crossinterpolate2(f, [10] * 5, [[1] * 5], tolerance=1e-12, maxiter=200,
+                                                nsearchglobalpivot=0)
+    assert tci3.pivoterror() <= 2e-12
+    assert all(d <= 200 for d in tci3.linkdims()) and tci3.rank() <= 200
+    for v in itertools.product(range(1, 4), repeat=5):
+        val = tci3.evaluate(list(v))
+        assert isinstance(val, complex)
+        assert val == pytest.approx(f(list(v)), rel=1e-10, abs=1e-14)
+    initialpivots = [[1, 1, 1, 1, 1], [10, 8, 10, 4, 4], [5, 4, 8, 9, 3], [7, 7, 10, 5, 9], [7, 7, 10, 5, 9]]
+    tci4, _, _ = T.crossinterpolate2(f, [10] * 5, initialpivots, tolerance=1e-12, maxiter=200,
+                                     nsearchglobalpivot=0)
+    assert tci4.pivoterror() <= 2e-12
+    # same function up to a constant factor: the Float64 run finds the same ranks
+    fr = T.lorentz([10] * 5, ctx=ctx)
+    tr, ranksr, _ = T.crossinterpolate2(fr, [10] * 5, [[1] * 5], tolerance=1e-12, maxiter=200,
+                                        nsearchglobalpivot=0)
+    assert tci3.rank() == tr.rank()
+
+
+def test_complex_tci2_global_search_is_loud(ctx):
+    f = _clorentz(ctx)
+    with pytest.raises(NotImplementedError, match="ComplexF64 site-tensor solve"):
+        T.crossinterpolate2(f, [10] * 5, [[1] * 5], tolerance=1e-8, maxiter=3, nsearchglobalpivot=5)
