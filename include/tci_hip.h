@@ -224,6 +224,15 @@ int tci_tt_evaluate_h(tci_ctx* ctx, int32_t L, const int32_t* dims, const int32_
                       const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
                       double* out);
 
+/* ComplexF64 versions (interleaved re, im): the site-tensor solve T = Pi1 * P^-1
+ * (tensorci2.jl:620-627; getrf of P^T with LAPACK's cabs1 partial pivoting) and the tensor-train
+ * evaluation (abstracttensortrain.jl:328-342; ncore counts complex entries, X is validated). */
+int tci_sitetensor_solve_c128_h(tci_ctx* ctx, const double* P, int64_t r, const double* Pi1,
+                                int64_t R, double* T);
+int tci_tt_evaluate_c128_h(tci_ctx* ctx, int32_t L, const int32_t* dims, const int32_t* bonddims,
+                           const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
+                           double* out);
+
 /* ----------------------------------------------------- synthetic inputs
  * Fills d_A (m x n, ld lda) with U[0,1): splitmix64(seed * 0xD1B54A32D192ED03 + (i + m*j)) >> 11
  * times 2^-53 -- the same stream as the oracle's orc_fill_uniform. */

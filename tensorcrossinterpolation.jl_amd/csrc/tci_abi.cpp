@@ -1361,6 +1361,75 @@ int tci_tt_evaluate_h(tci_ctx* c, int32_t L, const int32_t* dims, const int32_t*
     return TCI_OK;
 }
 
+int tci_tt_evaluate_c128_h(tci_ctx* c, int32_t L, const int32_t* dims, const int32_t* bonddims,
+                           const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
+                           double* out) {
+    if (!c || L < 1 || !dims || !bonddims || !cores || (npts > 0 && (!X || !out)))
+        return TCI_ERR_ARG;
+    if (bonddims[0] != 1 || bonddims[L] != 1)
+        return set_err(c, TCI_ERR_ARG, "tt: the first and last bond dimensions must be 1");
+    std::vector<int64_t> off(L + 1, 0);
+    int rmax = 1;
+    for (int t = 0; t < L; ++t) {
+        off[t + 1] = off[t] + (int64_t)bonddims[t] * dims[t] * bonddims[t + 1];
+        rmax = std::max(rmax, (int)bonddims[t + 1]);
+    }
+    if (off[L] > ncore) return set_err(c, TCI_ERR_ARG, "tt: core buffer smaller than the bond dimensions imply");
+    if (rmax > 1024) return set_err(c, TCI_ERR_ARG, "tt: bond dimension above 1024");
+    for (int64_t e = 0; e < npts * L; ++e)
+        if (X[e] < 1 || X[e] > dims[e % L]) return set_err(c, TCI_ERR_ARG, "tt: index out of range");
+    if (npts == 0) return TCI_OK;
+    if (npts > INT32_MAX) return set_err(c, TCI_ERR_ARG, "tt: too many points");
+    const size_t bc = (size_t)off[L] * 16, bx = (size_t)(npts * L) * 4, bm = (size_t)(2 * L + 1) * 4,
+                 bo = (size_t)(L + 1) * 8, bout = (size_t)npts * 16;
+    const size_t o1 = round_up(bc, 16), o2 = o1 + round_up(bx, 16), o3 = o2 + round_up(bm, 16),
+                 o4 = o3 + round_up(bo, 16), total = o4 + bout;
+    int st;
+    if ((st = ensure(c, (char**)&c->scratch2, &c->capScratch2, total))) return st;
+    if ((st = ensure_pinned(c, &c->hin, &c->capHin, o4))) return st;
+    memcpy(c->hin, cores, bc);
+    memcpy(c->hin + o1, X, bx);
+    memcpy(c->hin + o2, dims, (size_t)L * 4);
+    memcpy(c->hin + o2 + (size_t)L * 4, bonddims, (size_t)(L + 1) * 4);
+    memcpy(c->hin + o3, off.data(), bo);
+    char* d = c->scratch2;
+    HIPCHK(c, hipMemcpyAsync(d, c->hin, o4, hipMemcpyHostToDevice, c->stream));
+    tci::launch_ctt_eval(c->stream, reinterpret_cast<const double2*>(d),
+                         reinterpret_cast<const int64_t*>(d + o3),
+                         reinterpret_cast<const int32_t*>(d + o2 + (size_t)L * 4),
+                         reinterpret_cast<const int32_t*>(d + o2), L,
+                         reinterpret_cast<const int32_t*>(d + o1), (int)npts,
+                         reinterpret_cast<double2*>(d + o4));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(out, d + o4, bout, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_sitetensor_solve_c128_h(tci_ctx* c, const double* P, int64_t r, const double* Pi1,
+                                int64_t R, double* T) {
+    if (!c || (r > 0 && (!P || !T)) || (R > 0 && r > 0 && !Pi1) || r < 0 || R < 0)
+        return TCI_ERR_ARG;
+    if (r == 0 || R == 0) return TCI_OK;
+    if (r > 8192 || R > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int st;
+    if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(2 * r * r)))) return st;
+    if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(2 * R * r)))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * (R * r + r * r))))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+    HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * 16, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * 16, hipMemcpyHostToDevice, c->stream));
+    double2* dT = reinterpret_cast<double2*>(c->dA);
+    double2* work = dT + R * r;
+    tci::launch_csitetensor_solve(c->stream, reinterpret_cast<const double2*>(c->dF2), (int)r,
+                                  reinterpret_cast<const double2*>(c->dF1), (int)R, dT, work,
+                                  c->dPiv);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(T, dT, R * r * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
 int tci_fill_uniform_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda, uint64_t seed) {
     if (!c || lda < m) return TCI_ERR_ARG;
     tci::launch_fill_uniform(c->stream, d_A, m, n, lda, seed);

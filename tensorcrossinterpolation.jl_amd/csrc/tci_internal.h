@@ -141,6 +141,10 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
 
 void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int n, double cre,
                        double cim, double2* out, int64_t ldo, unsigned long long* maxbits);
+void launch_csitetensor_solve(hipStream_t s, const double2* P, int r, const double2* Pi1, int R,
+                              double2* T, double2* work, int* piv);
+void launch_ctt_eval(hipStream_t s, const double2* cores, const int64_t* off, const int32_t* bd,
+                     const int32_t* dims, int L, const int32_t* X, int npts, double2* out);
 void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,
                           int leftorth, const int64_t* rowperm, const int64_t* colperm,
                           double2* left, double2* right);

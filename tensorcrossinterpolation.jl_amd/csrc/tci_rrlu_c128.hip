@@ -408,6 +408,134 @@ __global__ void k_c128_scale(const double* __restrict__ re, int64_t ldr, int m, 
     if ((threadIdx.x & 63) == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
 }
 
+// T = Pi1 * P^-1 for ComplexF64 (setsitetensor!, tensorci2.jl:620-627: transpose(transpose(P) \
+// transpose(Pi1))): getrf of A = P^T with partial pivoting (LAPACK's pivot: first maximal
+// cabs1 = |re| + |im|), one 1024-thread workgroup, A in global memory (r x r).
+__global__ __launch_bounds__(1024) void k_cgetrf_T(const double2* __restrict__ P, int r,
+                                                   double2* __restrict__ A, int* __restrict__ piv) {
+    __shared__ double sv[16];
+    __shared__ int si[16];
+    __shared__ int sp;
+    const int tid = threadIdx.x;
+    for (int64_t e = tid; e < (int64_t)r * r; e += 1024) {  // A[i, j] = P[j, i]
+        const int i = (int)(e % r), j = (int)(e / r);
+        A[e] = P[j + (int64_t)i * r];
+    }
+    __syncthreads();
+    for (int k = 0; k < r; ++k) {
+        double bv = -1.0;
+        int bi = INT32_MAX;
+        for (int i = k + tid; i < r; i += 1024) {
+            const double2 a = A[i + (int64_t)k * r];
+            const double v = fabs(a.x) + fabs(a.y);
+            if (v > bv) { bv = v; bi = i; }
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double ov = __shfl_xor(bv, o);
+            const int oi = __shfl_xor(bi, o);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if ((tid & 63) == 0) { sv[tid >> 6] = bv; si[tid >> 6] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+            double v = sv[0];
+            int ix = si[0];
+            for (int w = 1; w < 16; ++w)
+                if (sv[w] > v || (sv[w] == v && si[w] < ix)) { v = sv[w]; ix = si[w]; }
+            sp = ix == INT32_MAX ? k : ix;
+            piv[k] = sp;
+        }
+        __syncthreads();
+        const int p = sp;
+        if (p != k)
+            for (int j = tid; j < r; j += 1024) {
+                const double2 t = A[k + (int64_t)j * r];
+                A[k + (int64_t)j * r] = A[p + (int64_t)j * r];
+                A[p + (int64_t)j * r] = t;
+            }
+        __syncthreads();
+        const double2 d = A[k + (int64_t)k * r];
+        for (int i = k + 1 + tid; i < r; i += 1024) A[i + (int64_t)k * r] = jl_cdiv(A[i + (int64_t)k * r], d);
+        __syncthreads();
+        const int nt = r - k - 1;
+        for (int64_t e = tid; e < (int64_t)nt * nt; e += 1024) {
+            const int i = k + 1 + (int)(e % nt), j = k + 1 + (int)(e / nt);
+            const double2 z = cmul(A[i + (int64_t)k * r], A[k + (int64_t)j * r]);
+            double2 a = A[i + (int64_t)j * r];
+            a.x = a.x - z.x;
+            a.y = a.y - z.y;
+            A[i + (int64_t)j * r] = a;
+        }
+        __syncthreads();
+    }
+}
+
+// getrs: one thread per right-hand side b = Pi1[q, :]^T; x = T[q, :]
+__global__ void k_cgetrs_rows(const double2* __restrict__ A, const int* __restrict__ piv, int r,
+                              const double2* __restrict__ Pi1, int R, double2* __restrict__ T) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= R) return;
+    double2* x = T + q;  // x[i] at T[q + i * R]
+    for (int i = 0; i < r; ++i) x[(int64_t)i * R] = Pi1[q + (int64_t)i * R];
+    for (int k = 0; k < r; ++k) {
+        const int p = piv[k];
+        if (p != k) {
+            const double2 t = x[(int64_t)k * R];
+            x[(int64_t)k * R] = x[(int64_t)p * R];
+            x[(int64_t)p * R] = t;
+        }
+    }
+    for (int i = 0; i < r; ++i) {  // unit lower
+        double2 s = x[(int64_t)i * R];
+        for (int t = 0; t < i; ++t) {
+            const double2 z = cmul(A[i + (int64_t)t * r], x[(int64_t)t * R]);
+            s.x = s.x - z.x;
+            s.y = s.y - z.y;
+        }
+        x[(int64_t)i * R] = s;
+    }
+    for (int i = r - 1; i >= 0; --i) {  // upper
+        double2 s = x[(int64_t)i * R];
+        for (int t = i + 1; t < r; ++t) {
+            const double2 z = cmul(A[i + (int64_t)t * r], x[(int64_t)t * R]);
+            s.x = s.x - z.x;
+            s.y = s.y - z.y;
+        }
+        x[(int64_t)i * R] = jl_cdiv(s, A[i + (int64_t)i * r]);
+    }
+}
+
+// evaluate(tt, x) (abstracttensortrain.jl:328-342) for ComplexF64 cores: one workgroup per
+// point, the running row vector in LDS (bond dimensions <= 1024)
+__global__ __launch_bounds__(256) void k_ctt_eval(const double2* __restrict__ cores,
+                                                  const int64_t* __restrict__ off,
+                                                  const int32_t* __restrict__ bd,
+                                                  const int32_t* __restrict__ dims, int L,
+                                                  const int32_t* __restrict__ X, double2* out) {
+    __shared__ double2 v[2][1024];
+    const int pt = blockIdx.x;
+    const int32_t* x = X + (int64_t)pt * L;
+    if (threadIdx.x == 0) v[0][0] = make_double2(1.0, 0.0);
+    __syncthreads();
+    int cur = 0;
+    for (int p = 0; p < L; ++p) {
+        const int ra = bd[p], rb = bd[p + 1], d = dims[p];
+        const double2* Tp = cores + off[p] + (int64_t)(x[p] - 1) * ra;  // T[:, x, :], ld ra * d
+        for (int b = threadIdx.x; b < rb; b += 256) {
+            double2 s = make_double2(0.0, 0.0);
+            for (int a = 0; a < ra; ++a) {
+                const double2 z = cmul(v[cur][a], Tp[a + (int64_t)b * ra * d]);
+                s.x = s.x + z.x;
+                s.y = s.y + z.y;
+            }
+            v[cur ^ 1][b] = s;
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (threadIdx.x == 0) out[pt] = v[cur][0];
+}
+
 }  // namespace
 
 int crrlu_grid(int m, int n, int t) {
@@ -449,6 +577,17 @@ void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int 
     if (grid < 1) grid = 1;
     if (grid > 8192) grid = 8192;
     k_c128_scale<<<grid, 256, 0, s>>>(re, ldr, m, n, cre, cim, out, ldo, maxbits);
+}
+
+void launch_csitetensor_solve(hipStream_t s, const double2* P, int r, const double2* Pi1, int R,
+                              double2* T, double2* work, int* piv) {
+    k_cgetrf_T<<<1, 1024, 0, s>>>(P, r, work, piv);
+    k_cgetrs_rows<<<(R + 63) / 64, 64, 0, s>>>(work, piv, r, Pi1, R, T);
+}
+
+void launch_ctt_eval(hipStream_t s, const double2* cores, const int64_t* off, const int32_t* bd,
+                     const int32_t* dims, int L, const int32_t* X, int npts, double2* out) {
+    if (npts > 0) k_ctt_eval<<<npts, 256, 0, s>>>(cores, off, bd, dims, L, X, out);
 }
 
 void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,

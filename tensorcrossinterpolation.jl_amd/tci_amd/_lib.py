@@ -69,6 +69,8 @@ SIGNATURES = {
                              C.c_int),
     "tci_update_pivots_c128_h": ([vp, vp, dbl, dbl, vp, i64, C.c_int32, vp, i64, C.c_int32, i64, dbl, dbl,
                                   C.c_int, C.c_int, vp, vp, vp, pi64, pdbl, vp, vp], C.c_int),
+    "tci_sitetensor_solve_c128_h": ([vp, vp, i64, vp, i64, vp], C.c_int),
+    "tci_tt_evaluate_c128_h": ([vp, C.c_int32, vp, vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_rrlu_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, pi64, pdbl, vp],
                            C.c_int),
     "tci_luci_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),

@@ -415,6 +415,13 @@ class TensorCI2:
         ctx = ctx or _lib.context()
         dims = np.asarray(self.localdims, np.int32)
         bd = np.asarray([self.sitetensors[0].shape[0]] + [T.shape[2] for T in self.sitetensors], np.int32)
+        if any(np.iscomplexobj(T) for T in self.sitetensors):  # TensorCI2{ComplexF64}
+            cores = np.concatenate([np.asarray(T, np.complex128).ravel(order="F") for T in self.sitetensors])
+            out = np.zeros(len(X), np.complex128)
+            ctx.check(ctx.lib.tci_tt_evaluate_c128_h(ctx.h, len(self), _lib.ptr(dims), _lib.ptr(bd),
+                                                     _lib.ptr(cores), cores.size, _lib.ptr(X), len(X),
+                                                     _lib.ptr(out)))
+            return out
         cores = np.concatenate([np.asarray(T, np.float64).ravel(order="F") for T in self.sitetensors])
         out = np.zeros(len(X))
         ctx.check(ctx.lib.tci_tt_evaluate_h(ctx.h, len(self), _lib.ptr(dims), _lib.ptr(bd), _lib.ptr(cores),
@@ -569,11 +576,18 @@ def _sitetensor_generic(f, Ib, Jb, Inext, solve):
 def sitetensor_device(f, Ib, Jb, Inext, solve=True):
     """T = Pi1 * P^-1 (tensorci2.jl:599-629) on the device; returns (T or None, max|Pi1|)."""
     if getattr(f, "is_complex", False):
-        if solve and Inext is not None:
-            raise NotImplementedError("ComplexF64 site-tensor solve (setsitetensor! with P^-1) is not "
-                                      "implemented on the device; run with nsearchglobalpivot=0")
         Pi1, mx = f.pi(Ib, Jb, 1, want_values=solve)
-        return (np.asfortranarray(Pi1) if solve else None), mx
+        if not solve or Inext is None:
+            return (np.asfortranarray(Pi1) if solve else None), mx
+        P, _ = f.pi(Inext, Jb, 0)
+        if P.shape[0] != P.shape[1]:
+            raise RuntimeError("Pivot matrix is not square!")
+        r, R = P.shape[0], Pi1.shape[0]
+        T = np.zeros(max(R * r, 1), np.complex128)
+        ctx = f.ctx
+        ctx.check(ctx.lib.tci_sitetensor_solve_c128_h(ctx.h, _lib.ptr(np.asfortranarray(P)), r,
+                                                      _lib.ptr(np.asfortranarray(Pi1)), R, _lib.ptr(T)))
+        return T[: R * r].reshape((R, r), order="F"), mx
     if not hasattr(f, "h"):
         return _sitetensor_generic(f, Ib, Jb, Inext, solve)
     ctx = f.ctx

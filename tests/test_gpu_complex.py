@@ -202,7 +202,33 @@ def test_complex_tci2_lorentz(ctx):
     assert tci3.rank() == tr.rank()
 
 
-def test_complex_tci2_global_search_is_loud(ctx):
+def test_complex_sitetensor_solve_and_tt_eval(ctx):
+    rng = np.random.default_rng(31)
+    for r, R in ((1, 5), (7, 70), (40, 400)):
+        P = crand(rng, r, r) + 2 * np.eye(r)
+        Pi1 = crand(rng, R, r)
+        T_ = np.zeros(R * r, np.complex128)
+        ctx.check(ctx.lib.tci_sitetensor_solve_c128_h(ctx.h, T._lib.ptr(np.asfortranarray(P)), r,
+                                                      T._lib.ptr(np.asfortranarray(Pi1)), R, T._lib.ptr(T_)))
+        Tm = T_.reshape((R, r), order="F")
+        np.testing.assert_allclose(Tm @ P, Pi1, rtol=0, atol=1e-12)
+    # tensor-train evaluation vs the host chain of products (abstracttensortrain.jl:328-342)
+    dims, bds = [3, 4, 2, 5], [1, 6, 9, 4, 1]
+    cores = [rng.random((bds[t], dims[t], bds[t + 1])) - 0.5 + 1j * rng.random((bds[t], dims[t], bds[t + 1]))
+             for t in range(4)]
+    tci = T.TensorCI2(dims)
+    tci.sitetensors = cores
+    X = np.array(list(itertools.product(*[range(1, d + 1) for d in dims])), np.int32)
+    got = tci.evaluate_many(X, ctx=ctx)
+    ref = np.array([tci.evaluate(list(x)) for x in X])
+    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=1e-14)
+
+
+def test_complex_tci2_with_global_search(ctx):
+    # the default flow: site tensors solved every iteration, DefaultGlobalPivotFinder on
     f = _clorentz(ctx)
-    with pytest.raises(NotImplementedError, match="ComplexF64 site-tensor solve"):
-        T.crossinterpolate2(f, [10] * 5, [[1] * 5], tolerance=1e-8, maxiter=3, nsearchglobalpivot=5)
+    tci, ranks, errors = T.crossinterpolate2(f, [10] * 5, [[1] * 5], tolerance=1e-12, maxiter=200,
+                                             rng=np.random.default_rng(0))
+    assert tci.pivoterror() <= 2e-12
+    for v in itertools.product(range(1, 4), repeat=5):
+        assert tci.evaluate(list(v)) == pytest.approx(f(list(v)), rel=1e-10, abs=1e-14)
