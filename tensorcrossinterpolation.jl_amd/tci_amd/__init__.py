@@ -7,6 +7,7 @@ from ._lib import Context, TCIArgumentError, TCIDeviceError, TCIError, context, 
 from .batcheval import (ComplexScaledEvaluator, F_CP, F_GAUSS, F_GAUSSMIX, F_LORENTZ, F_MPO, F_QEXP, F_QOSC, F_SUM, F_TABLE, F_TT,
                         GPUBatchEvaluator, cp_function, gauss, gaussmix, lorentz, quantics_bits,
                         quantics_exp, quantics_osc, sum_, table, tensortrain_function)
+from .cachedfunction import CachedFunction
 from .contraction import Contraction, contract, contract_naive, contract_TCI
 from .distributed import Comm, ShardedBatchEvaluator, column_blocks
 from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder

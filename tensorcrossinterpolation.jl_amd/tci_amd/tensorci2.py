@@ -532,16 +532,18 @@ def _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, wan
                            want_left, want_right):
     ctx = _ctx_of(f)
     Pi, mx = f.pi(np.asarray(rows, np.int32), np.asarray(cols, np.int32), 0)
-    Pi = np.asfortranarray(Pi, np.float64)
+    cplx = np.iscomplexobj(Pi)  # MatrixLUCI{ComplexF64}
+    dt = np.complex128 if cplx else np.float64
+    Pi = np.asfortranarray(Pi, dt)
     m, n = Pi.shape
     mr = int(max(min(int(maxrank), m, n), 0))
     rowidx = np.zeros(max(mr, 1), np.int64)
     colidx = np.zeros(max(mr, 1), np.int64)
     pe = np.zeros(mr + 1)
     npv = C.c_int64()
-    left = np.zeros(max(m * mr, 1)) if (want_factors and want_left) else None
-    right = np.zeros(max(mr * n, 1)) if (want_factors and want_right) else None
-    ctx.check(ctx.lib.tci_luci_h(ctx.h, _lib.ptr(Pi), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
+    left = np.zeros(max(m * mr, 1), dt) if (want_factors and want_left) else None
+    right = np.zeros(max(mr * n, 1), dt) if (want_factors and want_right) else None
+    ctx.check((ctx.lib.tci_luci_c128_h if cplx else ctx.lib.tci_luci_h)(ctx.h, _lib.ptr(Pi), m, n, max(m, 1), int(min(maxrank, INT64_MAX)),
                                  float(reltol), float(abstol), int(bool(leftorth)), _lib.ptr(rowidx),
                                  _lib.ptr(colidx), _lib.ptr(pe), _lib.ptr(left), _lib.ptr(right),
                                  C.byref(npv)))
@@ -566,8 +568,14 @@ def _sitetensor_generic(f, Ib, Jb, Inext, solve):
     if P.shape[0] != P.shape[1]:
         raise RuntimeError("Pivot matrix is not square!")
     R = Pi1.shape[0]
-    T = np.zeros(max(R * r, 1))
     ctx = _ctx_of(f)
+    if np.iscomplexobj(Pi1) or np.iscomplexobj(P):
+        T = np.zeros(max(R * r, 1), np.complex128)
+        ctx.check(ctx.lib.tci_sitetensor_solve_c128_h(ctx.h, _lib.ptr(np.asfortranarray(P, np.complex128)), r,
+                                                      _lib.ptr(np.asfortranarray(Pi1, np.complex128)), R,
+                                                      _lib.ptr(T)))
+        return T[: R * r].reshape((R, r), order="F"), mx
+    T = np.zeros(max(R * r, 1))
     ctx.check(ctx.lib.tci_sitetensor_solve_h(ctx.h, _lib.ptr(np.asfortranarray(P, np.float64)), r,
                                              _lib.ptr(np.asfortranarray(Pi1, np.float64)), R, _lib.ptr(T)))
     return T[: R * r].reshape((R, r), order="F"), mx

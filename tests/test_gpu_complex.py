@@ -232,3 +232,24 @@ def test_complex_tci2_with_global_search(ctx):
     assert tci.pivoterror() <= 2e-12
     for v in itertools.product(range(1, 4), repeat=5):
         assert tci.evaluate(list(v)) == pytest.approx(f(list(v)), rel=1e-10, abs=1e-14)
+
+
+@pytest.mark.parametrize("cplx", [False, True])
+def test_cachedfunction_tci2(ctx, cplx):
+    # CachedFunction over a device evaluator (misses evaluated in one device batch call, Pi
+    # factorised by the device rrLU): same TCI2 result as the evaluator itself; a second run is
+    # served from the cache
+    base = T.lorentz([10] * 5, ctx=ctx)
+    f = _clorentz(ctx) if cplx else base
+    cf = T.CachedFunction(f, [10] * 5, complex if cplx else float)
+    kw = dict(tolerance=1e-10, maxiter=20, nsearchglobalpivot=0)
+    t1, r1, e1 = T.crossinterpolate2(f, [10] * 5, [[1] * 5], **kw)
+    t2, r2, e2 = T.crossinterpolate2(cf, [10] * 5, [[1] * 5], **kw)
+    assert r1 == r2
+    np.testing.assert_allclose(e2, e1, rtol=1e-10, atol=1e-15)
+    for b in range(5):
+        assert np.array_equal(t1.Iset[b], t2.Iset[b]) and np.array_equal(t1.Jset[b], t2.Jset[b])
+    n = cf.ncacheddata()
+    assert n > 0
+    T.crossinterpolate2(cf, [10] * 5, [[1] * 5], **kw)
+    assert cf.ncacheddata() == n
