@@ -11,7 +11,9 @@
  * checked against the known-answer tests the reference ships in test/test_matrixlu.jl,
  * test/test_matrixluci.jl, test/test_batcheval.jl and test/test_tensorci2.jl (ported as JSON
  * fixtures under tests/golden/). Julia is absent from this image, so the reference itself
- * cannot be executed; see DESIGN.md "Oracle".
+ * cannot be executed; see DESIGN.md "Oracle". The ComplexF64 rrLU / MatrixLUCI restatement
+ * (orc_rrlu_c128, orc_luci_c128) is pinned by the complex argmax KAT (test_matrixlu.jl:39-52);
+ * its Julia Base pieces (ComplexF64 `/`, abs = hypot) are parity unpinned at their last ulp.
  *
  * Arithmetic contract (matches Julia without @fastmath): compile with -ffp-contract=off so
  * `a - x*y` stays a separate multiply and subtract (matrixlu.jl:318), normalisation is a true
