@@ -28,6 +28,9 @@
 namespace tci {
 namespace {
 
+#ifndef TCI_C128_NT
+#define TCI_C128_NT 0  // non-temporal stores of the updated trailing block (A/B switch)
+#endif
 constexpr int kCTR = 64;      // rows per tile (one wave lane per row)
 constexpr int kCTC = 32;      // columns per tile (4 waves x 8 columns)
 constexpr int kCThreads = 256;
@@ -195,7 +198,13 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step(CStepArgs g) {
                 const double2 z = cmul(xs[lane], ys[jl]);
                 a.x = a.x - z.x;
                 a.y = a.y - z.y;
+#if TCI_C128_NT
+                typedef double dv2 __attribute__((ext_vector_type(2)));
+                dv2 wv = {a.x, a.y};
+                __builtin_nontemporal_store(wv, reinterpret_cast<dv2*>(pa));
+#else
                 *pa = a;
+#endif
             }
             const double v = a.x * a.x + a.y * a.y;
             if (v > best.v) best = CCand{v, j, i};  // columns ascend: strict '>' keeps the first
