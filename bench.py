@@ -136,6 +136,11 @@ def main():
         if pn:
             by_pending[P] = round(pm / pn, 5)
     ctx.set_timing(False)
+    # the benchmarked factorisation once more with permutations and pivot errors, for the parity
+    # check against the CPU runs on the same matrix (rank 0 factorises the seed-0 matrix)
+    W.copy_from(A)
+    npd, _, rpd, cpd, ped = T.rrlu_inplace_device(W, maxrank=r, want_perms=True)
+    dev_res = (npd, rpd[:m].copy(), cpd[:n].copy(), ped.copy())
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -214,12 +219,19 @@ def main():
         if rank == 0:
             out["extras"] = extras(T, ctx)
             out["extras"]["pi_lorentz_sharded"] = sh
+    parity_ok = True
     if rank == 0 and not args.no_cpu and world == 1:
-        out["cpu_baseline"] = cpu_baseline(m, n, r, args.cpu_pivots)
+        base, cpu_res = cpu_baseline(m, n, r, args.cpu_pivots)
+        out["cpu_baseline"] = base
+        out["parity"] = parity_vs_cpu(dev_res, cpu_res, r)
+        parity_ok = out["parity"]["ok"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if not parity_ok:
+        sys.stderr.write("bench: device rrLU differs from the CPU oracle on the benchmarked matrix\n")
+        sys.exit(3)
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
@@ -321,13 +333,16 @@ def extras(T, ctx):
                              "pi_rows_per_s_call": round(m / wall, 1),
                              "write_GBps_device": round(8.0 * m * n / dev_s / 1e9, 1)}
         dm.free()
-    # TCI2 sweep wall time, config 1: 8d Lorentzian, localdims = fill(10, 8), tol = 1e-8
-    f = T.lorentz([10] * 8, ctx=ctx)
-    T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)  # warm
-    t0 = time.perf_counter()
-    tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-8, nsearchglobalpivot=0)
-    res["tci2_config1"] = {"wall_s": round(time.perf_counter() - t0, 4), "ranks": ranks,
-                           "final_error": errors[-1], "mode": "nsearchglobalpivot=0"}
+    # roofline fractions of the Pi assembly: the Lorentzian is HBM-write-bound (8 B per element);
+    # the quantics integrand is fp64 VALU-bound (exp/sin/pow per element), rated by its fp64 VALU
+    # instruction count per element from rocprofv3 (profiles/, scripts/pmc_valu.sh) when present
+    lz = res["pi_lorentz"]
+    lz["roofline"] = {"bound": "hbm-write", "achieved": lz["write_GBps_device"], "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(lz["write_GBps_device"] / HBM_PEAK_GBS, 4)}
+    res["pi_quantics_osc"]["roofline"] = qosc_roofline(res["pi_quantics_osc"])
+    # TCI2 sweep wall times of the BASELINE configs (scripts/tci2_configs.py), with the 1-core
+    # oracle's wall time next to them where the oracle finishes in seconds (C1, C3, C4)
+    res["tci2_configs"] = tci2_configs()
     # separable (CP-rank-K) Pi assembly of config 5 as an fp64 MFMA GEMM: 8192^2, K = 1024,
     # 12 legs of d = 32, against the measured fp64 MFMA peak
     import ctypes as C
@@ -429,18 +444,136 @@ def extras(T, ctx):
     return res
 
 
+def _host_info():
+    info = {"nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Socket(s)", "Core(s) per socket", "Thread(s) per core", "NUMA node(s)"):
+                info["lscpu_" + k.strip().lower().replace("(s)", "s").replace(" ", "_")] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def _native_omp_lib():
+    """oracle/cpu_rrlu_omp.c built with -march=native for THIS host (a second, no GPU involved);
+    falls back to the portable x86-64-v3 copy oracle/Makefile builds."""
+    import subprocess
+    import tempfile
+    src = os.path.join(ROOT, "oracle", "cpu_rrlu_omp.c")
+    out = os.path.join(tempfile.mkdtemp(prefix="tci_cpu_"), "libcpu_rrlu_omp_native.so")
+    try:
+        subprocess.run(["gcc", "-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+                        "-std=c11", "-fopenmp", "-shared", "-o", out, src, "-lm"], check=True,
+                       capture_output=True, timeout=60)
+        return out, "gcc -O3 -march=native -fopenmp -ffp-contract=off (built on this host)"
+    except Exception:
+        return None, "gcc -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off (portable oracle/Makefile build)"
+
+
+VALU_SUMMARY = os.path.join(ROOT, "profiles", "r02_qosc_valu.json")
+FP64_VECTOR_PEAK_TF = 78.6  # MI355X spec fp64 vector (and matrix) rate
+
+
+def qosc_roofline(rec):
+    """fp64 VALU roofline of the quantics assembly: flops/element from the committed PMC count of
+    fp64 VALU instructions (64 lanes; FMA = 2 flops), x elements / device time."""
+    if not os.path.exists(VALU_SUMMARY):
+        return {"bound": "valu-fp64", "achieved": None, "peak": FP64_VECTOR_PEAK_TF, "unit": "TFLOP/s",
+                "frac": None, "note": "no PMC summary committed"}
+    with open(VALU_SUMMARY) as fh:
+        v = json.load(fh)
+    fpe = v["fp64_flops_per_element"]
+    dev_s = rec["m"] / rec["pi_rows_per_s_device"]  # device time of one m x n assembly
+    tf = fpe * rec["m"] * rec["n"] / dev_s / 1e12
+    return {"bound": "valu-fp64", "achieved": round(tf, 2), "peak": FP64_VECTOR_PEAK_TF, "unit": "TFLOP/s",
+            "frac": round(tf / FP64_VECTOR_PEAK_TF, 4), "fp64_flops_per_element": fpe,
+            "source": os.path.relpath(VALU_SUMMARY, ROOT)}
+
+
+def tci2_configs():
+    os.environ.setdefault("TCI2_CONFIGS_ORACLE", "1")
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import tci2_configs as TC
+    TC.ORACLE = os.environ["TCI2_CONFIGS_ORACLE"] == "1"
+    cs = TC.configs()
+    out = {}
+    for name in ("C1_lorentz8d_parity", "C1_lorentz8d_default", "C3_gauss20d", "C3_gaussmix20d", "C4_qosc40",
+                 "C5_cp12d_K256"):
+        rec = cs[name]()
+        rec.pop("linkdims", None)
+        out[name] = rec
+    return out
+
+
 def cpu_baseline(m, n, r, pivots):
-    """The oracle (C restatement of _optimizerrlu!, one core) on the first `pivots` pivots of the
-    same (m, n) matrix: GFLOP/s over that bounded sample."""
+    """CPU baselines on the same seed-0 (m, n) matrix (SURVEY 8(d) "CPU baseline"):
+      (ii) all host cores -- oracle/cpu_rrlu_omp.c (OpenMP over columns, update fused with the next
+           argmax, bitwise the oracle's results), every pivot: the reported `value`;
+      (i)  one core -- the loop-for-loop restatement oracle/tci_oracle.c, first `pivots` pivots.
+    Returns (baseline dict, results of both for the parity check against the device)."""
     import oracle_lib as O
     a = O.fill_uniform(m * n, seed=0)
+    path, build = _native_omp_lib()
+    L = O.omp_lib(path)
+    threads = int(L.cpu_rrlu_threads())
+    w = a.copy()
     t0 = time.perf_counter()
-    npv, _, _, _ = O.rrlu_inplace_sample(a, m, n, r, pivots)
+    npo, erro, rpo, cpo = O.rrlu_inplace_omp(w, m, n, r, -1, path=path)
+    dto = time.perf_counter() - t0
+    pe_omp = np.concatenate([np.abs(w[np.arange(npo) * (m + 1)]), [erro]])
+    del w
+    t0 = time.perf_counter()
+    npv, err, rp, cp = O.rrlu_inplace_sample(a, m, n, r, pivots)
     dt = time.perf_counter() - t0
+    pe_one = np.concatenate([np.abs(a[np.arange(npv) * (m + 1)]), [err]])
+    del a
     fl = rrlu_flops(m, n, npv)
-    return {"value": round(fl / dt / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
-            "sample": f"oracle rrLU (tci_oracle.c, -O3, 1 thread) first {npv} of {r} pivots on the "
-                      f"same {m}x{n} matrix, {dt:.1f} s"}
+    base = {"value": round(rrlu_flops(m, n, npo) / dto / 1e9, 4), "unit": "GFLOP/s", "cores": threads,
+            "kind": "port",
+            "sample": f"all {npo} of {r} pivots of rrlu on the same {m}x{n} seed-0 matrix, "
+                      f"{dto:.2f} s: oracle/cpu_rrlu_omp.c (OpenMP over {threads} threads, rank-1 update fused "
+                      f"with the next argmax, bitwise the oracle's results)",
+            "build": build,
+            "host": _host_info(),
+            "single_thread": {"value": round(fl / dt / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
+                              "sample": f"oracle rrLU (tci_oracle.c, loop-for-loop, 1 thread) first {npv} of {r} "
+                                        f"pivots on the same {m}x{n} matrix, {dt:.1f} s"}}
+    return base, {"omp": (npo, rpo, cpo, pe_omp), "one": (npv, rp, cp, pe_one)}
+
+
+def parity_vs_cpu(dev, cpu, r):
+    """Device step vs both CPU runs on the same matrix: npivot, pivot rows / columns in pivot order,
+    the full permutations (all-pivot run) and the pivot errors, all bitwise."""
+    npd, rpd, cpd, ped = dev
+    res = {}
+    ok = True
+    for name, (npc, rpc, cpc, pec) in cpu.items():
+        k = min(npc, npd)
+        full = npc == npd
+        chk = {"npivot_equal": bool(full) if name == "omp" else bool(npd >= npc),
+               "pivots_compared": int(k),
+               "rowindices_equal": bool(np.array_equal(rpd[:k] - 1, rpc[:k])),
+               "colindices_equal": bool(np.array_equal(cpd[:k] - 1, cpc[:k])),
+               "pivoterrors_equal": bool(np.array_equal(ped[:k], pec[:k]))}
+        if name == "omp" and full:
+            chk["permutations_equal"] = bool(np.array_equal(rpd - 1, rpc) and np.array_equal(cpd - 1, cpc))
+            chk["lasterror_equal"] = bool(ped[npd] == pec[npc])
+        res["vs_" + name] = chk
+        ok = ok and all(v for kk, v in chk.items() if kk != "pivots_compared")
+    res["ok"] = ok
+    return res
 
 
 if __name__ == "__main__":

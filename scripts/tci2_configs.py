@@ -15,27 +15,41 @@ import numpy as np  # noqa: E402
 import tci_amd as T  # noqa: E402
 
 
-def run(name, f, localdims, initialpivots=None, **kw):
+ORACLE = os.environ.get("TCI2_CONFIGS_ORACLE", "0") == "1"  # also time the CPU oracle (where bounded)
+
+
+def run(name, f, localdims, initialpivots=None, oracle_ok=False, **kw):
     T.crossinterpolate2(f, localdims, initialpivots, **dict(kw, maxiter=1))  # warm the kernels
     t0 = time.perf_counter()
     tci, ranks, errors = T.crossinterpolate2(f, localdims, initialpivots, **kw)
     wall = time.perf_counter() - t0
-    return {"config": name, "wall_s": round(wall, 4), "iterations": len(ranks),
-            "ranks": ranks, "final_error": errors[-1], "linkdims": tci.linkdims(),
-            "kwargs": {k: v for k, v in kw.items() if k != "rng"}}
+    res = {"config": name, "wall_s": round(wall, 4), "iterations": len(ranks),
+           "ranks": ranks, "final_error": errors[-1], "linkdims": tci.linkdims(),
+           "kwargs": {k: v for k, v in kw.items() if k != "rng"}}
+    if ORACLE and oracle_ok and kw.get("nsearchglobalpivot", 5) == 0:
+        # the CPU oracle (1 core, deterministic mode) on the same integrand, initial pivots and kwargs
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        okw = {k: v for k, v in kw.items() if k in ("tolerance", "maxbonddim", "maxiter")}
+        t0 = time.perf_counter()
+        _, oranks, oerrors = O.crossinterpolate2(f.kind, f.params, localdims, initialpivots, **okw)
+        res["oracle_wall_s"] = round(time.perf_counter() - t0, 4)
+        res["oracle_ranks_equal"] = list(oranks) == list(ranks)
+        res["oracle_final_error"] = oerrors[-1]
+    return res
 
 
 def configs():
     out = {}
     out["C1_lorentz8d_parity"] = lambda: run("C1 8d Lorentzian d=10 tol=1e-8 (nsearchglobalpivot=0)",
                                              T.lorentz([10] * 8), [10] * 8, tolerance=1e-8,
-                                             nsearchglobalpivot=0)
+                                             nsearchglobalpivot=0, oracle_ok=True)
     out["C1_lorentz8d_default"] = lambda: run("C1 8d Lorentzian d=10 tol=1e-8 (default global search)",
                                               T.lorentz([10] * 8), [10] * 8, tolerance=1e-8,
                                               rng=np.random.default_rng(0))
     out["C3_gauss20d"] = lambda: run("C3 20d separable Gaussian d=16 tol=1e-10 maxbonddim=512",
                                      T.gauss([16] * 20, 0.05, 8.5), [16] * 20, [[8] * 20],
-                                     tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0)
+                                     tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0, oracle_ok=True)
 
     def gaussmix():
         rng = np.random.default_rng(3)
@@ -61,7 +75,7 @@ def configs():
         f = T.quantics_osc(40)
         p0 = T.optfirstpivot(f, [2] * 40)
         return run("C4 quantics exp(-10x) sin(2pi 100 x^1.1), 40 legs d=2 tol=1e-8", f, [2] * 40, [p0],
-                   tolerance=1e-8, nsearchglobalpivot=0)
+                   tolerance=1e-8, nsearchglobalpivot=0, oracle_ok=True)
     out["C4_qosc40"] = qosc
 
     def cp12():

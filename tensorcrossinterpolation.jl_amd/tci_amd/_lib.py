@@ -3,9 +3,11 @@
 The HIP library is the only compute path: if it is missing or no GPU is visible, every entry
 point raises -- there is no CPU fallback.
 """
+import atexit
 import ctypes as C
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -119,8 +121,34 @@ def ptr(a):
     return a.ctypes.data_as(vp)
 
 
+# Teardown order (SIGSEGV inside exit() after rocprofv3 finalisation): every
+# context and every device object it owns is released by an atexit hook, i.e. while the
+# interpreter and the HIP runtime are both still intact. After that, __del__ methods and
+# interpreter finalisation make no HIP calls at all.
+_live_contexts = weakref.WeakSet()
+_shutting_down = False
+
+
+def shutting_down():
+    return _shutting_down
+
+
+@atexit.register
+def _shutdown():
+    global _shutting_down
+    for c in list(_live_contexts):
+        try:
+            c.close()
+        except Exception:
+            pass
+    _shutting_down = True
+
+
 class Context:
-    """One tci_ctx (device stream + workspaces). Use `context()` for the per-thread default."""
+    """One tci_ctx (device stream + workspaces). Use `context()` for the per-thread default.
+
+    Device objects created on a context (integrands, DeviceMatrix) register with `own()`; `close()`
+    releases them before the context itself, and nothing touches HIP after the atexit hook."""
 
     def __init__(self, device=0):
         self.lib = load()
@@ -131,6 +159,17 @@ class Context:
                                      "(no visible MI355X / HIP runtime?)")
         self.h = h
         self.device = device
+        self._owned = weakref.WeakSet()
+        _live_contexts.add(self)
+
+    def own(self, obj):
+        """Registers a device object with a `release()` method, freed before the context."""
+        self._owned.add(obj)
+        return obj
+
+    @property
+    def alive(self):
+        return bool(getattr(self, "h", None)) and not _shutting_down
 
     def check(self, st):
         if st == TCI_OK:
@@ -143,9 +182,15 @@ class Context:
         raise TCIError(st, msg)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not _shutting_down:
+            for obj in list(getattr(self, "_owned", ())):
+                try:
+                    obj.release()
+                except Exception:
+                    pass
+            self.lib.tci_ctx_synchronize(self.h)
             self.lib.tci_ctx_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

@@ -41,12 +41,16 @@ class GPUBatchEvaluator:
                                                     np.ascontiguousarray(self.localdims, np.int32), self.L,
                                                     C.byref(h)))
         self.h = h
+        self.ctx.own(self)
+
+    def release(self):
+        if getattr(self, "h", None) and self.ctx.alive:
+            self.ctx.lib.tci_func_destroy(self.h)
+        self.h = None
 
     def __del__(self):
         try:
-            if getattr(self, "h", None):
-                self.ctx.lib.tci_func_destroy(self.h)
-                self.h = None
+            self.release()
         except Exception:
             pass
 

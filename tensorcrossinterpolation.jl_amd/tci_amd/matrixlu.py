@@ -205,6 +205,7 @@ class DeviceMatrix:
         p = C.c_void_p()
         self.ctx.check(self.ctx.lib.tci_malloc_d(self.ctx.h, C.byref(p), self.nbytes))
         self.ptr = p
+        self.ctx.own(self)
 
     def fill_uniform(self, seed):
         self.ctx.check(self.ctx.lib.tci_fill_uniform_d(self.ctx.h, self.ptr, self.m, self.n, self.ld, seed))
@@ -219,9 +220,11 @@ class DeviceMatrix:
         return buf.reshape((self.ld, max(self.n, 1)), order="F")[: self.m, : self.n]
 
     def free(self):
-        if self.ptr:
+        if self.ptr and self.ctx.alive:
             self.ctx.lib.tci_free_d(self.ctx.h, self.ptr)
-            self.ptr = None
+        self.ptr = None
+
+    release = free
 
     def __del__(self):
         try:

@@ -639,21 +639,30 @@ def _batch_maxabs(f, I, J, M):
     return mx.value
 
 
-_scratch_cache = {}
+class _Scratch:
+    """Per-context device scratch for Pi evaluations whose values are not needed (only max|.|)."""
+
+    def __init__(self, ctx, nelem):
+        self.ctx = ctx
+        self.size = max(int(nelem * 1.5), 1024)
+        p = C.c_void_p()
+        ctx.check(ctx.lib.tci_malloc_d(ctx.h, C.byref(p), self.size * 8))
+        self.ptr = p
+        ctx.own(self)
+
+    def release(self):
+        if self.ptr and self.ctx.alive:
+            self.ctx.lib.tci_free_d(self.ctx.h, self.ptr)
+        self.ptr = None
 
 
 def _scratch(ctx, nelem):
-    key = id(ctx)
-    cur = _scratch_cache.get(key)
-    if cur is None or cur[1] < nelem:
+    cur = getattr(ctx, "_scratch", None)
+    if cur is None or cur.ptr is None or cur.size < nelem:
         if cur is not None:
-            ctx.lib.tci_free_d(ctx.h, cur[0])
-        p = C.c_void_p()
-        size = max(int(nelem * 1.5), 1024)
-        ctx.check(ctx.lib.tci_malloc_d(ctx.h, C.byref(p), size * 8))
-        _scratch_cache[key] = (p, size)
-        cur = _scratch_cache[key]
-    return cur[0]
+            cur.release()
+        cur = ctx._scratch = _Scratch(ctx, nelem)
+    return cur.ptr
 
 
 def crossinterpolate2(f, localdims=None, initialpivots=None, **kwargs):

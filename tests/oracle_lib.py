@@ -222,6 +222,37 @@ def rrlu_inplace_sample(A_flat, m, n, maxrank, pivot_limit, reltol=1e-14, abstol
     return npv.value, err.value, rp, cp
 
 
+OMP_LIB_PATH = os.path.join(ROOT, "oracle", "libcpu_rrlu_omp.so")
+_omp = {}
+
+
+def omp_lib(path=None):
+    """The all-core rrLU baseline (oracle/cpu_rrlu_omp.c); `path` selects a host-native build."""
+    path = path or OMP_LIB_PATH
+    if path not in _omp:
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(path)
+        L.cpu_rrlu_inplace_omp.argtypes = [f64p, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_double,
+                                           C.c_double, C.c_int, i64p, i64p, C.POINTER(C.c_int64),
+                                           C.POINTER(C.c_double), C.c_int64]
+        L.cpu_rrlu_threads.restype = C.c_int
+        _omp[path] = L
+    return _omp[path]
+
+
+def rrlu_inplace_omp(A_flat, m, n, maxrank, pivot_limit=-1, reltol=1e-14, abstol=0.0, leftorth=True,
+                     path=None):
+    """All-core baseline: same results as rrlu_inplace_sample, bitwise (cpu_rrlu_omp.c)."""
+    rp = np.zeros(max(m, 1), np.int64)
+    cp = np.zeros(max(n, 1), np.int64)
+    npv, err = C.c_int64(), C.c_double()
+    omp_lib(path).cpu_rrlu_inplace_omp(A_flat, m, n, m, maxrank, reltol, abstol, int(leftorth), rp, cp,
+                                       C.byref(npv), C.byref(err), pivot_limit)
+    return npv.value, err.value, rp, cp
+
+
 def batcheval(kind, params, localdims, I, J, M):
     """I: (m, nl) int, J: (n, nr) int (1-based). Returns (out (m, prod(dc), n) F-order, maxabs)."""
     params = np.ascontiguousarray(params if params is not None and len(params) else [0.0], np.float64)

@@ -23,7 +23,7 @@ def _cfg(name):
     return next(c for c in GOLDEN if c["name"] == name)
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", [c["name"] for c in GOLDEN if c.get("cpu_check", True)])
 def test_oracle_reproduces_config_golden(name):
     c = _cfg(name)
     t, ranks, errors = O.crossinterpolate2(c["kind"], c["params"], c["localdims"], c["initialpivots"], **c["kw"])

@@ -4,6 +4,7 @@ Every case mirrors one @testset of the reference (file:line in tests/golden/refe
 CPU only: no GPU, no product code.
 """
 import itertools
+import os
 
 import numpy as np
 import pytest
@@ -304,3 +305,49 @@ def test_tt_function_reconstruction():
         for p in range(1, 4):
             ref = ref @ cores[p][:, idx[p] - 1, :]
         assert np.isclose(t.evaluate(list(idx)), ref[0, 0], rtol=1e-8)
+
+
+# ---------------------------------------------------------------- all-core CPU baseline
+@pytest.mark.parametrize("m,n,maxrank,leftorth", [(1, 1, 1, True), (37, 53, 37, True), (300, 211, 120, False),
+                                                  (513, 700, 200, True), (64, 1000, 64, False)])
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_omp_baseline_bitwise_equals_oracle(m, n, maxrank, leftorth, threads):
+    """oracle/cpu_rrlu_omp.c (bench.py's all-core cpu_baseline) is the same computation as the
+    loop-for-loop restatement: identical permutations, packed factors, npivot and error."""
+    import subprocess
+    import sys
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {O.ROOT + '/tests'!r})
+import oracle_lib as O
+A = O.fill_uniform({m} * {n}, seed={m + n})
+A[::7] = A[::7] - 0.5
+a1, a2 = A.copy(), A.copy()
+r1 = O.rrlu_inplace_sample(a1, {m}, {n}, {maxrank}, -1, leftorth={leftorth})
+r2 = O.rrlu_inplace_omp(a2, {m}, {n}, {maxrank}, -1, leftorth={leftorth})
+assert r1[0] == r2[0] and (r1[1] == r2[1] or (r1[1] != r1[1] and r2[1] != r2[1])), (r1[:2], r2[:2])
+assert np.array_equal(r1[2][:{m}], r2[2][:{m}]) and np.array_equal(r1[3][:{n}], r2[3][:{n}])
+assert np.array_equal(a1, a2)
+print("ok", r1[0])
+"""
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("ok")
+
+
+def test_omp_baseline_ties_and_nan():
+    I = np.array(list(itertools.product(range(1, 8), repeat=2)), np.int32)
+    Pi, _ = O.batcheval(1, [1.0], [7] * 4, I, I, 0)
+    Pi = np.ascontiguousarray(Pi[:, 0, :].ravel(order="F"))
+    B = O.fill_uniform(40 * 30, seed=9)
+    B[5] = np.nan
+    B[77] = np.nan
+    for A, m, n in ((Pi, 49, 49), (B, 40, 30)):
+        for reltol in (1e-14, 1e-3):
+            a1, a2 = A.copy(), A.copy()
+            r1 = O.rrlu_inplace_sample(a1, m, n, min(m, n), -1, reltol=reltol)
+            r2 = O.rrlu_inplace_omp(a2, m, n, min(m, n), -1, reltol=reltol)
+            assert r1[0] == r2[0]
+            assert np.array_equal(r1[2], r2[2]) and np.array_equal(r1[3], r2[3])
+            assert np.array_equal(a1, a2, equal_nan=True)
