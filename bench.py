@@ -441,7 +441,108 @@ def extras(T, ctx):
                                     "GFLOPs": round(rrlu_flops(m2, n2, r2) / dt / 1e9, 1)})
         A.free()
         W.free()
+    res["dense_mfma"] = dense_extras(T, ctx)
     return res
+
+
+MFMA_F64_SPEC_TFLOPS = 78.6  # MI355X fp64 matrix peak (spec; 2.4 GHz x 256 CU x 4 SIMD x 32 flop/clk)
+
+
+def dense_extras(T, ctx, only_k3=False):
+    """fp64 MFMA dense kernels (tci_dense.hip), device time from HIP events on
+    the context stream (timing families 20-22):
+    * the fp64 MFMA probe at 1 / 2 / 4 waves per SIMD, with the shader clock it held;
+    * K3, the blocked Schur-complement update C -= W V on 8192^2 at nb in {32, 64, 128, 256}
+      (BASELINE.md:46, SURVEY 7 hard part 1): TFLOP/s as a fraction of the 78.6 TF spec, and the
+      HBM-algorithmic rate (C read + written, W and V read once) as a fraction of 8 TB/s;
+    * K5, setsitetensor!'s solve at the C5 shape (r = 1024, R = 32768) and the scaled one (256, 8192);
+    * K4, the MatrixLUCI factor kernels of an 8192^2 matrix at np = 1024, both orthogonalities."""
+    import ctypes as C
+    out = {"spec_TFLOPs": MFMA_F64_SPEC_TFLOPS}
+    probe = {}
+    for w in (1, 2, 4):
+        tf, ghz = C.c_double(), C.c_double()
+        ctx.check(ctx.lib.tci_diag_mfma_f64_ex(ctx.h, w, C.byref(tf), C.byref(ghz)))
+        probe[f"waves_per_simd_{w}"] = {"TFLOPs": round(tf.value, 2), "clock_GHz": round(ghz.value, 3)}
+    out["probe"] = probe
+    best = max(v["TFLOPs"] for v in probe.values())
+    m = n = 8192
+    Cm = T.DeviceMatrix(m, n, ctx=ctx)
+    Cm.fill_uniform(seed=3)
+    k3 = []
+    for nb in (32, 64, 128, 256):
+        W = T.DeviceMatrix(m, nb, ctx=ctx)
+        W.fill_uniform(seed=4)
+        V = T.DeviceMatrix(nb, n, ctx=ctx)
+        V.fill_uniform(seed=5)
+        T.schur_update_device(Cm, W, V)
+        ctx.set_timing(True)
+        for _ in range(5):
+            T.schur_update_device(Cm, W, V)
+        kms, kn = ctx.kernel_stats(22)
+        ctx.set_timing(False)
+        sec = kms / kn * 1e-3
+        tfl = 2.0 * m * n * nb / sec / 1e12
+        gbs = (16.0 * m * n + 8.0 * (m + n) * nb) / sec / 1e9
+        k3.append({"m": m, "n": n, "nb": nb, "ms": round(sec * 1e3, 4), "TFLOPs": round(tfl, 2),
+                   "frac_of_spec": round(tfl / MFMA_F64_SPEC_TFLOPS, 4),
+                   "frac_of_probe": round(tfl / best, 4), "algorithmic_GBps": round(gbs, 1),
+                   "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
+        W.free()
+        V.free()
+    Cm.free()
+    out["schur_update_k3"] = k3
+    if only_k3:
+        return out
+    solves = []
+    for r, R in ((256, 8192), (1024, 32768), (1024, 64)):
+        P0 = T.DeviceMatrix(r, r, ctx=ctx, ld=r)
+        P0.fill_uniform(seed=6)
+        P = T.DeviceMatrix(r, r, ctx=ctx, ld=r)
+        Pi1 = T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+        Pi1.fill_uniform(seed=7)
+        Tm = T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+        rec = {"r": r, "R": R}
+        for tag, mask in (("mfma", 7), ("round1_scalar", 0), ("mfma_getrs_only", 4)):
+            ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+            P.copy_from(P0)
+            T.sitetensor_solve_device(P, Pi1, Tm)
+            ctx.set_timing(True)
+            for _ in range(3):
+                P.copy_from(P0)
+                T.sitetensor_solve_device(P, Pi1, Tm)
+            kms, kn = ctx.kernel_stats(20)
+            ctx.set_timing(False)
+            sec = kms / kn * 1e-3
+            fl = 2.0 / 3.0 * r ** 3 + 2.0 * R * r * r
+            rec[tag] = {"ms": round(sec * 1e3, 3), "TFLOPs": round(fl / sec / 1e12, 2),
+                        "frac_of_spec": round(fl / sec / 1e12 / MFMA_F64_SPEC_TFLOPS, 4)}
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 7))
+        solves.append(rec)
+        for x in (P0, P, Pi1, Tm):
+            x.free()
+    out["sitetensor_solve_k5"] = solves
+    lucis = []
+    A = T.DeviceMatrix(8192, 8192, ctx=ctx)
+    A.fill_uniform(seed=8)
+    Ah = A.to_host()
+    A.free()
+    for lo in (True, False):
+        npv = 1024
+        # GEMM with K = np over the full np x n (or m x np) block + TRSM m np^2 (or n np^2)
+        fl = 2.0 * npv * npv * 8192 + 1.0 * (8192 - npv) * npv * npv
+        rec = {"m": 8192, "n": 8192, "np": npv, "leftorthogonal": lo}
+        for tag, mask in (("mfma", 7), ("round1_scalar", 0)):
+            ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+            ctx.set_timing(True)
+            T.MatrixLUCI(Ah, maxrank=npv, leftorthogonal=lo, ctx=ctx).left()
+            kms, kn = ctx.kernel_stats(21)
+            ctx.set_timing(False)
+            rec[tag] = {"ms": round(kms / max(kn, 1), 3), "TFLOPs": round(fl / (kms / max(kn, 1) * 1e-3) / 1e12, 2)}
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 7))
+        lucis.append(rec)
+    out["luci_factors_k4"] = lucis
+    return out
 
 
 def _host_info():

@@ -70,7 +70,8 @@ int tci_ctx_synchronize(tci_ctx* ctx);
  * measured with hipEvents on the context stream: family 0 = rrLU pass that writes the Schur
  * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
  * 1 = batch evaluation; 3 + P (P = 1..16) = the read-only passes that applied P pending updates
- * (a breakdown of family 2). */
+ * (a breakdown of family 2); 20 = site-tensor solve (getrf + getrs of P^T), 21 = MatrixLUCI
+ * factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d. */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
@@ -94,6 +95,11 @@ int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
  * chunks that can hold the argmax. Bitwise identical results (same argmax, same tie order as
  * submatrixargmax, matrixlu.jl:46-87). Default on (env TCI_RRLU_SHADOW=0: off). */
 int tci_set_rrlu_shadow(tci_ctx* ctx, int enabled);
+
+/* fp64 MFMA forms of the MatrixLUCI factors (bit 1), the site-tensor getrf
+ * (bit 2) and getrs (bit 4); default 7 (env TCI_DENSE_MFMA). 0 restores the round-1 scalar
+ * kernels (A/B). Factors / solutions agree to the parity tolerances either way. */
+int tci_set_dense_mfma(tci_ctx* ctx, int mask);
 
 /* ------------------------------------------------------------ integrands */
 /* Uploads an integrand's parameters to the device once; localdims has L entries. */
@@ -216,6 +222,25 @@ int tci_sitetensor_h(tci_ctx* ctx, const tci_func* f, const int32_t* Ib, int64_t
 int tci_sitetensor_solve_h(tci_ctx* ctx, const double* P, int64_t r, const double* Pi1, int64_t R,
                            double* T);
 
+/* The same solve on device buffers (P r x r is clobbered by its LU; Pi1 and T R x r, ld R): no
+ * PCIe. Blocked right-looking getrf of P^T (panels factorised in LDS, partial pivoting as getrf)
+ * and a blocked getrs, the trailing / off-diagonal updates on fp64 MFMA (K3). */
+int tci_sitetensor_solve_d(tci_ctx* ctx, double* d_P, int64_t r, const double* d_Pi1, int64_t R,
+                           double* d_T);
+
+/* ------------------------------------------------ K3: fp64 MFMA GEMM / Schur update
+ * The blocked Schur-complement update of a right-looking LU, C -= W * V (C m x n ld ldc, W m x k
+ * ld ldw, V k x n ld ldv; device pointers), on v_mfma_f64_16x16x4f64 with the operands staged in
+ * LDS -- the trailing update of the site-tensor getrf and the off-diagonal work of every blocked
+ * triangular solve of this library (matrixluci.jl:194-241, tensorci2.jl:620-627 call LAPACK /
+ * BLAS there; rrLU itself has no such update: exact full pivoting). */
+int tci_schur_update_d(tci_ctx* ctx, double* d_C, int64_t m, int64_t n, int64_t ldc,
+                       const double* d_W, int64_t ldw, const double* d_V, int64_t ldv, int64_t k);
+/* C = beta * C + alpha * A * op(B); op(B) = B (k x n, ld ldb) or, transb != 0, B^T (B n x k). */
+int tci_dgemm_d(tci_ctx* ctx, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                const double* d_A, int64_t lda, const double* d_B, int64_t ldb, double beta,
+                double* d_C, int64_t ldc);
+
 /* evaluate(tt, idx) (abstracttensortrain.jl:328-342) of a tensor train at npts points, as the
  * global pivot search needs it (globalpivotfinder.jl:236): cores packed one after another, core
  * t being (bonddims[t], dims[t], bonddims[t+1]) column-major (the site tensors of a TensorCI2);
@@ -248,6 +273,9 @@ int tci_diag_stream_d(tci_ctx* ctx, const double* d_a, double* d_b, int64_t n, i
 /* Diagnostic: measured fp64 MFMA throughput (TFLOP/s) of independent v_mfma_f64_16x16x4f64
  * chains on every SIMD -- the peak the separable-assembly GEMM is rated against. */
 int tci_diag_mfma_f64(tci_ctx* ctx, double* tflops);
+/* The same probe with 1, 2 or 4 waves per SIMD (one workgroup per CU); *ghz = clock64 cycles of
+ * the loop / its wall time: the shader clock the chip held while issuing fp64 MFMA. */
+int tci_diag_mfma_f64_ex(tci_ctx* ctx, int waves_per_simd, double* tflops, double* ghz);
 
 /* ------------------------------------------------------------ device mem */
 int tci_malloc_d(tci_ctx* ctx, void** p, int64_t bytes);

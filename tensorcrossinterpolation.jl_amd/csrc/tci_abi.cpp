@@ -45,6 +45,7 @@ struct tci_ctx {
     size_t capS = 0;
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
+    int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
     int ncu = 0;           // compute units of the device
     double* colbuf = nullptr;  // mid path: published candidate columns
     size_t capColbuf = 0;
@@ -114,7 +115,7 @@ struct tci_ctx {
         size_t idx;
     };
     std::vector<EvPair> evpairs;
-    static constexpr int kFams = 3 + tci::kMaxPend + 1;
+    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 3;  // + 20 solve, 21 LUCI factors, 22 K3
     double fam_ms[kFams] = {};
     int64_t fam_n[kFams] = {};
 };
@@ -544,6 +545,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
+    if (const char* e = getenv("TCI_DENSE_MFMA")) c->dense = std::max(0, std::min(atoi(e), (int)tci::kDenseAll));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->ncu = prop.multiProcessorCount;
@@ -616,6 +618,12 @@ int tci_set_rrlu_small(tci_ctx* c, int enabled) {
 
 int tci_set_rrlu_shadow(tci_ctx* c, int enabled) {
     c->shadow = enabled != 0;
+    return TCI_OK;
+}
+
+int tci_set_dense_mfma(tci_ctx* c, int mask) {
+    if (!c || mask < 0 || mask > tci::kDenseAll) return TCI_ERR_ARG;
+    c->dense = mask;
     return TCI_OK;
 }
 
@@ -1098,9 +1106,11 @@ static int luci_outputs(tci_ctx* c, int64_t m, int64_t n, int leftorth, int64_t 
     if (fac) {
         if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(m * np)))) return st;
         if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(np * n)))) return st;
+        ev_begin(c, 21);
         tci::launch_luci_factors(c->stream, c->dL, m, c->dU, np, (int)m, (int)n, (int)np, leftorth,
                                  c->rowperm, c->colperm, left ? c->dF1 : nullptr,
-                                 right ? c->dF2 : nullptr);
+                                 right ? c->dF2 : nullptr, c->dense);
+        ev_end(c);
         HIPCHK(c, hipGetLastError());
         if (left)
             HIPCHK(c, hipMemcpyAsync(left, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
@@ -1253,7 +1263,7 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
         // Pi1), tensorci2.jl:609), and each evaluation resets c->maxbits
         if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
         if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
-        if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+        if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
         if ((st = ensure(c, &c->dI2, &c->capI2, (size_t)std::max<int64_t>(nInext * (wI + 1), 1))))
             return st;
         if (bn)
@@ -1263,7 +1273,9 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
     }
     if ((st = batcheval_launch(c, f, c->dI, nIb, wI, c->dJ, nJb, wJ, 1, c->dF1, ldR))) return st;
     if (solve) {
-        tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
+        ev_begin(c, 20);
+        tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv, c->dense);
+        ev_end(c);
         HIPCHK(c, hipGetLastError());
     }
     // T (and maxabs) down through one pinned stage
@@ -1289,10 +1301,12 @@ int tci_sitetensor_solve_h(tci_ctx* c, const double* P, int64_t r, const double*
     if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
     if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(R * r)))) return st;
     if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
     HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv);
+    ev_begin(c, 20);
+    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv, c->dense);
+    ev_end(c);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1318,6 +1332,75 @@ int tci_diag_mfma_f64(tci_ctx* c, double* tflops) {
     hipEventDestroy(e1);
     const double flops = (double)grid * 4 /* waves */ * iters * 8 * (16.0 * 16 * 4 * 2);
     *tflops = flops / (ms * 1e-3) / 1e12;
+    return TCI_OK;
+}
+
+int tci_sitetensor_solve_d(tci_ctx* c, double* d_P, int64_t r, const double* d_Pi1, int64_t R,
+                           double* d_T) {
+    if (!c || r < 0 || R < 0 || (r > 0 && R > 0 && (!d_P || !d_Pi1 || !d_T))) return TCI_ERR_ARG;
+    if (r == 0 || R == 0) return TCI_OK;
+    if (r > INT32_MAX / 2 || R > INT32_MAX / 2 || r * R > INT32_MAX * 64LL)
+        return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
+    ev_begin(c, 20);
+    tci::launch_sitetensor_solve(c->stream, d_P, (int)r, const_cast<double*>(d_Pi1), (int)R, d_T, c->dPiv, c->dense);
+    ev_end(c);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_dgemm_d(tci_ctx* c, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                const double* d_A, int64_t lda, const double* d_B, int64_t ldb, double beta,
+                double* d_C, int64_t ldc) {
+    if (!c || m < 0 || n < 0 || k < 0) return TCI_ERR_ARG;
+    if (m == 0 || n == 0) return TCI_OK;
+    if (!d_C || (k > 0 && (!d_A || !d_B)) || lda < std::max<int64_t>(m, 1) ||
+        ldb < std::max<int64_t>(transb ? n : k, 1) || ldc < m)
+        return set_err(c, TCI_ERR_ARG, "dgemm: bad pointer or leading dimension");
+    if (m > INT32_MAX || n > INT32_MAX || k > INT32_MAX) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    ev_begin(c, 22);
+    tci::launch_dgemm(c->stream, transb != 0, (int)m, (int)n, (int)k, alpha, d_A, lda, d_B, ldb, beta, d_C,
+                      ldc, d_C, ldc, nullptr, nullptr);
+    ev_end(c);
+    HIPCHK(c, hipGetLastError());
+    return TCI_OK;
+}
+
+int tci_schur_update_d(tci_ctx* c, double* d_C, int64_t m, int64_t n, int64_t ldc,
+                       const double* d_W, int64_t ldw, const double* d_V, int64_t ldv, int64_t k) {
+    return tci_dgemm_d(c, 0, m, n, k, -1.0, d_W, ldw, d_V, ldv, 1.0, d_C, ldc);
+}
+
+int tci_diag_mfma_f64_ex(tci_ctx* c, int waves_per_simd, double* tflops, double* ghz) {
+    if (!c || !tflops || waves_per_simd < 1 || waves_per_simd > 4) return TCI_ERR_ARG;
+    const int w = waves_per_simd == 3 ? 2 : waves_per_simd;
+    const int grid = std::max(c->ncu, 1), iters = 2048;
+    int st;
+    if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(64 + grid)))) return st;
+    long long* cyc = reinterpret_cast<long long*>(c->dF2 + 64);
+    tci::launch_mfma_probe2(c->stream, w, grid, 64, c->dF2, cyc);  // warm
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    tci::launch_mfma_probe2(c->stream, w, grid, iters, c->dF2, cyc);
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventSynchronize(e1));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    std::vector<long long> h(grid);
+    HIPCHK(c, hipMemcpy(h.data(), cyc, grid * sizeof(long long), hipMemcpyDeviceToHost));
+    double mean = 0;
+    for (long long v : h) mean += (double)v;
+    mean /= grid;
+    const double flops = (double)grid * 4 * w * iters * 8 * (16.0 * 16 * 4 * 2);
+    *tflops = flops / (ms * 1e-3) / 1e12;
+    // clock64 counts shader-clock cycles: cycles of the loop / its wall time ~ the clock held
+    if (ghz) *ghz = mean / (ms * 1e-3) / 1e9;
     return TCI_OK;
 }
 
@@ -1416,7 +1499,7 @@ int tci_sitetensor_solve_c128_h(tci_ctx* c, const double* P, int64_t r, const do
     if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(2 * r * r)))) return st;
     if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(2 * R * r)))) return st;
     if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * (R * r + r * r))))) return st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)r))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
     HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * 16, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * 16, hipMemcpyHostToDevice, c->stream));
     double2* dT = reinterpret_cast<double2*>(c->dA);

@@ -1,0 +1,590 @@
+// tci_dense.hip -- fp64 dense linear algebra of the TCI2 path on v_mfma_f64_16x16x4f64 (gfx950):
+//  K3  the blocked Schur-complement update C -= W * V (k_dgemm): the trailing update of a blocked
+//      right-looking LU, and the GEMM of every blocked triangular solve below;
+//  K4  MatrixLUCI factors (matrixluci.jl:161-241): the factor GEMMs (L11 * U, L * U11) and the
+//      triangular solves (TRSMs at :207, :235) as diagonal-block solves + K3 updates;
+//  K5  setsitetensor!'s solve T = Pi1 * P^-1 (tensorci2.jl:620-627, `transpose(P) \ transpose(Pi1)`):
+//      a blocked right-looking getrf of P^T (partial pivoting; the panel factorised in LDS, the
+//      trailing update on K3) and a blocked getrs whose off-diagonal work is K3.
+// None of this is inside rrLU: exact full pivoting (matrixlu.jl:46-87) needs the fully updated
+// trailing block before every pivot. Here the reference itself calls LAPACK / BLAS
+// (Julia `\`, `*`), whose summation order it does not pin; parity is rtol 1e-12 (factors) /
+// 1e-10 (solve) against the oracle's loop-order restatement.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "tci_internal.h"
+
+namespace tci {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------ K3
+// Out = beta * C + alpha * A * op(B):  A (m x k, ld lda), op(B) = B (k x n, ld ldb) or, with TB,
+// B(t, j) = Bt[j + t * ldb] (Bt is n x k); C and Out column-major (Out may alias C); optional
+// row / column maps put result (i, j) at Out[rmap[i] + cmap[j] * ldo].
+// A workgroup of 4 waves owns a (32 FM) x (32 FN) tile, each wave a (16 FM) x (16 FN) block of
+// FM x FN MFMA accumulators. k advances 16 at a time through two LDS buffers: the global loads
+// of stage s + 1 are in flight while stage s runs on the matrix cores, one barrier per stage.
+// The MFMA's A operand is fed from op(B) and its B operand from A, so the accumulator holds the
+// transposed tile: lane l owns rows i = l & 15 (16 consecutive rows = a 128-B column segment per
+// store) of four columns -- coalesced epilogue stores for column-major C.
+constexpr int kDgKB = 16;
+
+struct DgemmArgs {
+    int m, n, k;
+    double alpha, beta;
+    const double* A;
+    int64_t lda;
+    const double* B;
+    int64_t ldb;
+    const double* C;
+    int64_t ldc;
+    double* Out;
+    int64_t ldo;
+    const int64_t* rmap;
+    const int64_t* cmap;
+    int tm, tn;  // tiles along m and n
+};
+
+template <int WM, int WN, int FM, int FN, bool TB>
+__global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
+    constexpr int LDA_S = BM + 8, LDB_S = BN + 8;  // padded rows against bank conflicts
+    constexpr int QA = kDgKB * BM / NT, QB = kDgKB * BN / NT;
+    __shared__ double As[2][kDgKB * LDA_S];
+    __shared__ double Bs[2][kDgKB * LDB_S];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // XCD-aware tile order: consecutive workgroup ids go to different XCDs round-robin; give each
+    // XCD a contiguous run of tiles (column-major over tiles: a run shares B's column panel)
+    const int nt = g.tm * g.tn;
+    int b = blockIdx.x;
+    if ((nt & 7) == 0) b = (b & 7) * (nt >> 3) + (b >> 3);
+    const int ti = b % g.tm, tj = b / g.tm;
+    const int i0 = ti * BM, j0 = tj * BN;
+    const int wr = (wv % WM) * 16 * FM, wc = (wv / WM) * 16 * FN;
+    const int r = lane & 15, kk = lane >> 4;
+
+    dbl4 acc[FM][FN];
+#pragma unroll
+    for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+    // staging coordinates are the same every stage: element (t, i) of the A stage and (t, j) of
+    // the B stage; global addresses advance by 16 lda / 16 ldb (or 16) per stage
+    double ra[QA], rb[QB];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int e = tid + q * NT, t = e / BM, i = e % BM;
+            const int gi = i0 + i, gt = k0 + t;
+            ra[q] = (gi < g.m && gt < g.k) ? g.A[(int64_t)gi + (int64_t)gt * g.lda] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int e = tid + q * NT;
+            int t, j;
+            if (TB) { t = e / BN; j = e % BN; }
+            else { t = e % kDgKB; j = e / kDgKB; }
+            const int gj = j0 + j, gt = k0 + t;
+            double v = 0.0;
+            if (gj < g.n && gt < g.k)
+                v = TB ? g.B[(int64_t)gj + (int64_t)gt * g.ldb] : g.B[(int64_t)gt + (int64_t)gj * g.ldb];
+            rb[q] = v;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int e = tid + q * NT, t = e / BM, i = e % BM;
+            As[buf][t * LDA_S + i] = ra[q];
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int e = tid + q * NT;
+            int t, j;
+            if (TB) { t = e / BN; j = e % BN; }
+            else { t = e % kDgKB; j = e / kDgKB; }
+            Bs[buf][t * LDB_S + j] = rb[q];
+        }
+    };
+
+    const int nst = (g.k + kDgKB - 1) / kDgKB;
+    load(0);
+    store(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = 0; s < nst; ++s) {
+        if (s + 1 < nst) load((s + 1) * kDgKB);
+        const double* as = As[cur];
+        const double* bs = Bs[cur];
+#pragma unroll
+        for (int k4 = 0; k4 < kDgKB; k4 += 4) {
+            double af[FM], bf[FN];
+#pragma unroll
+            for (int x = 0; x < FM; ++x) af[x] = as[(k4 + kk) * LDA_S + wr + 16 * x + r];
+#pragma unroll
+            for (int y = 0; y < FN; ++y) bf[y] = bs[(k4 + kk) * LDB_S + wc + 16 * y + r];
+#pragma unroll
+            for (int x = 0; x < FM; ++x)
+#pragma unroll
+                for (int y = 0; y < FN; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[y], af[x], acc[x][y], 0, 0, 0);
+        }
+        if (s + 1 < nst) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    // acc[x][y][q]: row i = wr + 16x + (lane & 15), column j = wc + 16y + (lane >> 4) + 4q
+#pragma unroll
+    for (int x = 0; x < FM; ++x) {
+        const int i = i0 + wr + 16 * x + r;
+        if (i >= g.m) continue;
+        const int64_t orow = g.rmap ? g.rmap[i] : i;
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j0 + wc + 16 * y + kk + 4 * q;
+                if (j >= g.n) continue;
+                double v = g.alpha * acc[x][y][q];
+                if (g.beta != 0.0) v = g.beta * g.C[(int64_t)i + (int64_t)j * g.ldc] + v;
+                const int64_t ocol = g.cmap ? g.cmap[j] : j;
+                g.Out[orow + ocol * g.ldo] = v;
+            }
+    }
+}
+
+// tile shapes: 128 x 128 (8 waves of 64 x 32), 128 x 64 (4 waves of 64 x 32), 64 x 64 (4 waves
+// of 32 x 32); every form stays within 256 registers per lane so that two waves share a SIMD --
+// the fp64 MFMA pipe needs two issuing waves per SIMD to reach its rate (tci_diag_mfma_f64_ex:
+// 33.5 TF with one wave per SIMD, 72.4 TF with two)
+template <bool TB>
+static void dgemm_go(hipStream_t s, DgemmArgs g) {
+    const long long t128 = (long long)((g.m + 127) / 128) * ((g.n + 127) / 128);
+    const long long t12864 = (long long)((g.m + 127) / 128) * ((g.n + 63) / 64);
+    if (t128 >= 256) {
+        g.tm = (g.m + 127) / 128;
+        g.tn = (g.n + 127) / 128;
+        hipLaunchKernelGGL((k_dgemm<2, 4, 4, 2, TB>), dim3(g.tm * g.tn), dim3(512), 0, s, g);
+    } else if (t12864 >= 256) {
+        g.tm = (g.m + 127) / 128;
+        g.tn = (g.n + 63) / 64;
+        hipLaunchKernelGGL((k_dgemm<2, 2, 4, 2, TB>), dim3(g.tm * g.tn), dim3(256), 0, s, g);
+    } else {
+        g.tm = (g.m + 63) / 64;
+        g.tn = (g.n + 63) / 64;
+        hipLaunchKernelGGL((k_dgemm<2, 2, 2, 2, TB>), dim3(g.tm * g.tn), dim3(256), 0, s, g);
+    }
+}
+
+void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
+                  int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
+                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap) {
+    if (m <= 0 || n <= 0) return;
+    DgemmArgs g{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, Out ? Out : const_cast<double*>(C),
+                Out ? ldo : ldc, rmap, cmap, 0, 0};
+    if (tb) dgemm_go<true>(s, g);
+    else dgemm_go<false>(s, g);
+}
+
+// ------------------------------------------------------------- diagonal-block triangular solve
+// For every right-hand side q < nrhs, the nb-vector x_q(j) = X[q * rs + j * es] (j < nb <= NB) is
+// replaced by the solution of its nb x nb triangular system, M(j, t) = Mb[j * mj + t * mt]:
+//   forward  (lower):  for t = 0, 1, ...:   x_t [/= M(t, t)];  x_j -= M(j, t) x_t  for j > t
+//   backward (upper):  for t = nb-1, ...:   x_t [/= M(t, t)];  x_j -= M(j, t) x_t  for j < t
+// (the column-oriented form of getrs's substitutions: the updates of one step are independent,
+// so a thread's chain has NB-way instruction-level parallelism). One thread per right-hand side,
+// x in registers, M in LDS (zero-padded past nb), separate multiply and subtract.
+template <int NB, bool BACKWARD, bool UNIT>
+__global__ __launch_bounds__(64) void k_trsm_diag(double* __restrict__ X, int64_t rs, int64_t es,
+                                                  int nrhs, const double* __restrict__ Mb, int64_t mj,
+                                                  int64_t mt, int nb) {
+    // the forward solve runs as the backward one on reversed indices (j' = nb - 1 - j), so both
+    // share one loop body (hipcc hoists every LDS read of a fully unrolled forward body and spills)
+    __shared__ double Ms[NB * NB];  // Ms[t * NB + j] = M(j, t) in the backward numbering
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int j = e % NB, t = e / NB;
+        double v = j == t ? 1.0 : 0.0;
+        if (j < nb && t < nb) {
+            const int jj = BACKWARD ? j : nb - 1 - j, tt = BACKWARD ? t : nb - 1 - t;
+            v = Mb[(int64_t)jj * mj + (int64_t)tt * mt];
+        }
+        Ms[e] = v;
+    }
+    __syncthreads();
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nrhs) return;
+    double* xp = X + (int64_t)q * rs;
+    double x[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) x[j] = j < nb ? xp[(int64_t)(BACKWARD ? j : nb - 1 - j) * es] : 0.0;
+#pragma unroll
+    for (int t = NB - 1; t >= 0; --t) {
+        if (!UNIT) x[t] = x[t] / Ms[t * NB + t];
+#pragma unroll
+        for (int j = 0; j < t; ++j) x[j] = __dsub_rn(x[j], __dmul_rn(Ms[t * NB + j], x[t]));
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+        if (j < nb) xp[(int64_t)(BACKWARD ? j : nb - 1 - j) * es] = x[j];
+}
+
+constexpr int kDiagNB = 32;  // diagonal kernel width (x in 64 VGPRs)
+constexpr int kTrsmNB = 64;  // block width of the blocked solves (the K3 depth of their updates)
+
+static void trsm_diag32(hipStream_t s, double* X, int64_t rs, int64_t es, int nrhs, const double* Mb,
+                        int64_t mj, int64_t mt, int nb, bool backward, bool unit) {
+    if (nrhs <= 0 || nb <= 0) return;
+    // 64-thread workgroups: the per-thread chains are long, spread them over every CU
+    const dim3 grid((nrhs + 63) / 64), blk(64);
+    if (backward && unit)
+        hipLaunchKernelGGL((k_trsm_diag<kDiagNB, true, true>), grid, blk, 0, s, X, rs, es, nrhs, Mb, mj, mt, nb);
+    else if (backward)
+        hipLaunchKernelGGL((k_trsm_diag<kDiagNB, true, false>), grid, blk, 0, s, X, rs, es, nrhs, Mb, mj, mt, nb);
+    else if (unit)
+        hipLaunchKernelGGL((k_trsm_diag<kDiagNB, false, true>), grid, blk, 0, s, X, rs, es, nrhs, Mb, mj, mt, nb);
+    else
+        hipLaunchKernelGGL((k_trsm_diag<kDiagNB, false, false>), grid, blk, 0, s, X, rs, es, nrhs, Mb, mj, mt,
+                           nb);
+}
+
+// A diagonal block of up to 64: two 32-wide diagonal solves and the K3 update between them.
+// Either the right-hand sides are rows (rs == 1: X(q, j) = X[q + j es]) or columns (es == 1:
+// X(q, j) = X[j + q rs]); M(j, t) = Mb[j mj + t mt] with mj == 1 or mt == 1.
+static void trsm_diag(hipStream_t s, double* X, int64_t rs, int64_t es, int nrhs, const double* Mb,
+                      int64_t mj, int64_t mt, int nb, bool backward, bool unit) {
+    if (nb <= kDiagNB) {
+        trsm_diag32(s, X, rs, es, nrhs, Mb, mj, mt, nb, backward, unit);
+        return;
+    }
+    const int h = kDiagNB, nb2 = nb - h;
+    const bool rows = rs == 1;
+    double* X1 = X + (int64_t)h * es;  // second half
+    if (!backward) {
+        trsm_diag32(s, X, rs, es, nrhs, Mb, mj, mt, h, false, unit);
+        // x_j -= sum_{t < h} M(j, t) x_t for j >= h
+        const double* Mq = Mb + (int64_t)h * mj;  // M(h + j', t) = Mq[j' mj + t mt]
+        if (rows) {
+            if (mj == 1) launch_dgemm(s, true, nrhs, nb2, h, -1.0, X, es, Mq, mt, 1.0, X1, es, nullptr, 0, nullptr, nullptr);
+            else launch_dgemm(s, false, nrhs, nb2, h, -1.0, X, es, Mq, mj, 1.0, X1, es, nullptr, 0, nullptr, nullptr);
+        } else {  // C (nb2 x nrhs) = X1, A (j', t) = Mq (mj == 1, ld mt), B = X (h x nrhs, ld rs)
+            launch_dgemm(s, false, nb2, nrhs, h, -1.0, Mq, mt, X, rs, 1.0, X1, rs, nullptr, 0, nullptr, nullptr);
+        }
+        trsm_diag32(s, X1, rs, es, nrhs, Mb + (int64_t)h * mj + (int64_t)h * mt, mj, mt, nb2, false, unit);
+    } else {
+        trsm_diag32(s, X1, rs, es, nrhs, Mb + (int64_t)h * mj + (int64_t)h * mt, mj, mt, nb2, true, unit);
+        // x_j -= sum_{t >= h} M(j, t) x_t for j < h
+        const double* Mq = Mb + (int64_t)h * mt;  // M(j, h + t') = Mq[j mj + t' mt]
+        if (rows) {
+            if (mj == 1) launch_dgemm(s, true, nrhs, h, nb2, -1.0, X1, es, Mq, mt, 1.0, X, es, nullptr, 0, nullptr, nullptr);
+            else launch_dgemm(s, false, nrhs, h, nb2, -1.0, X1, es, Mq, mj, 1.0, X, es, nullptr, 0, nullptr, nullptr);
+        } else {
+            launch_dgemm(s, false, h, nrhs, nb2, -1.0, Mq, mt, X1, rs, 1.0, X, rs, nullptr, 0, nullptr, nullptr);
+        }
+        trsm_diag32(s, X, rs, es, nrhs, Mb, mj, mt, h, true, unit);
+    }
+}
+
+// ------------------------------------------------------------------------ K4 MatrixLUCI factors
+// leftorth: left = colstimespivotinv, i.e. X L11 = L21 (L11 unit lower; matrixluci.jl:194-213),
+// solved in place over L's rows np..m-1, left-looking over 64-column blocks right to left: the
+// K3 update X[:, jb:je] -= X[:, je:np] L11[je:np, jb:je] (K = np - je), then the diagonal block.
+void trsm_luci_left(hipStream_t s, double* L, int64_t ldl, int m, int np) {
+    const int rows = m - np;
+    if (rows <= 0) return;
+    double* X = L + np;
+    for (int jb = ((np - 1) / kTrsmNB) * kTrsmNB; jb >= 0; jb -= kTrsmNB) {
+        const int nb = std::min(kTrsmNB, np - jb), je = jb + nb;
+        if (je < np)
+            launch_dgemm(s, false, rows, nb, np - je, -1.0, X + (int64_t)je * ldl, ldl,
+                         L + je + (int64_t)jb * ldl, ldl, 1.0, X + (int64_t)jb * ldl, ldl, nullptr, 0,
+                         nullptr, nullptr);
+        // x_j -= sum_{t > j} x_t L11[t, j]: M(j, t) = L[t + j ldl]
+        trsm_diag(s, X + (int64_t)jb * ldl, 1, ldl, rows, L + jb + (int64_t)jb * ldl, ldl, 1, nb,
+                  true, true);
+    }
+}
+
+// !leftorth: right = pivotinvtimesrows, U11 X = U12 (U11 unit upper; matrixluci.jl:227-241), in
+// place over U's columns np..n-1, diagonal blocks bottom to top, each followed by the K3 update
+// of the rows above it: U12[0:jb, :] -= U11[0:jb, jb:je] X[jb:je, :] (right-looking: the
+// right-hand sides are columns here, so the rows above give the update its tiles).
+void trsm_luci_right(hipStream_t s, double* U, int64_t ldu, int n, int np) {
+    const int cols = n - np;
+    if (cols <= 0) return;
+    double* X = U + (int64_t)np * ldu;
+    for (int jb = ((np - 1) / kTrsmNB) * kTrsmNB; jb >= 0; jb -= kTrsmNB) {
+        const int nb = std::min(kTrsmNB, np - jb);
+        // x_a -= sum_{t > a} U11[a, t] x_t: M(a, t) = U[a + t ldu]
+        trsm_diag(s, X + jb, ldu, 1, cols, U + jb + (int64_t)jb * ldu, 1, ldu, nb, true, true);
+        if (jb > 0)
+            launch_dgemm(s, false, jb, cols, nb, -1.0, U + (int64_t)jb * ldu, ldu, X + jb, ldu, 1.0, X,
+                         ldu, nullptr, 0, nullptr, nullptr);
+    }
+}
+
+// ------------------------------------------------------------------------- K5 site-tensor solve
+// getrf of A = P^T (r x r) in place: panels of nbp columns, factorised in LDS by one workgroup
+// (partial pivoting: first maximal |a| of the updated column, as idamax), their interchanges
+// applied to the other columns, U12 = L11^-1 A12 (unit lower), then the K3 trailing update
+// A22 -= L21 U12. Same pivot rule as the unblocked k_getrf_transposed; values differ from it
+// only by the summation order of the updates.
+__global__ void k_transpose_sq(double* __restrict__ P, int r) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)r * r; e += stride) {
+        const int i = (int)(e % r), j = (int)(e / r);
+        if (i < j) {
+            const double a = P[i + (int64_t)j * r], b = P[j + (int64_t)i * r];
+            P[i + (int64_t)j * r] = b;
+            P[j + (int64_t)i * r] = a;
+        }
+    }
+}
+
+constexpr int kPanelLds = 128 * 1024;  // bytes of LDS for one panel
+
+// One workgroup factorises the panel in LDS, thread t owning rows t, t + 1024, ... Per column c:
+// the argmax partials of the rows >= c (computed in the previous step's update), one barrier,
+// every thread reduces the 16 wave results itself (no second barrier), the nbp-wide row swap c <->
+// p, one barrier, then each thread scales its rows and applies the rank-1 update to them, taking
+// the next column's argmax partial on the way.
+__global__ __launch_bounds__(1024) void k_getrf_panel(double* __restrict__ A, int r, int jb, int nbp,
+                                                      int* __restrict__ piv) {
+    extern __shared__ __attribute__((aligned(16))) double Ps[];  // [c][row - jb], ld = rows
+    __shared__ double sv[16];
+    __shared__ int si[16];
+    const int rows = r - jb, tid = threadIdx.x, nth = blockDim.x, nw = nth >> 6;
+    for (int e = tid; e < rows * nbp; e += nth) {
+        const int i = e % rows, c = e / rows;
+        Ps[e] = A[(int64_t)(jb + i) + (int64_t)(jb + c) * r];
+    }
+    __syncthreads();
+    // partial argmax of column 0
+    double bv = -1.0;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < rows; i += nth) {
+        const double v = fabs(Ps[i]);
+        if (v > bv) { bv = v; bi = i; }  // ascending i: first maximum
+    }
+    for (int c = 0; c < nbp; ++c) {
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double v2 = __shfl_xor(bv, off);
+            const int i2 = __shfl_xor(bi, off);
+            if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
+        }
+        if ((tid & 63) == 0) { sv[tid >> 6] = bv; si[tid >> 6] = bi; }
+        __syncthreads();
+        double b = sv[0];
+        int p = si[0];
+        for (int q = 1; q < nw; ++q)
+            if (sv[q] > b || (sv[q] == b && si[q] < p)) { b = sv[q]; p = si[q]; }
+        if (p == 0x7fffffff) p = c;
+        if (tid == 0) piv[jb + c] = jb + p;
+        if (p != c && tid < nbp) {
+            const double t = Ps[(int64_t)tid * rows + c];
+            Ps[(int64_t)tid * rows + c] = Ps[(int64_t)tid * rows + p];
+            Ps[(int64_t)tid * rows + p] = t;
+        }
+        __syncthreads();  // also orders this step's reads of sv/si before the next step's writes
+        const double* col = Ps + (int64_t)c * rows;
+        const double d = col[c];
+        bv = -1.0;
+        bi = 0x7fffffff;
+        for (int i = c + 1 + tid; i < rows; i += nth) {
+            const double l = col[i] / d;
+            Ps[(int64_t)c * rows + i] = l;
+            for (int cc = c + 1; cc < nbp; ++cc) {
+                double* o = Ps + (int64_t)cc * rows;
+                o[i] = __dsub_rn(o[i], __dmul_rn(l, o[c]));
+            }
+            if (c + 1 < nbp) {
+                const double v = fabs(Ps[(int64_t)(c + 1) * rows + i]);
+                if (v > bv) { bv = v; bi = i; }
+            }
+        }
+        // row c + 1 itself was updated above by its owner; column c + 1's candidates are rows > c
+    }
+    __syncthreads();
+    for (int e = tid; e < rows * nbp; e += nth) {
+        const int i = e % rows, c = e / rows;
+        A[(int64_t)(jb + i) + (int64_t)(jb + c) * r] = Ps[e];
+    }
+}
+
+// The panel's interchanges applied to every column outside it (laswp). They compose to a
+// permutation of at most 2 nbp rows (the panel's and the rows swapped into it), computed once per
+// workgroup in LDS: every thread (one per column) then moves its column's affected values with
+// independent loads and stores instead of nbp dependent swaps.
+template <int NBP>
+__global__ __launch_bounds__(256) void k_getrf_swap(double* __restrict__ A, int r, int jb, int nbp,
+                                                    const int* __restrict__ piv) {
+    __shared__ int pos[2 * NBP];  // affected row positions
+    __shared__ int src[2 * NBP];  // final content of pos[q]: the original row src[q]
+    __shared__ int naff;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        // wave 0 composes the interchanges: lane l holds slots l and l + 64 (pos, src); the
+        // search for row p is a ballot, the swap two readlanes
+        const int l = tid;
+        int pos0 = l < nbp ? jb + l : -1, src0 = pos0;
+        int pos1 = -1, src1 = -1;
+        int n = nbp;
+        for (int k = 0; k < nbp; ++k) {
+            const int p = piv[jb + k];
+            const unsigned long long b0 = __ballot(pos0 == p), b1 = __ballot(pos1 == p);
+            int qp;
+            if (b0) qp = __ffsll((long long)b0) - 1;
+            else if (b1) qp = 64 + __ffsll((long long)b1) - 1;
+            else {
+                qp = n++;
+                if (qp < 64) { if (l == qp) { pos0 = p; src0 = p; } }
+                else if (l == qp - 64) { pos1 = p; src1 = p; }
+            }
+            const int sk = __shfl(src0, k);  // k < nbp <= 64: slot k is in the first half
+            const int sp = qp < 64 ? __shfl(src0, qp) : __shfl(src1, qp - 64);
+            if (l == k) src0 = sp;
+            if (qp < 64) { if (l == qp) src0 = sk; }
+            else if (l == qp - 64) src1 = sk;
+        }
+        if (l < 2 * NBP) { pos[l] = pos0; src[l] = src0; }
+        if (l + 64 < 2 * NBP) { pos[l + 64] = pos1; src[l + 64] = src1; }
+        if (l == 0) naff = n;
+    }
+    __syncthreads();
+    const int cidx = blockIdx.x * blockDim.x + tid, nother = r - nbp;
+    if (cidx >= nother) return;
+    const int c = cidx < jb ? cidx : cidx + nbp;
+    double* col = A + (int64_t)c * r;
+    const int n = naff;
+    double v[2 * NBP];
+#pragma unroll
+    for (int q = 0; q < 2 * NBP; ++q)
+        if (q < n) v[q] = col[src[q]];
+#pragma unroll
+    for (int q = 0; q < 2 * NBP; ++q)
+        if (q < n) col[pos[q]] = v[q];
+}
+
+static int panel_width(int rows) {
+    int nbp = 64;
+    while (nbp > 4 && (int64_t)rows * nbp * 8 > kPanelLds) nbp >>= 1;
+    return nbp;
+}
+
+bool getrf_blocked_fits(int r) { return (int64_t)r * 4 * 8 <= kPanelLds; }
+
+void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv) {
+    hipLaunchKernelGGL(k_transpose_sq, dim3(std::min(2048, std::max(1, (r * r + 255) / 256))), dim3(256), 0, s,
+                       A, r);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_getrf_panel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        kPanelLds);
+    for (int jb = 0; jb < r;) {
+        const int rows = r - jb;
+        const int nbp = std::min(panel_width(rows), rows);
+        hipLaunchKernelGGL(k_getrf_panel, dim3(1), dim3(1024), (size_t)rows * nbp * 8, s, A, r, jb, nbp, piv);
+        const int je = jb + nbp, nother = r - nbp;
+        if (nother > 0) {
+            const dim3 g((nother + 255) / 256), b(256);
+            if (nbp <= 8) hipLaunchKernelGGL(k_getrf_swap<8>, g, b, 0, s, A, r, jb, nbp, piv);
+            else if (nbp <= 16) hipLaunchKernelGGL(k_getrf_swap<16>, g, b, 0, s, A, r, jb, nbp, piv);
+            else if (nbp <= 32) hipLaunchKernelGGL(k_getrf_swap<32>, g, b, 0, s, A, r, jb, nbp, piv);
+            else hipLaunchKernelGGL(k_getrf_swap<64>, g, b, 0, s, A, r, jb, nbp, piv);
+        }
+        // U12 = L11^-1 A12: right-hand sides are the columns je..r-1, M(j, t) = A[jb + j, jb + t]
+        if (je < r)
+            trsm_diag(s, A + jb + (int64_t)je * r, r, 1, r - je, A + jb + (int64_t)jb * r, 1, r, nbp, false, true);
+        if (je < r)
+            launch_dgemm(s, false, r - je, r - je, nbp, -1.0, A + je + (int64_t)jb * r, r,
+                         A + jb + (int64_t)je * r, r, 1.0, A + je + (int64_t)je * r, r,
+                         A + je + (int64_t)je * r, r, nullptr, nullptr);
+        jb = je;
+    }
+}
+
+// T (R x r) = Pi1 P^-1 given A = LU(P^T) and its interchanges: T's columns permuted as the rows of
+// P^T were (k_gather_cols), then T <- T L^-T (forward, unit) and T <- T U^-T (backward), each as
+// kTrsmNB-wide diagonal solves (one thread per row of T) and K3 updates.
+__global__ void k_piv_to_perm(const int* __restrict__ piv, int r, int* __restrict__ perm) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int a = 0; a < r; ++a) perm[a] = a;
+    for (int k = 0; k < r; ++k) {
+        const int p = piv[k];
+        const int t = perm[k];
+        perm[k] = perm[p];
+        perm[p] = t;
+    }
+}
+
+__global__ void k_gather_cols(const double* __restrict__ Pi1, int R, int r, const int* __restrict__ perm,
+                              double* __restrict__ T) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = gid; e < (int64_t)R * r; e += stride) {
+        const int q = (int)(e % R), a = (int)(e / R);
+        T[e] = Pi1[(int64_t)q + (int64_t)perm[a] * R];
+    }
+}
+
+void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv, const double* Pi1,
+                          int R, double* T, int* perm) {
+    hipLaunchKernelGGL(k_piv_to_perm, dim3(1), dim3(1), 0, s, piv, r, perm);
+    const long long work = (long long)R * r;
+    hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)std::min<long long>(8192, (work + 255) / 256)), dim3(256),
+                       0, s, Pi1, R, r, perm, T);
+    // left-looking over 64-column blocks of T: each block is brought up to date by one K3 update
+    // from the blocks already solved (K = jb, written once), then its diagonal block is solved
+    for (int jb = 0; jb < r; jb += kTrsmNB) {  // L: unit lower, M(j, t) = A[j + t r]
+        const int nb = std::min(kTrsmNB, r - jb);
+        if (jb > 0)  // T[:, jb:je] -= T[:, 0:jb] L[jb:je, 0:jb]^T
+            launch_dgemm(s, true, R, nb, jb, -1.0, T, R, A + jb, r, 1.0, T + (int64_t)jb * R, R, nullptr, 0,
+                         nullptr, nullptr);
+        trsm_diag(s, T + (int64_t)jb * R, 1, R, R, A + jb + (int64_t)jb * r, 1, r, nb, false, true);
+    }
+    for (int jb = ((r - 1) / kTrsmNB) * kTrsmNB; jb >= 0; jb -= kTrsmNB) {  // U, with its diagonal
+        const int nb = std::min(kTrsmNB, r - jb), je = jb + nb;
+        if (je < r)  // T[:, jb:je] -= T[:, je:r] U[jb:je, je:r]^T
+            launch_dgemm(s, true, R, nb, r - je, -1.0, T + (int64_t)je * R, R, A + jb + (int64_t)je * r, r, 1.0,
+                         T + (int64_t)jb * R, R, nullptr, 0, nullptr, nullptr);
+        trsm_diag(s, T + (int64_t)jb * R, 1, R, R, A + jb + (int64_t)jb * r, 1, r, nb, true, false);
+    }
+}
+
+// ------------------------------------------------------------------------- MFMA probe (diag)
+// Independent v_mfma_f64_16x16x4f64 chains, W waves per SIMD (256 * W threads per workgroup, one
+// workgroup per CU); cycles[blockIdx] = s_memtime cycles of wave 0's loop (the shader clock), so
+// the host gets both the rate and the clock it ran at.
+template <int W>
+__global__ __launch_bounds__(256 * W) void k_mfma_probe2(int iters, double* sink, long long* cycles) {
+    dbl4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+    const long long t0 = clock64();
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q], 0, 0, 0);
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+    const long long t1 = clock64();
+    if (threadIdx.x == 0) cycles[blockIdx.x] = t1 - t0;
+    if (s == 12345.0) sink[0] = s;
+}
+
+void launch_mfma_probe2(hipStream_t s, int waves_per_simd, int grid, int iters, double* sink,
+                        long long* cycles) {
+    switch (waves_per_simd) {
+        case 1: hipLaunchKernelGGL(k_mfma_probe2<1>, dim3(grid), dim3(256), 0, s, iters, sink, cycles); break;
+        case 2: hipLaunchKernelGGL(k_mfma_probe2<2>, dim3(grid), dim3(512), 0, s, iters, sink, cycles); break;
+        default: hipLaunchKernelGGL(k_mfma_probe2<4>, dim3(grid), dim3(1024), 0, s, iters, sink, cycles); break;
+    }
+}
+
+}  // namespace tci

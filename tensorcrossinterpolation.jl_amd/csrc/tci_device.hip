@@ -5,8 +5,10 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
-#include <algorithm>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "tci_internal.h"
 
@@ -189,26 +191,45 @@ __global__ void k_right_scatter_ro(const double* __restrict__ U, int64_t ldu, in
 }
 
 
+void trsm_luci_left(hipStream_t s, double* L, int64_t ldl, int m, int np);
+void trsm_luci_right(hipStream_t s, double* U, int64_t ldu, int n, int np);
+void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
+                  int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
+                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap);
+
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
-                         const int64_t* colperm, double* left, double* right) {
+                         const int64_t* colperm, double* left, double* right, int dense) {
     if (np <= 0) return;
+    const bool mf = dense & kDenseLuci;
     if (leftorth) {
         // right first: it reads the untouched L11; the TRSM then overwrites L21 in place
-        if (right)
-            hipLaunchKernelGGL(k_right_gemm_lo, dim3(grid_for((long long)np * n, 8192)), dim3(256),
-                               0, s, L, ldl, U, ldu, n, np, colperm, right);
+        if (right) {
+            if (mf)  // rowmatrix = L11 * U (K = np), columns scattered by colperm
+                launch_dgemm(s, false, np, n, np, 1.0, L, ldl, U, ldu, 0.0, nullptr, 0, right, np, nullptr,
+                             colperm);
+            else
+                hipLaunchKernelGGL(k_right_gemm_lo, dim3(grid_for((long long)np * n, 8192)), dim3(256),
+                                   0, s, L, ldl, U, ldu, n, np, colperm, right);
+        }
         if (left) {
-            launch_trsm<true>(s, L, ldl, np, m, np);
+            if (mf) trsm_luci_left(s, L, ldl, m, np);
+            else launch_trsm<true>(s, L, ldl, np, m, np);
             hipLaunchKernelGGL(k_left_scatter_lo, dim3(grid_for((long long)m * np, 8192)), dim3(256),
                                0, s, L, ldl, m, np, rowperm, left);
         }
     } else {
-        if (left)
-            hipLaunchKernelGGL(k_left_gemm_ro, dim3(grid_for((long long)m * np, 8192)), dim3(256), 0,
-                               s, L, ldl, U, ldu, m, np, rowperm, left);
+        if (left) {
+            if (mf)  // colmatrix = L * U11 (K = np), rows scattered by rowperm
+                launch_dgemm(s, false, m, np, np, 1.0, L, ldl, U, ldu, 0.0, nullptr, 0, left, m, rowperm,
+                             nullptr);
+            else
+                hipLaunchKernelGGL(k_left_gemm_ro, dim3(grid_for((long long)m * np, 8192)), dim3(256), 0,
+                                   s, L, ldl, U, ldu, m, np, rowperm, left);
+        }
         if (right) {
-            launch_trsm<false>(s, U, ldu, np, n, np);
+            if (mf) trsm_luci_right(s, U, ldu, n, np);
+            else launch_trsm<false>(s, U, ldu, np, n, np);
             hipLaunchKernelGGL(k_right_scatter_ro, dim3(grid_for((long long)np * n, 8192)),
                                dim3(256), 0, s, U, ldu, n, np, colperm, right);
         }
@@ -1272,10 +1293,22 @@ __global__ __launch_bounds__(256) void k_getrs_blocked(const double* __restrict_
     }
 }
 
+bool getrf_blocked_fits(int r);
+void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv);
+void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv, const double* Pi1,
+                          int R, double* T, int* perm);
+
+// piv: 2 r ints (interchanges, then the permutation they compose to)
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
-                             int* piv) {
-    hipLaunchKernelGGL(k_getrf_transposed, dim3(1), dim3(1024), 0, s, P, r, piv);
-    if (r > 4096 || R <= 0) {
+                             int* piv, int dense) {
+    if ((dense & kDenseGetrf) && getrf_blocked_fits(r)) launch_getrf_blocked(s, P, r, piv);
+    else hipLaunchKernelGGL(k_getrf_transposed, dim3(1), dim3(1024), 0, s, P, r, piv);
+    if (R <= 0) return;
+    if (dense & kDenseGetrs) {
+        launch_getrs_blocked(s, P, r, piv, Pi1, R, T, piv + r);
+        return;
+    }
+    if (r > 4096) {
         hipLaunchKernelGGL(k_getrs_rows, dim3((R + 127) / 128), dim3(128), 0, s, P, r, piv, Pi1, R, T);
         return;
     }

@@ -185,9 +185,12 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
 // ---- factors, batch evaluation, solve (tci_device.hip)
 // MatrixLUCI factors from position-order L (m x np) / U (np x n); L rows >= np (leftorth) or U
 // columns >= np (otherwise) are overwritten by the triangular solve.
+// dense: bit mask of the fp64 MFMA forms (tci_dense.hip) to use, kDense* below; 0 = the
+// round-1 scalar GEMMs / LDS TRSMs / single-workgroup getrf (kept for A/B)
+constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseAll = 7;
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
-                         const int64_t* colperm, double* left, double* right);
+                         const int64_t* colperm, double* left, double* right, int dense);
 void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed);
 void launch_stream_read(hipStream_t s, const double* a, int64_t n, unsigned long long* out, int grid);
 void launch_stream_copy(hipStream_t s, const double* a, double* b, int64_t n, int grid);
@@ -200,6 +203,16 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
                       unsigned long long* maxbits, void* scratch);
 int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n);
 
+// ---- fp64 MFMA dense algebra (tci_dense.hip)
+// Out = beta C + alpha A op(B) (op(B) = B, or with tb B(t, j) = B[j + t ldb]); Out null: in place
+// in C; rmap / cmap (nullable) scatter result (i, j) to Out[rmap[i] + cmap[j] ldo].
+void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
+                  int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
+                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap);
+// probe: waves_per_simd in {1, 2, 4}, one workgroup per CU; cycles[grid]: clock64 cycles of the loop
+void launch_mfma_probe2(hipStream_t s, int waves_per_simd, int grid, int iters, double* sink,
+                        long long* cycles);
+
 // diagnostic fp64 MFMA throughput probe: grid x 256 threads, iters x 8 x v_mfma_f64_16x16x4 per wave
 void launch_mfma_f64_probe(hipStream_t s, int grid, int iters, double* sink);
 
@@ -208,7 +221,8 @@ void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, cons
                     const int32_t* dims, int L, const int32_t* X, int npts, double* out, int rmax);
 
 // site-tensor solve: T (R x r) = Pi1 (R x r) * P^-1; P overwritten by its LU (partial pivot of P^T)
+// piv: 2 r ints
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
-                             int* piv);
+                             int* piv, int dense);
 
 }  // namespace tci

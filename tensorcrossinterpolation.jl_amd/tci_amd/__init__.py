@@ -11,8 +11,9 @@ from .cachedfunction import CachedFunction
 from .contraction import Contraction, contract, contract_naive, contract_TCI
 from .distributed import Comm, ShardedBatchEvaluator, column_blocks
 from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder
-from .matrixlu import (DeviceMatrix, colindices, diag, lastpivoterror, ldiv, left, npivots, pivoterrors,
-                       right, rowindices, rrLU, rrlu, rrlu_inplace_device)
+from .matrixlu import (DeviceMatrix, colindices, dgemm_device, diag, lastpivoterror, ldiv, left, npivots,
+                       pivoterrors, right, rowindices, rrLU, rrlu, rrlu_inplace_device, schur_update_device,
+                       sitetensor_solve_device)
 from .matrixluci import MatrixLUCI
 from .tensorci2 import (TensorCI2, convergencecriterion, crossinterpolate2, forwardsweep, kronecker_left, optfirstpivot,
                         kronecker_right, union_sets)

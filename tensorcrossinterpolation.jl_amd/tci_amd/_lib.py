@@ -56,6 +56,7 @@ SIGNATURES = {
     "tci_set_rrlu_small": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_mid": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_shadow": ([vp, C.c_int], C.c_int),
+    "tci_set_dense_mfma": ([vp, C.c_int], C.c_int),
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
@@ -84,6 +85,10 @@ SIGNATURES = {
     "tci_fill_uniform_d": ([vp, vp, i64, i64, i64, C.c_uint64], C.c_int),
     "tci_diag_stream_d": ([vp, vp, vp, i64, C.c_int, C.c_int, pdbl, pdbl], C.c_int),
     "tci_diag_mfma_f64": ([vp, pdbl], C.c_int),
+    "tci_diag_mfma_f64_ex": ([vp, C.c_int, pdbl, pdbl], C.c_int),
+    "tci_sitetensor_solve_d": ([vp, vp, i64, vp, i64, vp], C.c_int),
+    "tci_dgemm_d": ([vp, C.c_int, i64, i64, i64, dbl, vp, i64, vp, i64, dbl, vp, i64], C.c_int),
+    "tci_schur_update_d": ([vp, vp, i64, i64, i64, vp, i64, vp, i64, i64], C.c_int),
     "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
     "tci_free_d": ([vp, vp], C.c_int),
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),

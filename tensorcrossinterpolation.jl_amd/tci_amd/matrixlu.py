@@ -214,6 +214,17 @@ class DeviceMatrix:
         assert other.ld == self.ld and other.n == self.n
         self.ctx.check(self.ctx.lib.tci_memcpy_d2d(self.ctx.h, self.ptr, other.ptr, self.nbytes))
 
+    def upload(self, A):
+        """Copies a host m x n array in (padded to ld)."""
+        A = np.asarray(A, dtype=np.float64)
+        if A.shape != (self.m, self.n):
+            raise ValueError(f"upload: shape {A.shape} != {(self.m, self.n)}")
+        buf = np.zeros((self.ld, max(self.n, 1)), order="F")
+        buf[: self.m, : self.n] = A
+        self.ctx.check(self.ctx.lib.tci_memcpy_h2d(self.ctx.h, self.ptr, _lib.ptr(buf.ravel(order="F")),
+                                                   self.nbytes))
+        return self
+
     def to_host(self):
         buf = np.empty(self.ld * max(self.n, 1))
         self.ctx.check(self.ctx.lib.tci_memcpy_d2h(self.ctx.h, _lib.ptr(buf), self.ptr, self.nbytes))
@@ -250,3 +261,29 @@ def rrlu_inplace_device(dm, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftort
                                          C.byref(err), _lib.ptr(pe)))
     k = npv.value
     return k, err.value, rowperm, colperm, pe[: k + 1]
+
+
+def dgemm_device(A, B, C_, alpha=1.0, beta=0.0, transb=False, k=None):
+    """C = beta C + alpha A op(B) on DeviceMatrix operands (fp64 MFMA, K3 of DESIGN.md):
+    op(B) = B (k x n) or, transb, B^T (B n x k). Asynchronous on the context stream."""
+    ctx = C_.ctx
+    k = A.n if k is None else int(k)
+    ctx.check(ctx.lib.tci_dgemm_d(ctx.h, int(bool(transb)), C_.m, C_.n, k, float(alpha), A.ptr, A.ld,
+                                  B.ptr, B.ld, float(beta), C_.ptr, C_.ld))
+
+
+def schur_update_device(C_, W, V):
+    """C -= W V (the blocked Schur-complement update of a right-looking LU) on DeviceMatrix
+    operands: C m x n, W m x k, V k x n."""
+    ctx = C_.ctx
+    ctx.check(ctx.lib.tci_schur_update_d(ctx.h, C_.ptr, C_.m, C_.n, C_.ld, W.ptr, W.ld, V.ptr, V.ld, W.n))
+
+
+def sitetensor_solve_device(P, Pi1, T_):
+    """T = Pi1 P^-1 (setsitetensor!'s solve, tensorci2.jl:620-627) on DeviceMatrix operands with
+    ld = rows (P r x r is clobbered by its LU; Pi1, T R x r)."""
+    ctx = T_.ctx
+    r, R = P.m, Pi1.m
+    if P.ld != r or Pi1.ld != R or T_.ld != R or P.n != r or Pi1.n != r or T_.m != R or T_.n != r:
+        raise ValueError("sitetensor_solve_device: P r x r, Pi1 and T R x r with ld = rows")
+    ctx.check(ctx.lib.tci_sitetensor_solve_d(ctx.h, P.ptr, r, Pi1.ptr, R, T_.ptr))

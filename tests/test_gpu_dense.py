@@ -1,0 +1,101 @@
+"""fp64 MFMA dense algebra (tci_dense.hip), through the C ABI:
+
+* K3 `tci_dgemm_d` / `tci_schur_update_d` against numpy fp64 (ragged tiles, k = 0, k not a
+  multiple of the 16-deep LDS stage, B and B^T), tolerance |err| <= 4 k eps sum|a||b| per entry
+  (MFMA accumulates with one rounding per fused step, numpy/OpenBLAS in its own blocked order);
+* K5 the blocked getrf/getrs of setsitetensor!'s solve `T = Pi1 * P^-1` (tensorci2.jl:620-627)
+  at r in {256, 1024} against the oracle's loop-order restatement (rtol 1e-10, the site-tensor
+  bar of DESIGN.md section 3);
+* K4 MatrixLUCI factors with np in {256, 1024} (matrixluci.jl:161-241) against the oracle at
+  rtol 1e-12 (pivots bitwise: the rrLU is unchanged).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+T = pytest.importorskip("tci_amd")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+def _dev(ctx, A, tight=False):
+    A = np.asarray(A, dtype=np.float64)
+    return T.DeviceMatrix(A.shape[0], A.shape[1], ctx=ctx, ld=A.shape[0] if tight else None).upload(A)
+
+
+def _bound(A, B, k):
+    return 4 * max(k, 1) * np.finfo(float).eps * (np.abs(A) @ np.abs(B)) + 1e-300
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (17, 33, 5), (200, 130, 64), (1000, 700, 37), (129, 257, 0),
+                                   (2100, 1500, 100)])
+@pytest.mark.parametrize("transb", [False, True])
+def test_dgemm_vs_numpy(ctx, m, n, k, transb):
+    rng = np.random.default_rng(m * 7 + n + k)
+    A = rng.standard_normal((m, max(k, 1)))[:, :k]
+    Bop = rng.standard_normal((max(k, 1), n))[:k, :]
+    C0 = rng.standard_normal((m, n))
+    dA = _dev(ctx, A) if k else T.DeviceMatrix(m, 1, ctx=ctx)
+    dB = _dev(ctx, Bop.T if transb else Bop) if k else T.DeviceMatrix(max(n, 1), 1, ctx=ctx)
+    dC = _dev(ctx, C0)
+    alpha, beta = -1.25, 0.5
+    T.dgemm_device(dA, dB, dC, alpha=alpha, beta=beta, transb=transb, k=k)
+    got = dC.to_host()
+    want = beta * C0 + alpha * (A @ Bop)
+    err = np.abs(got - want)
+    assert np.all(err <= abs(alpha) * _bound(A, Bop, k) + 4 * np.finfo(float).eps * np.abs(want)), err.max()
+
+
+def test_schur_update_k3(ctx):
+    # the standalone K3 shape of BASELINE.md:46 at a reduced size: C -= W V, nb = 256
+    rng = np.random.default_rng(3)
+    m, n, nb = 1536, 1280, 256
+    C0, W, V = rng.random((m, n)), rng.random((m, nb)), rng.random((nb, n))
+    dC = _dev(ctx, C0)
+    T.schur_update_device(dC, _dev(ctx, W), _dev(ctx, V))
+    got = dC.to_host()
+    want = C0 - W @ V
+    assert np.all(np.abs(got - want) <= _bound(W, V, nb) + 4 * np.finfo(float).eps * np.abs(C0)), \
+        np.abs(got - want).max()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("r,R", [(256, 8192), (1024, 4096), (333, 1000), (70, 2000)])
+def test_sitetensor_solve_mfma(ctx, r, R):
+    rng = np.random.default_rng(r * 11 + R)
+    # pivot matrices of a TCI are well conditioned by construction (maxvol-like pivots); a
+    # diagonally weighted random matrix stands in for one, with partial pivoting still exercised
+    P = rng.random((r, r)) + 0.5 * np.sqrt(r) * np.eye(r) * rng.choice([-1, 1], r)
+    Pi1 = rng.random((R, r))
+    ref = O.sitetensor_solve(P, Pi1).reshape((R, r), order="F")
+    dP, dPi1, dT = _dev(ctx, P, True), _dev(ctx, Pi1, True), T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+    T.sitetensor_solve_device(dP, dPi1, dT)
+    got = dT.to_host()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+    # the host entry takes the same path
+    T_ = np.zeros(R * r)
+    ctx.check(ctx.lib.tci_sitetensor_solve_h(ctx.h, T._lib.ptr(np.asfortranarray(P).ravel(order="F")), r,
+                                             T._lib.ptr(np.asfortranarray(Pi1).ravel(order="F")), R,
+                                             T._lib.ptr(T_)))
+    np.testing.assert_allclose(T_.reshape((R, r), order="F"), ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("np_", [256, 1024])
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_luci_factors_mfma(ctx, np_, leftorth):
+    A = O.fill_uniform(2304 * 1792, 21).reshape((2304, 1792), order="F")
+    luci = T.MatrixLUCI(A, maxrank=np_, leftorthogonal=leftorth, ctx=ctx)
+    ref = O.OracleLU(A, maxrank=np_, leftorthogonal=leftorth)
+    assert np.array_equal(luci.rowindices() - 1, ref.rowindices())
+    assert np.array_equal(luci.colindices() - 1, ref.colindices())
+    np.testing.assert_allclose(luci.left(), ref.left, rtol=1e-12, atol=1e-12 * np.abs(ref.left).max())
+    np.testing.assert_allclose(luci.right(), ref.right, rtol=1e-12, atol=1e-12 * np.abs(ref.right).max())
