@@ -57,6 +57,12 @@ extern "C" {
 
 typedef struct tci_ctx tci_ctx;
 typedef struct tci_func tci_func;
+typedef struct tci_comm tci_comm;
+/* Host-side exchange hook of the column-sharded rrLU: all-gather `count` doubles per rank from
+ * d_send into d_recv (rank-major; device pointers of the calling context). Returns 0 on success.
+ * Used when no RCCL communicator is passed (e.g. ranks sharing one GPU, or a Julia Distributed
+ * transport); called with the context stream synchronised. */
+typedef int (*tci_exchange_fn)(void* user, const double* d_send, double* d_recv, int64_t count);
 
 /* ---------------------------------------------------------------- context */
 int tci_ctx_create(int device, tci_ctx** out);
@@ -257,6 +263,37 @@ int tci_sitetensor_solve_c128_h(tci_ctx* ctx, const double* P, int64_t r, const 
 int tci_tt_evaluate_c128_h(tci_ctx* ctx, int32_t L, const int32_t* dims, const int32_t* bonddims,
                            const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
                            double* out);
+
+/* ------------------------------------------------- multi-GPU: RCCL over xGMI
+ * One process per GPU. Rank 0 makes the 128-byte unique id (tci_comm_unique_id; nbytes gets its
+ * size), the host broadcasts it (torch.distributed / MPI / Julia Distributed), every rank
+ * creates its communicator on its context's device. Collectives are enqueued on the context
+ * stream (asynchronous: synchronise the context before reading results on the host). */
+int tci_comm_unique_id(void* id, int64_t* nbytes);
+int tci_comm_create(tci_ctx* ctx, int nranks, int rank, const void* id, tci_comm** out);
+int tci_comm_destroy(tci_comm* comm);
+int tci_comm_allgather_d(tci_comm* comm, const void* d_send, void* d_recv, int64_t bytes);
+/* in-place max over ranks of count uint64 words (maxsample as the bit pattern of |x|: non-negative
+ * doubles order like their bits, a NaN's bits exceed every finite |x|, Julia's NaN-propagating max) */
+int tci_comm_allreduce_max_u64_d(tci_comm* comm, void* d_buf, int64_t count);
+
+/* Column-sharded rrlu! (matrixlu.jl:346-396 with submatrixargmax :46-87 and addpivot! :254-322 split
+ * across ranks): rank r holds global columns [c0, c0 + nloc) of the m x n matrix as
+ * d_A (ld lda, even) columns 0..nloc-1; column nloc of d_A must exist and is scratch (the pivot
+ * column is installed there on every rank). Per pivot every rank runs its pass on its columns, the
+ * local winners and their columns are all-gathered (RCCL when comm is given, else exch, else
+ * nranks must be 1) and every rank commits the same global winner in the reference's tie order:
+ * permutations, npivot, lu.error and pivot errors are bitwise those of tci_rrlu_h on the full
+ * matrix, on every rank (rowperm m, colperm n global, 1-based). d_A is clobbered. */
+int tci_rrlu_sharded_d(tci_ctx* ctx, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks,
+                       double* d_A, int64_t m, int64_t nloc, int64_t lda, int64_t c0, int64_t n,
+                       int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
+                       int64_t* colperm, int64_t* npivot, double* lasterror, double* pivoterrors);
+/* Factors of the last tci_rrlu_sharded_d on this context, position order as tci_rrlu_h: L (m x np,
+ * ld m, identical on every rank; NULL to skip) and this rank's columns of U (np x n, ld ldu: only
+ * the columns whose original index lies in [c0, c0 + nloc) are written; the caller combines the
+ * ranks' disjoint columns). NaN checks of matrixlu.jl:376-381 on what this rank holds. */
+int tci_rrlu_sharded_factors_h(tci_ctx* ctx, double* L, double* U, int64_t ldu);
 
 /* ----------------------------------------------------- synthetic inputs
  * Fills d_A (m x n, ld lda) with U[0,1): splitmix64(seed * 0xD1B54A32D192ED03 + (i + m*j)) >> 11

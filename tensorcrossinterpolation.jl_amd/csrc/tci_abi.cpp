@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/tci_hip.h"
 #include "tci_internal.h"
 
@@ -98,6 +100,17 @@ struct tci_ctx {
     size_t capL = 0;
     double* dU = nullptr;
     size_t capU = 0;
+    // column-sharded rrLU: local column positions (+ ghost), exchange records, local winner
+    int32_t* colposL = nullptr;
+    size_t capColposL = 0;
+    double* shsend = nullptr;
+    size_t capShSend = 0;
+    double* shrecv = nullptr;
+    size_t capShRecv = 0;
+    Cand* lout = nullptr;
+    size_t capLout = 0;
+    int64_t sh_np = 0, sh_nloc = 0, sh_c0 = 0, sh_m = 0, sh_n = 0;
+    int sh_leftorth = 1;
     char* cws = nullptr;  // ComplexF64 rrLU: state, candidates, pivot column / row buffers
     size_t capCws = 0;
     double* dRe = nullptr;  // ComplexF64 2-site update: real values of f before the scaling
@@ -118,6 +131,12 @@ struct tci_ctx {
     static constexpr int kFams = 3 + tci::kMaxPend + 1 + 3;  // + 20 solve, 21 LUCI factors, 22 K3
     double fam_ms[kFams] = {};
     int64_t fam_n[kFams] = {};
+};
+
+struct tci_comm {
+    tci_ctx* ctx = nullptr;
+    ncclComm_t nc = nullptr;
+    int nranks = 1, rank = 0;
 };
 
 struct tci_func {
@@ -526,6 +545,151 @@ int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
     return TCI_OK;
 }
 
+
+// ------------------------------------------------------------------ column-sharded rrLU driver
+// The loop of rrlu_device with the selection split across ranks: the passes run unchanged on
+// this rank's columns (+ the ghost column) and publish the local winner; then gather -> exchange
+// (RCCL all-gather on the context stream, a host callback, or a copy for one rank) -> commit, all
+// stream-ordered: the host only polls the stop flag in growing chunks, as rrlu_device does.
+int shard_exchange(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks, int64_t rec) {
+    if (comm) {
+        if (ncclAllGather(c->shsend, c->shrecv, (size_t)rec, ncclFloat64, comm->nc, c->stream) != ncclSuccess)
+            return set_err(c, TCI_ERR_DEVICE, "rrlu_sharded: ncclAllGather failed");
+        return TCI_OK;
+    }
+    if (exch) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (exch(user, c->shsend, c->shrecv, rec) != 0)
+            return set_err(c, TCI_ERR_DEVICE, "rrlu_sharded: exchange callback failed");
+        return TCI_OK;
+    }
+    if (nranks != 1) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
+    HIPCHK(c, hipMemcpyAsync(c->shrecv, c->shsend, rec * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    return TCI_OK;
+}
+
+int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks,
+                        double* dA, int64_t m, int64_t nloc, int64_t lda, int64_t c0, int64_t n,
+                        int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* np_out,
+                        double* err_out) {
+    int st;
+    if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
+    if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
+    if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
+    if ((st = ensure(c, &c->colposL, &c->capColposL, (size_t)nloc + 2))) return st;
+    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
+    if ((st = ensure(c, &c->lout, &c->capLout, 1))) return st;
+    const int64_t rec = tci::shard_rec(m);
+    if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)rec))) return st;
+    if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)(rec * nranks)))) return st;
+    const int mi = (int)m, nl1 = (int)(nloc + 1);  // local columns + the ghost
+    tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, (int)n);
+    tci::launch_shard_init(c->stream, c->colposL, (int)nloc, c0);
+    int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
+    if (mr < 0) mr = 0;
+    c->ldUp = std::max<int64_t>(mr, 1);
+    if (m == 0 || n == 0 || mr == 0) {
+        HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *np_out = 0;
+        *err_out = (0 >= std::min(m, n)) ? 0.0 : c->hst->error;
+        return TCI_OK;
+    }
+    if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
+    if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
+    if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * nl1)))) return st;
+    const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
+    const int64_t ldx = round_up(m + 2, 16), ldy = round_up(nl1 + 2, 16);
+    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPend * ldx)))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPend * ldy)))) return st;
+    if ((m + tci::kRowsPerTile - 1) / tci::kRowsPerTile > kMaxGrid)
+        return set_err(c, TCI_ERR_ARG, "rrlu: too many rows");
+    tci::PassArgs g;
+    g.A = dA;
+    g.lda = lda;
+    g.m = mi;
+    g.n = nl1;
+    g.k = -1;
+    g.X = c->xbuf;
+    g.ldx = ldx;
+    g.Y = c->ybuf;
+    g.ldy = ldy;
+    g.rowpos = c->rowpos;
+    g.colpos = c->colposL;
+    g.st = c->st;
+    g.Lp = c->Lp;
+    g.ldl = m;
+    g.Up = c->Up;
+    g.ldu = c->ldUp;
+    g.leftorth = leftorth;
+    g.cand = c->cand;
+    g.cb = pick_cb(m, nl1);
+    g.rev = 0;
+    g.rowphys = c->rowperm;
+    g.colphys = c->colperm;
+    g.pivvals = c->pivv;
+    g.reltol = reltol;
+    g.abstol = abstol;
+    g.ticket = c->ticket;
+    g.selk = 0;
+    g.lout = c->lout;
+    const bool shadow = c->shadow && lda % 4 == 0;
+    g.S = nullptr;
+    g.lds = 0;
+    if (shadow) {
+        g.lds = round_up(m, 16);
+        if ((st = ensure(c, &c->sbuf, &c->capS, (size_t)(g.lds * nl1)))) return st;
+        g.S = c->sbuf;
+    }
+    const int grid = tci::argmax_grid(mi, nl1, -1, g.cb, std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
+    auto select = [&](int selk) -> int {
+        tci::launch_shard_gather(c->stream, c->lout, dA, lda, mi, c->ybuf, ldy, c0, c->shsend);
+        int e = shard_exchange(c, comm, exch, user, nranks, rec);
+        if (e) return e;
+        tci::launch_shard_commit(c->stream, c->shrecv, nranks, rec, mi, selk, c->st, reltol, abstol, c->rowpos,
+                                 c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0, (int)nloc, dA, lda,
+                                 c->ybuf, ldy);
+        return TCI_OK;
+    };
+    tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // local argmax of A
+    if ((st = select(0))) return st;
+    int64_t k = 0, chunk = 2, t0 = 0;
+    bool stopped = false;
+    while (k < mr && !stopped) {
+        const int64_t kend = std::min<int64_t>(k + chunk, mr);
+        for (int64_t kk = k; kk < kend; ++kk) {
+            const int P = (int)(kk - t0) + 1;
+            const bool flush = (P >= nb) && (kk + 1 < mr);
+            g.k = (int)kk;
+            g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
+            g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
+            const bool sampled = kk % c->timing_stride == 0;
+            ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
+            tci::launch_pass(c->stream, P, flush, shadow, g, grid);
+            ev_end(c, sampled);
+            if (g.selk >= 0 && (st = select(g.selk))) return st;
+            if (flush) t0 = kk + 1;
+        }
+        k = kend;
+        if (k < mr) {
+            HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (c->hst->done) stopped = true;
+            chunk = std::min<int64_t>(chunk * 2, 64);
+        }
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int64_t np = c->hst->np;
+    double err = c->hst->error;
+    if (np >= std::min(m, n)) err = 0.0;  // matrixlu.jl:391-393
+    *np_out = np;
+    *err_out = err;
+    return TCI_OK;
+}
+
 }  // namespace
 
 // =================================================================== C ABI
@@ -585,7 +749,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
-    fr(c->dU); fr(c->cws); fr(c->dRe);
+    fr(c->dU); fr(c->cws); fr(c->dRe); fr(c->colposL); fr(c->shsend); fr(c->shrecv); fr(c->lout);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
@@ -1572,6 +1736,114 @@ int tci_memcpy_d2h(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
 int tci_memcpy_d2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int tci_comm_unique_id(void* id, int64_t* nbytes) {
+    if (nbytes) *nbytes = NCCL_UNIQUE_ID_BYTES;
+    if (!id) return nbytes ? TCI_OK : TCI_ERR_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return TCI_ERR_DEVICE;
+    memcpy(id, &u, sizeof u);
+    return TCI_OK;
+}
+
+int tci_comm_create(tci_ctx* c, int nranks, int rank, const void* id, tci_comm** out) {
+    if (!c || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return TCI_ERR_ARG;
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    tci_comm* cm = new tci_comm();
+    cm->ctx = c;
+    cm->nranks = nranks;
+    cm->rank = rank;
+    const ncclResult_t r = ncclCommInitRank(&cm->nc, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete cm;
+        return set_err(c, TCI_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    *out = cm;
+    return TCI_OK;
+}
+
+int tci_comm_destroy(tci_comm* cm) {
+    if (!cm) return TCI_OK;
+    if (cm->ctx && cm->ctx->stream) hipStreamSynchronize(cm->ctx->stream);
+    if (cm->nc) ncclCommDestroy(cm->nc);
+    delete cm;
+    return TCI_OK;
+}
+
+int tci_comm_allgather_d(tci_comm* cm, const void* d_send, void* d_recv, int64_t bytes) {
+    if (!cm || bytes < 0 || (bytes > 0 && (!d_send || !d_recv))) return TCI_ERR_ARG;
+    tci_ctx* c = cm->ctx;
+    if (bytes == 0) return TCI_OK;
+    const ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes, ncclUint8, cm->nc, c->stream);
+    if (r != ncclSuccess) return set_err(c, TCI_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return TCI_OK;
+}
+
+int tci_comm_allreduce_max_u64_d(tci_comm* cm, void* d_buf, int64_t count) {
+    if (!cm || count < 0 || (count > 0 && !d_buf)) return TCI_ERR_ARG;
+    tci_ctx* c = cm->ctx;
+    if (count == 0) return TCI_OK;
+    const ncclResult_t r = ncclAllReduce(d_buf, d_buf, (size_t)count, ncclUint64, ncclMax, cm->nc, c->stream);
+    if (r != ncclSuccess) return set_err(c, TCI_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return TCI_OK;
+}
+
+int tci_rrlu_sharded_d(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks, double* d_A,
+                       int64_t m, int64_t nloc, int64_t lda, int64_t c0, int64_t n, int64_t maxrank,
+                       double reltol, double abstol, int leftorth, int64_t* rowperm, int64_t* colperm,
+                       int64_t* npivot, double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror || m < 0 || nloc < 0 || n < 0 || c0 < 0 || c0 + nloc > n || nranks < 1)
+        return TCI_ERR_ARG;
+    if (comm && comm->nranks != nranks) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: nranks != comm size");
+    if (m > 0 && (!d_A || lda < m || lda % 2)) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: bad matrix / lda");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int64_t np;
+    double err;
+    int st = rrlu_sharded_device(c, comm, exch, user, nranks, d_A, m, nloc, lda, c0, n, maxrank, reltol, abstol,
+                                 leftorth, &np, &err);
+    if (st) return st;
+    c->sh_np = np;
+    c->sh_nloc = nloc;
+    c->sh_c0 = c0;
+    c->sh_m = m;
+    c->sh_n = n;
+    c->sh_leftorth = leftorth;
+    *npivot = np;
+    *lasterror = err;
+    if ((st = pivot_errors(c, np, err, pivoterrors))) return st;
+    return fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0);
+}
+
+int tci_rrlu_sharded_factors_h(tci_ctx* c, double* L, double* U, int64_t ldu) {
+    if (!c) return TCI_ERR_ARG;
+    const int64_t m = c->sh_m, n = c->sh_n, np = c->sh_np;
+    if (np <= 0) return TCI_OK;
+    if (U && ldu < np) return set_err(c, TCI_ERR_ARG, "ldu < npivot");
+    int st;
+    if ((st = ensure(c, &c->dL, &c->capL, (size_t)(m * np)))) return st;
+    if ((st = ensure(c, &c->dU, &c->capU, (size_t)(np * n)))) return st;
+    if (U) HIPCHK(c, hipMemcpy2DAsync(c->dU, np * sizeof(double), U, ldu * sizeof(double), np * sizeof(double), n,
+                                      hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
+    tci::launch_extract_shard(c->stream, c->Lp, m, c->Up, c->ldUp, c->pivv, c->rowperm, c->colperm, (int)m, (int)n,
+                              (int)np, c->sh_leftorth, L ? c->dL : nullptr, m, U ? c->dU : nullptr, np, c->flag,
+                              c->sh_c0, (int)c->sh_nloc);
+    HIPCHK(c, hipMemcpyAsync(c->hflag, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (L) HIPCHK(c, hipMemcpyAsync(L, c->dL, m * np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (U) HIPCHK(c, hipMemcpy2DAsync(U, ldu * sizeof(double), c->dU, np * sizeof(double), np * sizeof(double), n,
+                                      hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (*c->hflag & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+    if (*c->hflag & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
     return TCI_OK;
 }
 

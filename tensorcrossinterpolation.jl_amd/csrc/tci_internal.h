@@ -67,6 +67,9 @@ struct PassArgs {
     // (multiple of 4); null when the shadow search is off
     float* S;
     int64_t lds;
+    // column-sharded rrLU (tci_rrlu_sharded_d): the pass tail writes its rank-local winner here
+    // instead of committing pivot selk (null: commit as usual)
+    Cand* lout = nullptr;
 };
 
 // Selection fields of PassArgs as seen by the device.
@@ -80,6 +83,7 @@ struct SelArgs {
     unsigned* ticket;
     double reltol, abstol;
     int selk;
+    Cand* lout;  // non-null: local winner only, no commit (column-sharded rrLU)
 };
 
 // MPO-MPO contraction integrand (TCI_F_MPO): LDS limits of the environment kernel, in doubles
@@ -181,6 +185,30 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
                     const double* pivvals, const int64_t* rowphys, const int64_t* colphys, int m,
                     int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
                     int* flag);
+
+// ---- column-sharded rrLU (tci_rrlu.hip). Rank r holds the global columns [c0, c0 + nloc) as its
+// local physical columns 0..nloc-1 plus a ghost column nloc: the column of the last committed
+// pivot, installed on every rank so that the unchanged passes derive x_k from it. Per pivot each
+// rank's pass publishes its local winner (lout); k_shard_gather packs it, the pending y's of its
+// column and that column's stale values into a record of kShardRec(m) doubles; the records of all
+// ranks are all-gathered (RCCL); k_shard_commit reduces them in rank order (every rank reaches the
+// same winner: abs2, then column position, then row position -- submatrixargmax's order), commits
+// it to the replicated row / global column maps and installs the ghost.
+constexpr int kShardHdr = 4 + kMaxPend;
+inline int64_t shard_rec(int64_t m) { return (kShardHdr + m + 1) / 2 * 2; }
+void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0);
+void launch_shard_gather(hipStream_t s, const Cand* lout, const double* A, int64_t lda, int m,
+                         const double* Y, int64_t ldy, int64_t c0, double* send);
+void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t rec, int m, int k,
+                         RrluState* st, double reltol, double abstol, int32_t* rowpos,
+                         int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
+                         int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
+                         int64_t ldy);
+// extraction of a sharded rank's part: U columns whose physical column is in [c0, c0 + nloc)
+void launch_extract_shard(hipStream_t s, const double* Lp, int64_t ldlp, const double* Up, int64_t ldup,
+                          const double* pivvals, const int64_t* rowphys, const int64_t* colphys, int m,
+                          int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
+                          int* flag, int64_t c0, int nloc);
 
 // ---- factors, batch evaluation, solve (tci_device.hip)
 // MatrixLUCI factors from position-order L (m x np) / U (np x n); L rows >= np (leftorth) or U

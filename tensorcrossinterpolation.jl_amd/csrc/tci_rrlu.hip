@@ -268,6 +268,10 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     block_reduce_cand<NT>(w);
     if (threadIdx.x == 0) {
         __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sel.lout) {  // column-sharded: this rank's winner, committed after the exchange
+            *sel.lout = Cand{w.v, w.val, w.cpos, w.rpos, w.pc, w.pr};
+            return;
+        }
         commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
                      sel.colphys, sel.pivvals, rk, ck);
 #if TCI_PASS_PROF
@@ -940,8 +944,8 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 
 template <int P>
 static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs& g, int grid) {
-    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals,
-                      g.st,     g.ticket, g.reltol,  g.abstol,  g.selk};
+    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
+                      g.ticket, g.reltol, g.abstol,  g.selk,    g.lout};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
                   g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
     if (shadow) {
@@ -1665,7 +1669,7 @@ __global__ void k_extract(const double* __restrict__ Lp, int64_t ldlp, const dou
                           int64_t ldup, const double* __restrict__ pivvals,
                           const int64_t* __restrict__ rowphys, const int64_t* __restrict__ colphys,
                           int m, int n, int np, int leftorth, double* __restrict__ L, int64_t ldl,
-                          double* __restrict__ U, int64_t ldu, int* flag) {
+                          double* __restrict__ U, int64_t ldu, int* flag, int64_t c0, int64_t nloc) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int f = 0;
@@ -1680,10 +1684,12 @@ __global__ void k_extract(const double* __restrict__ Lp, int64_t ldlp, const dou
     }
     for (int64_t e = gid; e < (int64_t)np * n; e += stride) {
         const int t = (int)(e % np), pos = (int)(e / np);
+        const int64_t pc = colphys[pos] - c0;  // local physical column (sharded: others skip)
+        if (pc < 0 || pc >= nloc) continue;
         double v;
         if (pos < t) v = 0.0;
         else if (pos == t) v = leftorth ? pivvals[t] : 1.0;
-        else v = Up[t + colphys[pos] * ldup];
+        else v = Up[t + pc * ldup];
         if (pos >= t && isnan(pos == t ? pivvals[t] : v)) f |= 2;
         if (U) U[t + (int64_t)pos * ldu] = v;
     }
@@ -1699,7 +1705,113 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
     if (g > 4096) g = 4096;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(k_extract, dim3((int)g), dim3(256), 0, s, Lp, ldlp, Up, ldup, pivvals, rowphys,
-                       colphys, m, n, np, leftorth, L, ldl, U, ldu, flag);
+                       colphys, m, n, np, leftorth, L, ldl, U, ldu, flag, (int64_t)0, (int64_t)n);
+}
+
+void launch_extract_shard(hipStream_t s, const double* Lp, int64_t ldlp, const double* Up, int64_t ldup,
+                          const double* pivvals, const int64_t* rowphys, const int64_t* colphys, int m,
+                          int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
+                          int* flag, int64_t c0, int nloc) {
+    long long work = (long long)m * np + (long long)np * n;
+    long long g = (work + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_extract, dim3((int)g), dim3(256), 0, s, Lp, ldlp, Up, ldup, pivvals, rowphys,
+                       colphys, m, n, np, leftorth, L, ldl, U, ldu, flag, c0, (int64_t)nloc);
+}
+
+// ------------------------------------------------------------ column-sharded rrLU (tci_internal.h)
+__global__ void k_shard_init(int32_t* colpos_loc, int nloc, int64_t c0) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j <= nloc) colpos_loc[j] = j < nloc ? (int32_t)(c0 + j) : -1;  // the ghost is never trailing
+}
+
+void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0) {
+    hipLaunchKernelGGL(k_shard_init, dim3((nloc + 256) / 256), dim3(256), 0, s, colpos_loc, nloc, c0);
+}
+
+__device__ __forceinline__ double bits_dbl(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t dbl_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// Record: [0] abs2, [1] value, [2] column | row position (int32 pair), [3] global physical column |
+// physical row, [4, 4 + kMaxPend) the pending y's of that column, then its m stale values.
+__global__ __launch_bounds__(256) void k_shard_gather(const Cand* __restrict__ lout, const double* __restrict__ A,
+                                                      int64_t lda, int m, const double* __restrict__ Y,
+                                                      int64_t ldy, int64_t c0, double* __restrict__ send) {
+    const Cand c = *lout;
+    const bool has = c.v >= 0.0;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        send[0] = c.v;
+        send[1] = c.val;
+        send[2] = bits_dbl((uint64_t)(uint32_t)c.cpos | ((uint64_t)(uint32_t)c.rpos << 32));
+        const int32_t pcg = has ? (int32_t)(c0 + c.pcol) : -1;
+        send[3] = bits_dbl((uint64_t)(uint32_t)pcg | ((uint64_t)(uint32_t)c.prow << 32));
+    }
+    if (tid < kMaxPend) send[4 + tid] = has ? Y[(int64_t)tid * ldy + c.pcol] : 0.0;
+    const double* col = A + (int64_t)(has ? c.pcol : 0) * lda;
+    for (int i = tid; i < m; i += blockDim.x) send[kShardHdr + i] = has ? col[i] : 0.0;
+}
+
+void launch_shard_gather(hipStream_t s, const Cand* lout, const double* A, int64_t lda, int m,
+                         const double* Y, int64_t ldy, int64_t c0, double* send) {
+    hipLaunchKernelGGL(k_shard_gather, dim3(1), dim3(256), 0, s, lout, A, lda, m, Y, ldy, c0, send);
+}
+
+__global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__ recv, int nranks, int64_t rec,
+                                                      int m, int k, RrluState* st, double reltol, double abstol,
+                                                      int32_t* rowpos, int32_t* colpos_g, int64_t* rowphys,
+                                                      int64_t* colphys_g, double* pivvals, int32_t* colpos_loc,
+                                                      int64_t c0, int nloc, double* A, int64_t lda, double* Y,
+                                                      int64_t ldy) {
+    __shared__ int win, ok;
+    if (threadIdx.x == 0) {
+        CandR w = cand_none();
+        int wr = -1;
+        for (int r = 0; r < nranks; ++r) {
+            const double* h = recv + (int64_t)r * rec;
+            const uint64_t b2 = dbl_bits(h[2]), b3 = dbl_bits(h[3]);
+            const CandR c{h[0], h[1], (int)(uint32_t)b2, (int)(uint32_t)(b2 >> 32), (int)(uint32_t)b3,
+                          (int)(uint32_t)(b3 >> 32)};
+            if (c.v >= 0.0 && cand_better(c.v, c.cpos, c.rpos, w.v, w.cpos, w.rpos)) {
+                w = c;
+                wr = r;
+            }
+        }
+        int accepted = 0;
+        if (!st->done) {
+            const int64_t rk = rowphys[k], ck = colphys_g[k];
+            commit_pivot(k, w, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals, rk, ck);
+            if (!st->done) {
+                accepted = 1;
+                const int64_t pcg = st->q;  // global physical column of the pivot
+                if (pcg >= c0 && pcg < c0 + nloc) colpos_loc[pcg - c0] = k;
+                if (ck >= c0 && ck < c0 + nloc) colpos_loc[ck - c0] = colpos_g[ck];
+                colpos_loc[nloc] = k;
+                st->q = nloc;  // the passes take the pivot column from the ghost
+            }
+        }
+        win = wr;
+        ok = accepted;
+    }
+    __syncthreads();
+    if (!ok) return;
+    // the ghost: the winner's stale column and its pending y's (every trailing value NaN: no winner,
+    // pivot NaN, the column is NaN as the reference's would be after the division)
+    const double* src = win >= 0 ? recv + (int64_t)win * rec : nullptr;
+    double* g = A + (int64_t)nloc * lda;
+    const double qnan = __longlong_as_double(0x7ff8000000000000LL);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) g[i] = src ? src[kShardHdr + i] : qnan;
+    if (threadIdx.x < kMaxPend) Y[(int64_t)threadIdx.x * ldy + nloc] = src ? src[4 + threadIdx.x] : 0.0;
+}
+
+void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t rec, int m, int k,
+                         RrluState* st, double reltol, double abstol, int32_t* rowpos,
+                         int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
+                         int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
+                         int64_t ldy) {
+    hipLaunchKernelGGL(k_shard_commit, dim3(1), dim3(256), 0, s, recv, nranks, rec, m, k, st, reltol, abstol,
+                       rowpos, colpos_g, rowphys, colphys_g, pivvals, colpos_loc, c0, nloc, A, lda, Y, ldy);
 }
 
 }  // namespace tci

@@ -9,7 +9,8 @@ from .batcheval import (ComplexScaledEvaluator, F_CP, F_GAUSS, F_GAUSSMIX, F_LOR
                         quantics_exp, quantics_osc, sum_, table, tensortrain_function)
 from .cachedfunction import CachedFunction
 from .contraction import Contraction, contract, contract_naive, contract_TCI
-from .distributed import Comm, ShardedBatchEvaluator, column_blocks
+from .distributed import (Comm, DeviceComm, HostExchange, ShardedBatchEvaluator, column_blocks, rrlu_sharded,
+                          rrlu_sharded_factors)
 from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder
 from .matrixlu import (DeviceMatrix, colindices, dgemm_device, diag, lastpivoterror, ldiv, left, npivots,
                        pivoterrors, right, rowindices, rrLU, rrlu, rrlu_inplace_device, schur_update_device,

@@ -89,12 +89,23 @@ SIGNATURES = {
     "tci_sitetensor_solve_d": ([vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_dgemm_d": ([vp, C.c_int, i64, i64, i64, dbl, vp, i64, vp, i64, dbl, vp, i64], C.c_int),
     "tci_schur_update_d": ([vp, vp, i64, i64, i64, vp, i64, vp, i64, i64], C.c_int),
+    "tci_comm_unique_id": ([vp, pi64], C.c_int),
+    "tci_comm_create": ([vp, C.c_int, C.c_int, vp, C.POINTER(vp)], C.c_int),
+    "tci_comm_destroy": ([vp], C.c_int),
+    "tci_comm_allgather_d": ([vp, vp, vp, i64], C.c_int),
+    "tci_comm_allreduce_max_u64_d": ([vp, vp, i64], C.c_int),
+    "tci_rrlu_sharded_d": ([vp, vp, vp, vp, C.c_int, vp, i64, i64, i64, i64, i64, i64, dbl, dbl, C.c_int,
+                            vp, vp, pi64, pdbl, vp], C.c_int),
+    "tci_rrlu_sharded_factors_h": ([vp, vp, vp, i64], C.c_int),
     "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
     "tci_free_d": ([vp, vp], C.c_int),
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy_d2h": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy_d2d": ([vp, vp, vp, i64], C.c_int),
 }
+
+# tci_exchange_fn (include/tci_hip.h): int (*)(void* user, const double* d_send, double* d_recv, int64 count)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, vp, vp, vp, i64)
 
 _lib = None
 _lock = threading.Lock()

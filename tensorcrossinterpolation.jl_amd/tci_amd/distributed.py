@@ -12,6 +12,7 @@ replicated factorisations agree exactly and all ranks keep identical TCI2 state.
 `ShardedBatchEvaluator` wraps any evaluator with the `pi(I, J, M) -> (matrix, maxabs)` method of
 `GPUBatchEvaluator` and is itself such an evaluator, so `crossinterpolate2` takes it unchanged.
 """
+import ctypes as C
 import math
 
 import numpy as np
@@ -76,6 +77,28 @@ class Comm:
     def barrier(self):
         self.dist.barrier(group=self.group)
 
+    def broadcast_bytes(self, arr, src=0):
+        """uint8 array from rank `src` to every rank."""
+        torch = self.torch
+        t = torch.from_numpy(np.ascontiguousarray(arr, np.uint8).copy()).to(self.device)
+        self.dist.broadcast(t, src=src, group=self.group)
+        return t.cpu().numpy()
+
+    def allgather_flat(self, buf):
+        """float64 vectors of equal length from every rank, concatenated in rank order."""
+        torch = self.torch
+        t = torch.from_numpy(np.ascontiguousarray(buf, np.float64)).to(self.device)
+        out = torch.empty(self.world * t.numel(), dtype=torch.float64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy()
+
+    def allreduce_sum(self, a):
+        torch = self.torch
+        a = np.asarray(a, np.float64)
+        t = torch.from_numpy(np.asfortranarray(a).ravel(order="F").copy()).to(self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t.cpu().numpy().reshape(a.shape, order="F")
+
 
 class ShardedBatchEvaluator:
     """A BatchEvaluator{Float64} whose batch evaluation is split over the ranks of `comm` by
@@ -135,3 +158,105 @@ class ShardedBatchEvaluator:
         J = np.asarray(Jset, np.int32).reshape(len(Jset), nr)
         out, _ = self.pi(I, J, M)
         return out.reshape((len(Iset),) + tuple(self.localdims[nl:nl + M]) + (len(Jset),), order="F")
+
+
+# ------------------------------------------------------------------ device-resident data path
+class DeviceComm:
+    """An RCCL communicator inside libtci_hip.so (tci_comm_*), bound to a context's device and
+    stream: collectives on device buffers, enqueued on the context stream -- no host staging.
+    The 128-byte unique id goes from rank 0 to the others over `comm` (a `Comm`, i.e. the
+    torch.distributed host group)."""
+
+    def __init__(self, ctx, comm):
+        from . import _lib
+
+        self.ctx, self.rank, self.world = ctx, comm.rank, comm.world
+        lib = ctx.lib
+        nbytes = C.c_int64()
+        ctx.check(lib.tci_comm_unique_id(None, C.byref(nbytes)))
+        uid = np.zeros(nbytes.value, np.uint8)
+        if comm.rank == 0:
+            ctx.check(lib.tci_comm_unique_id(_lib.ptr(uid), None))
+        uid = comm.broadcast_bytes(uid)
+        h = C.c_void_p()
+        ctx.check(lib.tci_comm_create(ctx.h, comm.world, comm.rank, _lib.ptr(uid), C.byref(h)))
+        self.h = h
+        ctx.own(self)
+
+    def allgather(self, d_send, d_recv, nbytes):
+        self.ctx.check(self.ctx.lib.tci_comm_allgather_d(self.h, d_send, d_recv, int(nbytes)))
+
+    def release(self):
+        if getattr(self, "h", None) and self.ctx.alive:
+            self.ctx.lib.tci_comm_destroy(self.h)
+        self.h = None
+
+    close = release
+
+
+class HostExchange:
+    """The tci_exchange_fn hook over a host `Comm` (gloo): device -> host, all-gather, host ->
+    device. For ranks that cannot form an RCCL communicator (several ranks on one GPU, CPU-side
+    transports); correct everywhere, slower than DeviceComm."""
+
+    def __init__(self, ctx, comm):
+        from . import _lib
+
+        self.ctx, self.comm = ctx, comm
+        self._lib = _lib
+
+        def fn(user, d_send, d_recv, count):
+            try:
+                buf = np.empty(int(count))
+                ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, _lib.ptr(buf), d_send, buf.nbytes))
+                allb = comm.allgather_flat(buf)
+                ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, d_recv, _lib.ptr(allb), allb.nbytes))
+                return 0
+            except Exception:  # reported to the library as a failed exchange
+                return 1
+
+        self.fn = _lib.EXCHANGE_FN(fn)  # keep a reference for the library's lifetime of the call
+
+
+def rrlu_sharded(local, m, n, c0, nloc, comm=None, exchange=None, nranks=1, maxrank=None, reltol=1e-14,
+                 abstol=0.0, leftorthogonal=True):
+    """Column-sharded rrlu! over the ranks (tci_rrlu_sharded_d): `local` is this rank's DeviceMatrix
+    holding global columns [c0, c0 + nloc) as its columns 0..nloc-1 plus one scratch column (so
+    local.n == nloc + 1). comm: a DeviceComm (RCCL) or exchange: a HostExchange; neither for one
+    rank. Returns (npivot, error, rowperm, colperm, pivoterrors), identical on every rank and
+    bitwise those of rrlu on the full matrix (1-based permutations)."""
+    from . import _lib
+
+    ctx = local.ctx
+    if local.n != nloc + 1 or local.m != m:
+        raise ValueError("rrlu_sharded: the local matrix must be m x (nloc + 1)")
+    mr = min(m, n) if maxrank is None else int(maxrank)
+    rowperm = np.zeros(max(m, 1), np.int64)
+    colperm = np.zeros(max(n, 1), np.int64)
+    pe = np.zeros(max(min(mr, m, n), 0) + 1)
+    npv, err = C.c_int64(), C.c_double()
+    world = comm.world if comm is not None else (exchange.comm.world if exchange is not None else nranks)
+    ctx.check(ctx.lib.tci_rrlu_sharded_d(ctx.h, comm.h if comm is not None else None,
+                                         exchange.fn if exchange is not None else None, None, int(world),
+                                         local.ptr, m, nloc, local.ld, c0, n, int(min(mr, 2 ** 62)),
+                                         float(reltol), float(abstol), int(bool(leftorthogonal)),
+                                         _lib.ptr(rowperm), _lib.ptr(colperm), C.byref(npv), C.byref(err),
+                                         _lib.ptr(pe)))
+    k = npv.value
+    return k, err.value, rowperm[:m], colperm[:n], pe[: k + 1]
+
+
+def rrlu_sharded_factors(ctx, m, n, npivot, host_comm=None):
+    """L (m x np) and U (np x n) of the last rrlu_sharded on `ctx`, position order. U's columns are
+    combined over the ranks with `host_comm` (each rank fills only its own columns)."""
+    from . import _lib
+
+    L = np.zeros((m, npivot), order="F")
+    U = np.zeros((npivot, n), order="F")
+    if npivot == 0:
+        return L, U
+    ctx.check(ctx.lib.tci_rrlu_sharded_factors_h(ctx.h, L.ctypes.data_as(C.c_void_p),
+                                                 U.ctypes.data_as(C.c_void_p), npivot))
+    if host_comm is not None and host_comm.world > 1:
+        U = host_comm.allreduce_sum(U)
+    return L, U

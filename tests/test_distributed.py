@@ -144,3 +144,53 @@ def test_sharded_tci2_two_ranks_one_gpu(tmp_path):
     for r in res:
         assert r["ranks"] and r["errors"] and r["isets"] and r["jsets"] and r["qosc"], r
     assert res[0]["linkdims"] == res[1]["linkdims"]
+
+
+# ------------------------------------------------------------------ column-sharded rrLU protocol
+def _shard_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import oracle_lib as O
+        from sharded_protocol import sharded_rrlu
+
+        comm = Comm(device="cpu")
+        res = {}
+        rng = np.random.default_rng(11)
+        cases = {
+            "random": (rng.random((37, 29)), {}),
+            # integer Lorentzian values: exact ties across column blocks (tie order by position)
+            "ties": (1.0 / (1.0 + np.add.outer(np.arange(40) % 5, np.arange(33) % 4) ** 2), {}),
+            "rightorth": (rng.random((25, 31)), {"leftorth": False}),
+            "maxrank": (rng.random((30, 30)), {"maxrank": 7}),
+            "lowrank_stop": (rng.random((40, 3)) @ rng.random((3, 26)), {"reltol": 1e-10}),
+            "wide_few_cols": (rng.random((12, 4)), {}),  # world 3: ranks with 1-2 columns
+        }
+        for name, (A, kw) in cases.items():
+            m, n = A.shape
+            j0, j1 = column_blocks(n, world)[rank]
+            npv, err, rp, cp, L, U = sharded_rrlu(A[:, j0:j1], m, n, j0, comm.allgather_flat, **kw)
+            U = comm.allreduce_sum(U)
+            ref = O.OracleLU(A, maxrank=kw.get("maxrank", min(m, n)), reltol=kw.get("reltol", 1e-14),
+                             leftorthogonal=kw.get("leftorth", True))
+            res[name] = bool(npv == ref.npivot and np.array_equal(rp, ref.rowpermutation)
+                             and np.array_equal(cp, ref.colpermutation) and np.array_equal(L, ref.L)
+                             and np.array_equal(U, ref.U) and (err == ref.error or (np.isnan(err) and np.isnan(ref.error))))
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_rrlu_protocol_gloo(tmp_path, world):
+    """The column-sharded rrLU protocol (local argmax, all-gather of candidates + columns, the same
+    commit on every rank) reproduces the unsharded oracle bit for bit (tests/sharded_protocol.py)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        assert all(res.values()), (r, res)

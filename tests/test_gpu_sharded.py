@@ -1,0 +1,131 @@
+"""Column-sharded rrLU on the device (tci_rrlu_sharded_d), through the C ABI:
+bitwise against the unsharded oracle (permutations, npivot, lu.error, pivot errors, L, U).
+
+* one rank (no exchange) in-process: the sharded driver's passes + ghost column + commit;
+* 2 and 3 ranks sharing cuda:0 with the host exchange hook (gloo) -- RCCL refuses two ranks on one
+  device, so this is how the multi-rank device path is checked on a one-GPU box;
+* one rank through an RCCL communicator (tci_comm_*: unique id over gloo, ncclAllGather on the
+  context stream): the RCCL data path of bench.py --gpus N.
+The parent process never touches the GPU in the multi-process tests (children are spawned).
+Reference: /root/reference/src/matrixlu.jl:46-87 (submatrixargmax), :295-322 (addpivot!),
+:346-396 (_optimizerrlu!).
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+T = pytest.importorskip("tci_amd")
+from tci_amd.distributed import Comm, DeviceComm, HostExchange, column_blocks, rrlu_sharded, rrlu_sharded_factors  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cases():
+    rng = np.random.default_rng(5)
+    return {
+        "random_1000x900_r100": (O.fill_uniform(1000 * 900, 3).reshape((1000, 900), order="F"), dict(maxrank=100)),
+        "ties_lorentz_600x500": (1.0 / (1.0 + np.add.outer(np.arange(600) % 7, np.arange(500) % 5) ** 2),
+                                 dict(maxrank=60)),
+        "rightorth_700x800_r50": (rng.random((700, 800)), dict(maxrank=50, leftorth=False)),
+        "lowrank_stop": (rng.random((400, 12)) @ rng.random((12, 300)), dict(reltol=1e-10)),
+        "tall_8300x120_r40": (O.fill_uniform(8300 * 120, 4).reshape((8300, 120), order="F"), dict(maxrank=40)),
+    }
+
+
+def _run_rank(ctx, A, rank, world, kw, comm=None, exchange=None):
+    m, n = A.shape
+    j0, j1 = column_blocks(n, world)[rank]
+    nloc = j1 - j0
+    loc = T.DeviceMatrix(m, nloc + 1, ctx=ctx)
+    loc.upload(np.hstack([A[:, j0:j1], np.zeros((m, 1))]))
+    out = rrlu_sharded(loc, m, n, j0, nloc, comm=comm, exchange=exchange, nranks=world,
+                       maxrank=kw.get("maxrank"), reltol=kw.get("reltol", 1e-14),
+                       leftorthogonal=kw.get("leftorth", True))
+    loc.free()
+    return out
+
+
+def _check(A, kw, out, L, U):
+    npv, err, rp, cp, pe = out
+    ref = O.OracleLU(A, maxrank=kw.get("maxrank", min(A.shape)), reltol=kw.get("reltol", 1e-14),
+                     leftorthogonal=kw.get("leftorth", True))
+    res = {"npivot": npv == ref.npivot,
+           "rowperm": bool(np.array_equal(rp - 1, ref.rowpermutation)),
+           "colperm": bool(np.array_equal(cp - 1, ref.colpermutation)),
+           "error": bool(err == ref.error),
+           "pivoterrors": bool(np.array_equal(pe, ref.pivoterrors)),
+           "L": bool(np.array_equal(L, ref.L)), "U": bool(np.array_equal(U, ref.U))}
+    return res
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", list(_cases()))
+@pytest.mark.parametrize("shadow", [1, 0])
+def test_sharded_one_rank_bitwise(ctx, name, shadow):
+    A, kw = _cases()[name]
+    ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, shadow))
+    try:
+        out = _run_rank(ctx, A, 0, 1, kw)
+        L, U = rrlu_sharded_factors(ctx, A.shape[0], A.shape[1], out[0])
+    finally:
+        ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, 1))
+    res = _check(A, kw, out, L, U)
+    assert all(res.values()), res
+
+
+def _multi_worker(rank, world, port, outdir, mode):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ctx = T.Context(0)
+        host = Comm(device="cpu")
+        comm = exchange = None
+        if mode == "rccl":
+            comm = DeviceComm(ctx, host)
+        else:
+            exchange = HostExchange(ctx, host)
+        res = {}
+        for name, (A, kw) in _cases().items():
+            out = _run_rank(ctx, A, rank, world, kw, comm=comm, exchange=exchange)
+            L, U = rrlu_sharded_factors(ctx, A.shape[0], A.shape[1], out[0], host_comm=host)
+            res[name] = _check(A, kw, out, L, U)
+        if comm is not None:
+            comm.close()
+        ctx.close()
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,mode", [(2, "host"), (3, "host"), (1, "rccl")])
+def test_sharded_multi_rank_bitwise(tmp_path, world, mode):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_multi_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        bad = {k: v for k, v in res.items() if not all(v.values())}
+        assert not bad, (r, bad)
