@@ -216,9 +216,14 @@ def main():
 
     if not args.no_extras:
         sh = sharded_pi(T, ctx, dist, world, rank)
+        try:  # a failure of the multi-GPU extras must not cost the headline line
+            shr = sharded_extras(T, ctx, dist, world, rank, dev_res if rank == 0 else None)
+        except Exception as e:  # noqa: BLE001
+            shr = {"sharded_extras_error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             out["extras"] = extras(T, ctx)
             out["extras"]["pi_lorentz_sharded"] = sh
+            out["extras"].update(shr)
     parity_ok = True
     if rank == 0 and not args.no_cpu and world == 1:
         base, cpu_res = cpu_baseline(m, n, r, args.cpu_pivots)
@@ -250,6 +255,100 @@ def pmc_traffic(fam, m, n, r, nb, shadow):
     return {"traffic": rec["hbm_bytes_per_launch"],
             "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE, "
                               f"{rec['dispatches_profiled']} dispatches)"}
+
+
+def sharded_extras(T, ctx, dist, world, rank, full_res):
+    """Multi-GPU data path on device buffers, every rank:
+    * rrlu_sharded: one rrLU column-sharded over the ranks (tci_rrlu_sharded_d: per pivot one
+      candidate record all-gathered over RCCL), on the metric matrix (8192^2, r = 256; its pivots
+      must equal the unsharded device factorisation rank 0 ran above) and on a config-5-size
+      matrix (32768^2 = 8 GiB, r = 1024) -- strong scaling: value = flops / max-over-ranks time;
+    * pi_sharded_with_gather: the 8192^2 Lorentzian Pi evaluated by column blocks and all-gathered
+      into a replicated device matrix on every rank (ncclAllGather in place)."""
+    import ctypes as C
+
+    from tci_amd.distributed import Comm, DeviceComm, column_blocks, rrlu_sharded
+
+    host = Comm(device="cpu") if dist is not None else None
+    dcomm = DeviceComm(ctx, host)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def tmax(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    res = {}
+    recs = []
+    for (m, n, r, reps) in ((8192, 8192, 256, 3), (32768, 32768, 1024, 2)):
+        j0, j1 = column_blocks(n, world)[rank]
+        nloc = j1 - j0
+        A0 = T.DeviceMatrix(m, nloc + 1, ctx=ctx)
+        ctx.check(ctx.lib.tci_fill_uniform_block_d(ctx.h, A0.ptr, m, nloc, A0.ld, 0, m * j0))
+        W = T.DeviceMatrix(m, nloc + 1, ctx=ctx)
+        W.copy_from(A0)
+        out = rrlu_sharded(W, m, n, j0, nloc, comm=dcomm, maxrank=r)  # warm-up (+ pivots for parity)
+        times = []
+        for _ in range(reps):
+            W.copy_from(A0)
+            barrier()
+            t0 = time.perf_counter()
+            rrlu_sharded(W, m, n, j0, nloc, comm=dcomm, maxrank=r)
+            barrier()
+            times.append(time.perf_counter() - t0)
+        dt = tmax(min(times))
+        rec = {"m": m, "n": n, "r": r, "ranks": world, "npivot": out[0], "ms": round(dt * 1e3, 3),
+               "GFLOPs": round(rrlu_flops(m, n, out[0]) / dt / 1e9, 1),
+               "exchange_bytes_per_pivot": 8 * world * (4 + 16 + m)}
+        if full_res is not None and (m, n, r) == (8192, 8192, 256):
+            npd, rpd, cpd, ped = full_res
+            rec["pivots_equal_unsharded"] = bool(out[0] == npd and np.array_equal(out[2], rpd)
+                                                 and np.array_equal(out[3], cpd) and np.array_equal(out[4], ped))
+        recs.append(rec)
+        A0.free()
+        W.free()
+    res["rrlu_sharded"] = recs
+    # Pi assembly + device all-gather of the column blocks (n divisible by world: equal blocks)
+    m = n = 8192
+    rng = np.random.default_rng(1)
+    I = rng.integers(1, 11, (m, 10)).astype(np.int32)
+    J = rng.integers(1, 11, (n, 10)).astype(np.int32)
+    f = T.lorentz([10] * 20, ctx=ctx)
+    w = n // world
+    full = T.DeviceMatrix(m, w * world, ctx=ctx)
+    blk_ptr = C.c_void_p(full.ptr.value + 8 * full.ld * w * rank)
+    Jl = np.ascontiguousarray(J[rank * w:(rank + 1) * w])
+    mx = C.c_double()
+
+    def run():
+        ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(I), m, 10, T._lib.ptr(Jl), w, 10, 0, blk_ptr,
+                                          full.ld, C.byref(mx)))
+        dcomm.allgather(blk_ptr, full.ptr, 8 * full.ld * w)
+
+    run()
+    times = []
+    for _ in range(5):
+        barrier()
+        t0 = time.perf_counter()
+        run()
+        barrier()
+        times.append(time.perf_counter() - t0)
+    dt = tmax(min(times))
+    res["pi_sharded_with_gather"] = {"m": m, "n": w * world, "L": 20, "ranks": world,
+                                     "ms": round(dt * 1e3, 4), "pi_rows_per_s": round(m / dt, 1),
+                                     "gathered_GB": round(8.0 * full.ld * w * world / 1e9, 3),
+                                     "note": "column blocks evaluated per rank, ncclAllGather into a replicated "
+                                             "device Pi (no host staging)"}
+    full.free()
+    dcomm.close()
+    return res
 
 
 def sharded_pi(T, ctx, dist, world, rank):

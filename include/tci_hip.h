@@ -301,6 +301,11 @@ int tci_rrlu_sharded_factors_h(tci_ctx* ctx, double* L, double* U, int64_t ldu);
 int tci_fill_uniform_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
                        uint64_t seed);
 
+/* The same stream from element index `offset` on: (i, j) gets splitmix64(seed * K + offset + i + m*j);
+ * offset = m * c0 fills the column block [c0, c0 + n) of the m-row seed matrix (sharded inputs). */
+int tci_fill_uniform_block_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda,
+                             uint64_t seed, uint64_t offset);
+
 /* Diagnostic roofline calibration: average device time (ms) of a 16-B-per-lane stream read of
  * n doubles at d_a, and (if d_b) of a stream copy d_a -> d_b, over `reps` launches of `grid`
  * 256-thread workgroups (grid <= 0: 2048). */

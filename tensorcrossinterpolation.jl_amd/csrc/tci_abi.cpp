@@ -1685,6 +1685,15 @@ int tci_fill_uniform_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t ld
     return TCI_OK;
 }
 
+int tci_fill_uniform_block_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda, uint64_t seed,
+                             uint64_t offset) {
+    if (!c || lda < m) return TCI_ERR_ARG;
+    tci::launch_fill_uniform(c->stream, d_A, m, n, lda, seed, offset);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
 int tci_diag_stream_d(tci_ctx* c, const double* d_a, double* d_b, int64_t n, int reps, int grid,
                       double* ms_read, double* ms_copy) {
     if (!c || !d_a || n < 2 || reps < 1) return TCI_ERR_ARG;

@@ -244,10 +244,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-__global__ void k_fill_uniform(double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed) {
+__global__ void k_fill_uniform(double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed, uint64_t offset) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const uint64_t base = seed * 0xD1B54A32D192ED03ull;
+    const uint64_t base = seed * 0xD1B54A32D192ED03ull + offset;
     for (int64_t e = gid; e < m * n; e += stride) {
         const int64_t i = e % m, j = e / m;
         A[i + j * lda] = (double)(splitmix64(base + (uint64_t)e) >> 11) * 0x1.0p-53;
@@ -301,9 +301,9 @@ void launch_stream_copy(hipStream_t s, const double* a, double* b, int64_t n, in
 }
 
 void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda,
-                         uint64_t seed) {
+                         uint64_t seed, uint64_t offset) {
     hipLaunchKernelGGL(k_fill_uniform, dim3(grid_for(m * n, 8192)), dim3(256), 0, s, A, m, n, lda,
-                       seed);
+                       seed, offset);
 }
 
 // --------------------------------------------------------- batch evaluation

@@ -219,7 +219,8 @@ constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseAll = 7;
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
                          const int64_t* colperm, double* left, double* right, int dense);
-void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed);
+void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t lda, uint64_t seed,
+                         uint64_t offset = 0);
 void launch_stream_read(hipStream_t s, const double* a, int64_t n, unsigned long long* out, int grid);
 void launch_stream_copy(hipStream_t s, const double* a, double* b, int64_t n, int grid);
 

@@ -83,6 +83,7 @@ SIGNATURES = {
     "tci_sitetensor_solve_h": ([vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_tt_evaluate_h": ([vp, i32, vp, vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_fill_uniform_d": ([vp, vp, i64, i64, i64, C.c_uint64], C.c_int),
+    "tci_fill_uniform_block_d": ([vp, vp, i64, i64, i64, C.c_uint64, C.c_uint64], C.c_int),
     "tci_diag_stream_d": ([vp, vp, vp, i64, C.c_int, C.c_int, pdbl, pdbl], C.c_int),
     "tci_diag_mfma_f64": ([vp, pdbl], C.c_int),
     "tci_diag_mfma_f64_ex": ([vp, C.c_int, pdbl, pdbl], C.c_int),

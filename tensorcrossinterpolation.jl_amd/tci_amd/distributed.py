@@ -103,14 +103,77 @@ class Comm:
 class ShardedBatchEvaluator:
     """A BatchEvaluator{Float64} whose batch evaluation is split over the ranks of `comm` by
     column blocks of Jset; each rank's block runs on its own GPU through `local` (a
-    GPUBatchEvaluator on that rank's device)."""
+    GPUBatchEvaluator on that rank's device).
 
-    def __init__(self, local, comm):
+    shard_rrlu: the 2-site update keeps Pi sharded on the devices -- each rank evaluates its column
+    block into HBM and the column-sharded rrLU (tci_rrlu_sharded_d) factorises it across the ranks,
+    exchanging one candidate record per pivot over `device_comm` (a DeviceComm: RCCL) or, without
+    one, over the host group (HostExchange). Pi never leaves the devices and is never replicated.
+    Without shard_rrlu (or when the MatrixLUCI factors are needed) Pi is all-gathered and factorised
+    replicated, as before."""
+
+    def __init__(self, local, comm, shard_rrlu=False, device_comm=None):
         self.local = local
         self.comm = comm
         self.localdims = list(local.localdims)
         self.L = len(self.localdims)
         self.name = f"sharded({getattr(local, 'name', 'f')})"
+        self.shard_rrlu = bool(shard_rrlu)
+        self.device_comm = device_comm
+        self._exchange = None
+        self._buf = None
+
+    @property
+    def ctx(self):
+        return self.local.ctx
+
+    def exchange(self):
+        if self.device_comm is None and self._exchange is None:
+            self._exchange = HostExchange(self.local.ctx, self.comm)
+        return self._exchange
+
+    def local_block_device(self, I, J, M=0):
+        """This rank's block of Pi evaluated into HBM, as an m x (nloc + 1) device matrix (the last
+        column is the sharded rrLU's scratch), plus (j0, j1) and the global max|Pi|."""
+        from . import _lib
+
+        ctx = self.local.ctx
+        I = np.ascontiguousarray(np.asarray(I, np.int32))
+        J = np.ascontiguousarray(np.asarray(J, np.int32))
+        m, nl = I.shape
+        D = self.localdims[nl] if M == 1 else 1
+        j0, j1 = self.block(len(J))
+        nloc = j1 - j0
+        rows = m * D
+        ld = max(16, (rows + 15) // 16 * 16)
+        need = ld * (nloc + 1)
+        if self._buf is None or self._buf.size < need:
+            if self._buf is not None:
+                self._buf.free()
+            self._buf = _DevBuf(ctx, int(need * 1.25) + 1024)
+        view = _DevView(ctx, self._buf.ptr, rows, nloc + 1, ld)
+        mx = 0.0
+        if nloc > 0 and rows > 0:
+            Jl = np.ascontiguousarray(J[j0:j1])
+            m_ = C.c_double()
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), nloc,
+                                              Jl.shape[1], M, view.ptr, ld, C.byref(m_)))
+            mx = m_.value
+        return view, (j0, j1), self.comm.allreduce_maxabs(mx)
+
+    def update_pivots_sharded(self, rows, cols, maxrank, reltol, abstol, leftorth):
+        """updatepivots!'s :full search with Pi sharded on the devices: returns the dict of
+        tensorci2.update_pivots_device (pivot positions, pivot errors, max|Pi|; no factors)."""
+        rows = np.asarray(rows, np.int32)
+        cols = np.asarray(cols, np.int32)
+        view, (j0, j1), gmx = self.local_block_device(rows, cols, 0)
+        m, n = len(rows), len(cols)
+        npv, err, rp, cp, pe = rrlu_sharded(view, m, n, j0, j1 - j0, comm=self.device_comm,
+                                            exchange=None if self.device_comm is not None else self.exchange(),
+                                            maxrank=min(int(maxrank), m, n), reltol=reltol, abstol=abstol,
+                                            leftorthogonal=leftorth)
+        return {"rowidx": rp[:npv].copy(), "colidx": cp[:npv].copy(), "pivoterrors": pe.copy(), "maxabs": gmx,
+                "npivot": npv}
 
     def block(self, n):
         """This rank's column range of an n-column Pi."""
@@ -161,25 +224,52 @@ class ShardedBatchEvaluator:
 
 
 # ------------------------------------------------------------------ device-resident data path
+class _DevBuf:
+    """Raw device allocation owned by a context (float64 elements)."""
+
+    def __init__(self, ctx, nelem):
+        self.ctx, self.size = ctx, int(nelem)
+        p = C.c_void_p()
+        ctx.check(ctx.lib.tci_malloc_d(ctx.h, C.byref(p), self.size * 8))
+        self.ptr = p
+        ctx.own(self)
+
+    def free(self):
+        if self.ptr and self.ctx.alive:
+            self.ctx.lib.tci_free_d(self.ctx.h, self.ptr)
+        self.ptr = None
+
+    release = free
+
+
+class _DevView:
+    """m x n column-major view (ld) of device memory, DeviceMatrix-like."""
+
+    def __init__(self, ctx, ptr, m, n, ld):
+        self.ctx, self.ptr, self.m, self.n, self.ld = ctx, ptr, int(m), int(n), int(ld)
+
+
 class DeviceComm:
     """An RCCL communicator inside libtci_hip.so (tci_comm_*), bound to a context's device and
     stream: collectives on device buffers, enqueued on the context stream -- no host staging.
     The 128-byte unique id goes from rank 0 to the others over `comm` (a `Comm`, i.e. the
     torch.distributed host group)."""
 
-    def __init__(self, ctx, comm):
+    def __init__(self, ctx, comm=None):
         from . import _lib
 
-        self.ctx, self.rank, self.world = ctx, comm.rank, comm.world
+        self.ctx = ctx
+        self.rank, self.world = (comm.rank, comm.world) if comm is not None else (0, 1)
         lib = ctx.lib
         nbytes = C.c_int64()
         ctx.check(lib.tci_comm_unique_id(None, C.byref(nbytes)))
         uid = np.zeros(nbytes.value, np.uint8)
-        if comm.rank == 0:
+        if self.rank == 0:
             ctx.check(lib.tci_comm_unique_id(_lib.ptr(uid), None))
-        uid = comm.broadcast_bytes(uid)
+        if comm is not None:
+            uid = comm.broadcast_bytes(uid)
         h = C.c_void_p()
-        ctx.check(lib.tci_comm_create(ctx.h, comm.world, comm.rank, _lib.ptr(uid), C.byref(h)))
+        ctx.check(lib.tci_comm_create(ctx.h, self.world, self.rank, _lib.ptr(uid), C.byref(h)))
         self.h = h
         ctx.own(self)
 

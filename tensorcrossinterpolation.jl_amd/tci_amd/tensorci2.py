@@ -464,6 +464,8 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
     if getattr(f, "is_complex", False):
         return _update_pivots_c128(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                    want_left, want_right)
+    if getattr(f, "shard_rrlu", False) and not want_factors:
+        return f.update_pivots_sharded(rows, cols, maxrank, reltol, abstol, leftorth)
     if not hasattr(f, "h"):
         return _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                       want_left, want_right)

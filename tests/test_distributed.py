@@ -104,7 +104,7 @@ def test_sharded_batcheval_gloo(tmp_path, world):
         assert all(res.values()), (r, res)
 
 
-def _gpu_worker(rank, world, port, outdir):
+def _gpu_worker(rank, world, port, outdir, shard_rrlu=False):
     import torch.distributed as dist
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -113,13 +113,13 @@ def _gpu_worker(rank, world, port, outdir):
 
         ctx = T.context(0)
         local = T.lorentz([8] * 6, ctx=ctx)
-        fs = ShardedBatchEvaluator(local, Comm(device="cpu"))
+        fs = ShardedBatchEvaluator(local, Comm(device="cpu"), shard_rrlu=shard_rrlu)
         kw = dict(tolerance=1e-10, maxiter=8, nsearchglobalpivot=0)
         tci, ranks, errors = T.crossinterpolate2(fs, [8] * 6, **kw)
         ref, rranks, rerrors = T.crossinterpolate2(local, [8] * 6, **kw)
         q = T.quantics_osc(16, ctx=ctx)
         p0 = T.optfirstpivot(q, [2] * 16)
-        qs = ShardedBatchEvaluator(q, Comm(device="cpu"))
+        qs = ShardedBatchEvaluator(q, Comm(device="cpu"), shard_rrlu=shard_rrlu)
         t2, r2, e2 = T.crossinterpolate2(qs, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
         t2r, r2r, e2r = T.crossinterpolate2(q, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
         res = {
@@ -136,10 +136,13 @@ def _gpu_worker(rank, world, port, outdir):
 
 
 @pytest.mark.gpu
-def test_sharded_tci2_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("shard_rrlu", [False, True])
+def test_sharded_tci2_two_ranks_one_gpu(tmp_path, shard_rrlu):
+    """shard_rrlu=False: Pi all-gathered, replicated rrLU; True: Pi stays sharded on the device and
+    the column-sharded rrLU factorises it across the ranks (host exchange: two ranks share cuda:0)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_gpu_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_gpu_worker, args=(2, _free_port(), str(tmp_path), shard_rrlu), nprocs=2, join=True)
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
     for r in res:
         assert r["ranks"] and r["errors"] and r["isets"] and r["jsets"] and r["qosc"], r
