@@ -48,6 +48,7 @@ struct DgemmArgs {
     const int64_t* rmap;
     const int64_t* cmap;
     int tm, tn;  // tiles along m and n
+    unsigned long long* maxbits;  // optional: atomicMax of |Out| bit patterns (Julia's NaN-propagating max)
 };
 
 template <int WM, int WN, int FM, int FN, bool TB>
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
         cur ^= 1;
     }
     // acc[x][y][q]: row i = wr + 16x + (lane & 15), column j = wc + 16y + (lane >> 4) + 4q
+    unsigned long long mb = 0;  // |v| bits: unsigned order = value order, +NaN above +Inf
 #pragma unroll
     for (int x = 0; x < FM; ++x) {
         const int i = i0 + wr + 16 * x + r;
@@ -156,7 +158,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
                 if (g.beta != 0.0) v = g.beta * g.C[(int64_t)i + (int64_t)j * g.ldc] + v;
                 const int64_t ocol = g.cmap ? g.cmap[j] : j;
                 g.Out[orow + ocol * g.ldo] = v;
+                const unsigned long long b = (unsigned long long)__double_as_longlong(fabs(v));
+                mb = b > mb ? b : mb;
             }
+    }
+    if (g.maxbits) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(mb, off);
+            mb = o > mb ? o : mb;
+        }
+        if (lane == 0) atomicMax(g.maxbits, mb);
     }
 }
 
@@ -185,10 +197,11 @@ static void dgemm_go(hipStream_t s, DgemmArgs g) {
 
 void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
                   int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
-                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap) {
+                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap,
+                  unsigned long long* maxbits) {
     if (m <= 0 || n <= 0) return;
     DgemmArgs g{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, Out ? Out : const_cast<double*>(C),
-                Out ? ldo : ldc, rmap, cmap, 0, 0};
+                Out ? ldo : ldc, rmap, cmap, 0, 0, maxbits};
     if (tb) dgemm_go<true>(s, g);
     else dgemm_go<false>(s, g);
 }

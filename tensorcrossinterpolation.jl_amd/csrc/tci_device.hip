@@ -193,9 +193,6 @@ __global__ void k_right_scatter_ro(const double* __restrict__ U, int64_t ldu, in
 
 void trsm_luci_left(hipStream_t s, double* L, int64_t ldl, int m, int np);
 void trsm_luci_right(hipStream_t s, double* U, int64_t ldu, int n, int np);
-void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
-                  int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
-                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap);
 
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
@@ -917,74 +914,9 @@ __global__ __launch_bounds__(256) void k_gemm_cp(const double* __restrict__ EL, 
     block_maxabs(mx, maxbits);
 }
 
-// Large products: a workgroup (4 waves) owns a 128 x 128 tile, each wave 64 x 64 (4 x 4 MFMA
-// blocks, 16 accumulators); K advances in blocks of 16 staged in LDS (k-major rows padded by 8
-// doubles against bank conflicts), 16 MFMAs per 8 fragment reads.
+// Large products go through the K3 kernel (tci_dense.hip k_dgemm: 128 x 128 tiles, two waves per
+// SIMD); k staged 16 at a time, so the factors are padded to a multiple of kGemmKB rows.
 constexpr int kGemmKB = 16;
-constexpr int kGemmLd = 128 + 8;
-
-__global__ __launch_bounds__(256) void k_gemm_cp_lds(const double* __restrict__ EL, int64_t ldR,
-                                                     const double* __restrict__ ER, int64_t ldC, int Kp,
-                                                     int64_t mR, int n, double* __restrict__ out,
-                                                     int64_t ldo, unsigned long long* maxbits) {
-    __shared__ double As[kGemmKB * kGemmLd];
-    __shared__ double Bs[kGemmKB * kGemmLd];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t R0 = (int64_t)blockIdx.x * 128, j0 = (int64_t)blockIdx.y * 128;
-    const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
-    const int r = lane & 15, kk = lane >> 4;
-    dbl4 acc[4][4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = dbl4{0.0, 0.0, 0.0, 0.0};
-    for (int kb = 0; kb < Kp; kb += kGemmKB) {
-        // stage 16 x 128 of each factor: 8 doubles per thread each, as double2
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = threadIdx.x + q * 256;  // double2 index in [0, 1024)
-            const int row = e >> 6, c = (e & 63) * 2;
-            const double2 a = *reinterpret_cast<const double2*>(EL + (int64_t)(kb + row) * ldR + R0 + c);
-            const double2 b = *reinterpret_cast<const double2*>(ER + (int64_t)(kb + row) * ldC + j0 + c);
-            As[row * kGemmLd + c] = a.x;
-            As[row * kGemmLd + c + 1] = a.y;
-            Bs[row * kGemmLd + c] = b.x;
-            Bs[row * kGemmLd + c + 1] = b.y;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k4 = 0; k4 < kGemmKB; k4 += 4) {
-            double af[4], bf[4];
-#pragma unroll
-            for (int x = 0; x < 4; ++x) af[x] = As[(k4 + kk) * kGemmLd + wr + 16 * x + r];
-#pragma unroll
-            for (int y = 0; y < 4; ++y) bf[y] = Bs[(k4 + kk) * kGemmLd + wc + 16 * y + r];
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[x], bf[y], acc[x][y], 0, 0, 0);
-        }
-        __syncthreads();
-    }
-    double mx = 0.0;
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int64_t R = R0 + wr + 16 * x + (lane >> 4) + 4 * g;
-                const int64_t j = j0 + wc + 16 * y + (lane & 15);
-                if (R < mR && j < n) {
-                    const double v = acc[x][y][g];
-                    out[R + ldo * j] = v;
-                    const double av = fabs(v);
-                    mx = (isnan(av) || av > mx) ? av : mx;
-                }
-            }
-    block_maxabs(mx, maxbits);
-}
 
 // fp64 MFMA throughput probe (diagnostic): every wave issues independent 16x16x4 chains
 __global__ __launch_bounds__(256) void k_mfma_f64_probe(int iters, double* sink) {
@@ -1041,9 +973,9 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
             hipLaunchKernelGGL(k_cp_factors, dim3(grid_for(ldC * K4, 4096)), dim3(256), 0, s, f, J, nr,
                                n, 1, 0, K, K4, ldC, f.L - nr, true, ER);
         }
-        if (mR >= 128 && n >= 128 && K4 >= 32)
-            hipLaunchKernelGGL(k_gemm_cp_lds, dim3((unsigned)(ldR / 128), (unsigned)(ldC / 128)), dim3(256),
-                               0, s, EL, ldR, ER, ldC, K4, mR, n, out, ldo, maxbits);
+        if (mR >= 128 && n >= 128 && K4 >= 32)  // Pi = EL^T ER on the K3 kernel (2 waves / SIMD)
+            launch_dgemm(s, true, (int)mR, n, K4, 1.0, EL, ldR, ER, ldC, 0.0, nullptr, 0, out, ldo, nullptr, nullptr,
+                         maxbits);
         else
             hipLaunchKernelGGL(k_gemm_cp, dim3((unsigned)(ldR / 64), (unsigned)(ldC / 64)), dim3(256), 0,
                                s, EL, ldR, ER, ldC, K4, mR, n, out, ldo, maxbits);

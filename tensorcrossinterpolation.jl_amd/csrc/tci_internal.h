@@ -235,9 +235,11 @@ int64_t batcheval_scratch_bytes(const FuncDev& f, int m, int D, int n);
 // ---- fp64 MFMA dense algebra (tci_dense.hip)
 // Out = beta C + alpha A op(B) (op(B) = B, or with tb B(t, j) = B[j + t ldb]); Out null: in place
 // in C; rmap / cmap (nullable) scatter result (i, j) to Out[rmap[i] + cmap[j] ldo].
+// maxbits (nullable): atomicMax of the |result| bit patterns (the fused maxabs of batch evaluation)
 void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, const double* A,
                   int64_t lda, const double* B, int64_t ldb, double beta, const double* C,
-                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap);
+                  int64_t ldc, double* Out, int64_t ldo, const int64_t* rmap, const int64_t* cmap,
+                  unsigned long long* maxbits = nullptr);
 // probe: waves_per_simd in {1, 2, 4}, one workgroup per CU; cycles[grid]: clock64 cycles of the loop
 void launch_mfma_probe2(hipStream_t s, int waves_per_simd, int grid, int iters, double* sink,
                         long long* cycles);
