@@ -49,6 +49,20 @@ class OracleEvaluator:
         out, mx = self.O.batcheval(self.kind, self.params, self.localdims, I, J, M)
         return out.reshape((-1, len(J)), order="F"), mx
 
+    def points(self, X):
+        X = np.asarray(X, np.int32).reshape(-1, len(self.localdims))
+        return self.pi(np.zeros((1, 0), np.int32), X)[0][0, :].copy()
+
+
+class ZeroTT:
+    """Test-only stand-in for a TensorCI2 in the global search: tt(x) = 0, so |f - tt| = |f|."""
+
+    def __init__(self, localdims):
+        self.localdims = list(localdims)
+
+    def evaluate_many(self, X, ctx=None):
+        return np.zeros(len(X))
+
 
 def _cpu_worker(rank, world, port, outdir):
     import torch.distributed as dist
@@ -122,7 +136,13 @@ def _gpu_worker(rank, world, port, outdir, shard_rrlu=False):
         qs = ShardedBatchEvaluator(q, Comm(device="cpu"), shard_rrlu=shard_rrlu)
         t2, r2, e2 = T.crossinterpolate2(qs, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
         t2r, r2r, e2r = T.crossinterpolate2(q, [2] * 16, [p0], tolerance=1e-8, maxiter=6, nsearchglobalpivot=0)
+        # with the default global pivot search, starts split over the ranks (same seed as one process)
+        kwg = dict(tolerance=1e-10, maxiter=8, nsearchglobalpivot=5)
+        tg, rg, eg = T.crossinterpolate2(fs, [8] * 6, rng=np.random.default_rng(3), **kwg)
+        tgr, rgr, egr = T.crossinterpolate2(local, [8] * 6, rng=np.random.default_rng(3), **kwg)
         res = {
+            "global_search": rg == rgr and list(eg) == list(egr)
+                             and all(np.array_equal(a, b) for a, b in zip(tg.Iset, tgr.Iset)),
             "ranks": ranks == rranks, "errors": list(errors) == list(rerrors),
             "isets": all(np.array_equal(a, b) for a, b in zip(tci.Iset, ref.Iset)),
             "jsets": all(np.array_equal(a, b) for a, b in zip(tci.Jset, ref.Jset)),
@@ -145,7 +165,7 @@ def test_sharded_tci2_two_ranks_one_gpu(tmp_path, shard_rrlu):
     mp.spawn(_gpu_worker, args=(2, _free_port(), str(tmp_path), shard_rrlu), nprocs=2, join=True)
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
     for r in res:
-        assert r["ranks"] and r["errors"] and r["isets"] and r["jsets"] and r["qosc"], r
+        assert r["ranks"] and r["errors"] and r["isets"] and r["jsets"] and r["qosc"] and r["global_search"], r
     assert res[0]["linkdims"] == res[1]["linkdims"]
 
 
@@ -194,6 +214,41 @@ def test_sharded_rrlu_protocol_gloo(tmp_path, world):
     import torch.multiprocessing as mp
 
     mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        assert all(res.values()), (r, res)
+
+
+def _search_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from tci_amd.globalpivotfinder import DefaultGlobalPivotFinder
+
+        ld = [5, 7, 4, 6, 3]
+        res = {}
+        for nsearch in (1, 5, 9):
+            finder = DefaultGlobalPivotFinder(nsearch=nsearch, maxnglobalpivot=5)
+            fs = ShardedBatchEvaluator(OracleEvaluator(1, [1.0], ld), Comm(device="cpu"))
+            # rank 0's generator decides the starts; the single-process run uses the same seed
+            got = finder(ZeroTT(ld), fs, 1e-6, rng=np.random.default_rng(100 + nsearch if rank == 0 else 7))
+            ref = finder(ZeroTT(ld), OracleEvaluator(1, [1.0], ld), 1e-6, rng=np.random.default_rng(100 + nsearch))
+            res[f"n{nsearch}"] = got == ref and len(ref) == min(nsearch, 5)
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_global_search_gloo(tmp_path, world):
+    """The global pivot search with its starts split over the ranks finds the same pivots, in the
+    same order, as one process from the same starts (globalpivotfinder.jl:219-252)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_search_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         res = json.load(open(tmp_path / f"rank{r}.json"))
         assert all(res.values()), (r, res)
