@@ -58,6 +58,7 @@ extern "C" {
 typedef struct tci_ctx tci_ctx;
 typedef struct tci_func tci_func;
 typedef struct tci_comm tci_comm;
+typedef struct tci_cache tci_cache;
 /* Host-side exchange hook of the column-sharded rrLU: all-gather `count` doubles per rank from
  * d_send into d_recv (rank-major; device pointers of the calling context). Returns 0 on success.
  * Used when no RCCL communicator is passed (e.g. ranks sharing one GPU, or a Julia Distributed
@@ -263,6 +264,26 @@ int tci_sitetensor_solve_c128_h(tci_ctx* ctx, const double* P, int64_t r, const 
 int tci_tt_evaluate_c128_h(tci_ctx* ctx, int32_t L, const int32_t* dims, const int32_t* bonddims,
                            const double* cores, int64_t ncore, const int32_t* X, int64_t npts,
                            double* out);
+
+/* ------------------------------------------------- CachedFunction memo on the device
+ * CachedFunction{Float64}(f, localdims) (cachedfunction.jl:53-135) over a device integrand: the
+ * memo is a hash table in HBM keyed by key(x) = sum((x .- 1) .* coeffs), coeffs =
+ * cumprod([1; localdims[1:end-1]]) (:197-199; index spaces below 2^62.5 keys, else TCI_ERR_ARG).
+ * tci_cache_batcheval_d/h are tci_batcheval_d/h through the memo (the batch method, :255-302):
+ * hits come from the table, the distinct misses of the batch are evaluated in one batch
+ * evaluation of f and inserted; *nmiss = how many. The table grows (rehash) as needed. */
+int tci_cache_create(tci_ctx* ctx, const int32_t* localdims, int32_t L, int64_t capacity, tci_cache** out);
+int tci_cache_destroy(tci_cache* cache);
+int tci_cache_clear(tci_cache* cache);                /* clearcache!(cf), :305-308 */
+int tci_cache_size(tci_cache* cache, int64_t* n);     /* length of cacheddata(cf) */
+/* cacheddata(cf) (:160-170) as (key, value) pairs: up to capacity written, *n = stored entries */
+int tci_cache_dump_h(tci_cache* cache, int64_t* keys, double* vals, int64_t capacity, int64_t* n);
+int tci_cache_batcheval_d(tci_ctx* ctx, tci_cache* cache, const tci_func* f, const int32_t* I, int64_t m,
+                          int32_t nl, const int32_t* J, int64_t n, int32_t nr, int32_t M, double* d_out,
+                          int64_t ldo, double* maxabs, int64_t* nmiss);
+int tci_cache_batcheval_h(tci_ctx* ctx, tci_cache* cache, const tci_func* f, const int32_t* I, int64_t m,
+                          int32_t nl, const int32_t* J, int64_t n, int32_t nr, int32_t M, double* out,
+                          int64_t ldo, double* maxabs, int64_t* nmiss);
 
 /* ------------------------------------------------- multi-GPU: RCCL over xGMI
  * One process per GPU. Rank 0 makes the 128-byte unique id (tci_comm_unique_id; nbytes gets its

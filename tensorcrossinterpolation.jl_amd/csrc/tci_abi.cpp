@@ -139,6 +139,25 @@ struct tci_comm {
     int nranks = 1, rank = 0;
 };
 
+struct tci_cache {
+    tci_ctx* ctx = nullptr;
+    int L = 0;
+    std::vector<int64_t> coeffs;
+    int64_t* dcoeff = nullptr;
+    unsigned long long* keys = nullptr;
+    double* vals = nullptr;
+    unsigned* state = nullptr;
+    int64_t cap = 0, size = 0;
+    int64_t *kI = nullptr, *kJ = nullptr, *miss = nullptr, *dup = nullptr;
+    size_t capKI = 0, capKJ = 0, capMiss = 0, capDup = 0;
+    int32_t* X = nullptr;
+    size_t capX = 0;
+    double* mv = nullptr;
+    size_t capMv = 0;
+    unsigned long long* counts = nullptr;
+    unsigned long long* hcounts = nullptr;
+};
+
 struct tci_func {
     tci_ctx* ctx = nullptr;
     int kind = 0;
@@ -1853,6 +1872,198 @@ int tci_rrlu_sharded_factors_h(tci_ctx* c, double* L, double* U, int64_t ldu) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (*c->hflag & 1) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
     if (*c->hflag & 2) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    return TCI_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ CachedFunction device memo
+namespace {
+
+int cache_alloc_table(tci_cache* h, int64_t cap) {
+    tci_ctx* c = h->ctx;
+    unsigned long long* k = nullptr;
+    double* v = nullptr;
+    unsigned* st = nullptr;
+    if (hipMalloc((void**)&k, cap * 8) != hipSuccess || hipMalloc((void**)&v, cap * 8) != hipSuccess ||
+        hipMalloc((void**)&st, cap * 4) != hipSuccess) {
+        if (k) hipFree(k);
+        if (v) hipFree(v);
+        return set_err(c, TCI_ERR_NOMEM, "cache: table allocation failed");
+    }
+    HIPCHK(c, hipMemsetAsync(k, 0xff, cap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(st, 0, cap * 4, c->stream));
+    if (h->keys) {  // rehash the ready entries
+        tci::launch_cache_rehash(c->stream, h->keys, h->vals, h->cap, k, v, st, cap);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(h->keys);
+        hipFree(h->vals);
+        hipFree(h->state);
+    }
+    h->keys = k;
+    h->vals = v;
+    h->state = st;
+    h->cap = cap;
+    return TCI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tci_cache_create(tci_ctx* c, const int32_t* localdims, int32_t L, int64_t capacity, tci_cache** out) {
+    if (!c || !out || L <= 0 || !localdims) return TCI_ERR_ARG;
+    *out = nullptr;
+    double log2space = 0;
+    for (int t = 0; t < L; ++t) {
+        if (localdims[t] <= 0) return set_err(c, TCI_ERR_ARG, "cache: localdims must be positive");
+        log2space += std::log2((double)localdims[t]);
+    }
+    if (log2space >= 62.5) return set_err(c, TCI_ERR_ARG, "cache: index space beyond 2^62 keys (use a host cache)");
+    tci_cache* h = new tci_cache();
+    h->ctx = c;
+    h->L = L;
+    h->coeffs.assign(L, 1);
+    for (int t = 1; t < L; ++t) h->coeffs[t] = h->coeffs[t - 1] * localdims[t - 1];
+    int64_t cap = 1024;
+    while (cap < 2 * capacity) cap <<= 1;
+    int st;
+    if (hipMalloc((void**)&h->dcoeff, L * 8) != hipSuccess || hipMalloc((void**)&h->counts, 16) != hipSuccess ||
+        hipHostMalloc((void**)&h->hcounts, 16, 0) != hipSuccess) {
+        tci_cache_destroy(h);
+        return TCI_ERR_NOMEM;
+    }
+    if (hipMemcpy(h->dcoeff, h->coeffs.data(), L * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        (st = cache_alloc_table(h, cap))) {
+        tci_cache_destroy(h);
+        return TCI_ERR_DEVICE;
+    }
+    *out = h;
+    return TCI_OK;
+}
+
+int tci_cache_destroy(tci_cache* h) {
+    if (!h) return TCI_OK;
+    if (h->ctx && h->ctx->stream) hipStreamSynchronize(h->ctx->stream);
+    for (void* p : {(void*)h->dcoeff, (void*)h->keys, (void*)h->vals, (void*)h->state, (void*)h->kI, (void*)h->kJ,
+                    (void*)h->miss, (void*)h->dup, (void*)h->X, (void*)h->mv, (void*)h->counts})
+        if (p) hipFree(p);
+    if (h->hcounts) hipHostFree(h->hcounts);
+    delete h;
+    return TCI_OK;
+}
+
+int tci_cache_clear(tci_cache* h) {
+    if (!h) return TCI_ERR_ARG;
+    tci_ctx* c = h->ctx;
+    HIPCHK(c, hipMemsetAsync(h->keys, 0xff, h->cap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(h->state, 0, h->cap * 4, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    h->size = 0;
+    return TCI_OK;
+}
+
+int tci_cache_size(tci_cache* h, int64_t* n) {
+    if (!h || !n) return TCI_ERR_ARG;
+    *n = h->size;
+    return TCI_OK;
+}
+
+int tci_cache_dump_h(tci_cache* h, int64_t* keys, double* vals, int64_t capacity, int64_t* n) {
+    if (!h || !n) return TCI_ERR_ARG;
+    tci_ctx* c = h->ctx;
+    std::vector<unsigned long long> k(h->cap);
+    std::vector<double> v(h->cap);
+    HIPCHK(c, hipMemcpyAsync(k.data(), h->keys, h->cap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(v.data(), h->vals, h->cap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int64_t q = 0;
+    for (int64_t s = 0; s < h->cap; ++s) {
+        if (k[s] == ~0ull) continue;
+        if (keys && vals && q < capacity) {
+            keys[q] = (int64_t)k[s];
+            vals[q] = v[s];
+        }
+        ++q;
+    }
+    *n = q;
+    return TCI_OK;
+}
+
+int tci_cache_batcheval_d(tci_ctx* c, tci_cache* h, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                          const int32_t* J, int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo,
+                          double* maxabs, int64_t* nmiss) {
+    if (!c || !h || !f || h->ctx != c || m < 0 || n < 0) return TCI_ERR_ARG;
+    if (f->L != h->L) return set_err(c, TCI_ERR_ARG, "cache: the integrand's leg count differs from the cache's");
+    if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+    if (M < 0 || M > 1) return set_err(c, TCI_ERR_ARG, "only M = 0 or M = 1 centre legs are supported");
+    const int64_t D = M ? f->localdims[nl] : 1, mR = m * D, tot = mR * n;
+    if (ldo < mR) return set_err(c, TCI_ERR_ARG, "ldo < m * prod(centre dims)");
+    if (nmiss) *nmiss = 0;
+    if (maxabs) *maxabs = 0.0;
+    if (tot == 0) return TCI_OK;
+    int st;
+    if ((st = upload_index(c, &c->dI, &c->capI, I, m, nl))) return st;
+    if ((st = upload_index(c, &c->dJ, &c->capJ, J, n, nr))) return st;
+    if (2 * (h->size + tot) > h->cap) {
+        int64_t cap = h->cap;
+        while (2 * (h->size + tot) > cap) cap <<= 1;
+        if ((st = cache_alloc_table(h, cap))) return st;
+    }
+    if ((st = ensure(c, &h->kI, &h->capKI, (size_t)m))) return st;
+    if ((st = ensure(c, &h->kJ, &h->capKJ, (size_t)n))) return st;
+    if ((st = ensure(c, &h->miss, &h->capMiss, (size_t)(2 * tot)))) return st;
+    if ((st = ensure(c, &h->dup, &h->capDup, (size_t)tot))) return st;
+    tci::launch_cache_partial_keys(c->stream, c->dI, (int)m, nl, h->dcoeff, 0, h->kI);
+    tci::launch_cache_partial_keys(c->stream, c->dJ, (int)n, nr, h->dcoeff, f->L - nr, h->kJ);
+    HIPCHK(c, hipMemsetAsync(h->counts, 0, 16, c->stream));
+    tci::CacheProbeArgs a{h->keys, h->vals, h->state, h->cap, h->kI, h->kJ, M ? h->coeffs[nl] : 0, m, mR, n, d_out,
+                          ldo, h->miss, h->dup, h->counts};
+    if (m == 0 || nl == 0) HIPCHK(c, hipMemsetAsync(h->kI, 0, 8 * std::max<int64_t>(m, 1), c->stream));
+    if (n == 0 || nr == 0) HIPCHK(c, hipMemsetAsync(h->kJ, 0, 8 * std::max<int64_t>(n, 1), c->stream));
+    tci::launch_cache_probe(c->stream, a);
+    HIPCHK(c, hipMemcpyAsync(h->hcounts, h->counts, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t nm = (int64_t)h->hcounts[0], nd = (int64_t)h->hcounts[1];
+    if (nm > 0) {
+        if ((st = ensure(c, &h->X, &h->capX, (size_t)(nm * f->L)))) return st;
+        if ((st = ensure(c, &h->mv, &h->capMv, (size_t)nm))) return st;
+        tci::launch_cache_gather_points(c->stream, h->miss, nm, c->dI, nl, c->dJ, nr, M, m, mR, h->X);
+        // the misses as ONE batch evaluation: no left legs, the points as columns
+        if ((st = batcheval_launch(c, f, c->dI, 1, 0, h->X, nm, f->L, 0, h->mv, 1))) return st;
+        tci::launch_cache_fill(c->stream, h->miss, nm, h->mv, h->vals, h->state, mR, d_out, ldo);
+    }
+    tci::launch_cache_dups(c->stream, a, nd);
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, 8, c->stream));
+    tci::launch_cache_maxabs(c->stream, d_out, mR, n, ldo, c->maxbits);
+    HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    h->size += nm;
+    if (nmiss) *nmiss = nm;
+    if (maxabs) {
+        double v;
+        unsigned long long b = *c->hmaxbits;
+        memcpy(&v, &b, sizeof v);
+        *maxabs = v;
+    }
+    return TCI_OK;
+}
+
+int tci_cache_batcheval_h(tci_ctx* c, tci_cache* h, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,
+                          const int32_t* J, int64_t n, int32_t nr, int32_t M, double* out, int64_t ldo,
+                          double* maxabs, int64_t* nmiss) {
+    if (!c || !f) return TCI_ERR_ARG;
+    const int64_t D = (M && nl < f->L) ? f->localdims[nl] : 1, mR = m * D;
+    const int64_t ld = round_up(std::max<int64_t>(mR, 1), 2);
+    int st;
+    if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(ld * std::max<int64_t>(n, 1))))) return st;
+    if ((st = tci_cache_batcheval_d(c, h, f, I, m, nl, J, n, nr, M, c->dF1, ld, maxabs, nmiss))) return st;
+    if (out && mR > 0 && n > 0) {
+        HIPCHK(c, hipMemcpy2DAsync(out, ldo * sizeof(double), c->dF1, ld * sizeof(double), mR * sizeof(double), n,
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     return TCI_OK;
 }
 

@@ -210,6 +210,35 @@ void launch_extract_shard(hipStream_t s, const double* Lp, int64_t ldlp, const d
                           int n, int np, int leftorth, double* L, int64_t ldl, double* U, int64_t ldu,
                           int* flag, int64_t c0, int nloc);
 
+// ---- CachedFunction device memo (tci_cache.hip)
+struct CacheProbeArgs {
+    unsigned long long* keys;
+    double* vals;
+    unsigned* state;
+    int64_t cap;
+    const int64_t* kI;
+    const int64_t* kJ;
+    int64_t ccoef;
+    int64_t m, mR, n;
+    double* out;
+    int64_t ldo;
+    int64_t* miss;
+    int64_t* dup;
+    unsigned long long* counts;
+};
+void launch_cache_partial_keys(hipStream_t s, const int32_t* T, int cnt, int w, const int64_t* coeff, int t0,
+                               int64_t* out);
+void launch_cache_probe(hipStream_t s, const CacheProbeArgs& a);
+void launch_cache_gather_points(hipStream_t s, const int64_t* miss, int64_t nmiss, const int32_t* I, int nl,
+                                const int32_t* J, int nr, int M, int64_t m, int64_t mR, int32_t* X);
+void launch_cache_fill(hipStream_t s, const int64_t* miss, int64_t nmiss, const double* v, double* vals,
+                       unsigned* state, int64_t mR, double* out, int64_t ldo);
+void launch_cache_dups(hipStream_t s, const CacheProbeArgs& a, int64_t ndup);
+void launch_cache_maxabs(hipStream_t s, const double* out, int64_t mR, int64_t n, int64_t ldo,
+                         unsigned long long* maxbits);
+void launch_cache_rehash(hipStream_t s, const unsigned long long* ok, const double* ov, int64_t ocap,
+                         unsigned long long* nk, double* nv, unsigned* ns, int64_t ncap);
+
 // ---- factors, batch evaluation, solve (tci_device.hip)
 // MatrixLUCI factors from position-order L (m x np) / U (np x n); L rows >= np (leftorth) or U
 // columns >= np (otherwise) are overwritten by the triangular solve.

@@ -90,6 +90,13 @@ SIGNATURES = {
     "tci_sitetensor_solve_d": ([vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_dgemm_d": ([vp, C.c_int, i64, i64, i64, dbl, vp, i64, vp, i64, dbl, vp, i64], C.c_int),
     "tci_schur_update_d": ([vp, vp, i64, i64, i64, vp, i64, vp, i64, i64], C.c_int),
+    "tci_cache_create": ([vp, i32p, i32, i64, C.POINTER(vp)], C.c_int),
+    "tci_cache_destroy": ([vp], C.c_int),
+    "tci_cache_clear": ([vp], C.c_int),
+    "tci_cache_size": ([vp, pi64], C.c_int),
+    "tci_cache_dump_h": ([vp, vp, vp, i64, pi64], C.c_int),
+    "tci_cache_batcheval_d": ([vp, vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl, pi64], C.c_int),
+    "tci_cache_batcheval_h": ([vp, vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl, pi64], C.c_int),
     "tci_comm_unique_id": ([vp, pi64], C.c_int),
     "tci_comm_create": ([vp, C.c_int, C.c_int, vp, C.POINTER(vp)], C.c_int),
     "tci_comm_destroy": ([vp], C.c_int),

@@ -9,14 +9,72 @@ Batch evaluation (:255-302) looks every point up and evaluates only the misses: 
 device batch call when f is a device evaluator (GPUBatchEvaluator / ComplexScaledEvaluator:
 f.points), else by calling f point by point like the reference. As a TCI2 evaluator it supplies
 Pi through pi(); the rrLU and factors then run on the device (tci_luci_h / tci_luci_c128_h).
+
+Device memo: when f is a real device integrand (GPUBatchEvaluator) and the
+keys fit 62 bits, the memo itself lives in HBM (tci_cache_*, tci_cache.hip): a Pi block is served
+by one probe pass (hits straight into Pi), the batch's distinct misses evaluated in one batch
+evaluation of f and inserted -- no host dictionary, no per-point traffic.
 """
+import ctypes as C
 import math
 
 import numpy as np
 
 
+class _DeviceMemo:
+    """tci_cache over a context (owned by it: released before the context)."""
+
+    def __init__(self, ctx, localdims):
+        from . import _lib
+
+        self.ctx, self._lib = ctx, _lib
+        h = C.c_void_p()
+        ld = np.ascontiguousarray(localdims, np.int32)
+        ctx.check(ctx.lib.tci_cache_create(ctx.h, ld, len(ld), 4096, C.byref(h)))
+        self.h = h
+        ctx.own(self)
+
+    def release(self):
+        if getattr(self, "h", None) and self.ctx.alive:
+            self.ctx.lib.tci_cache_destroy(self.h)
+        self.h = None
+
+    def size(self):
+        n = C.c_int64()
+        self.ctx.check(self.ctx.lib.tci_cache_size(self.h, C.byref(n)))
+        return n.value
+
+    def clear(self):
+        self.ctx.check(self.ctx.lib.tci_cache_clear(self.h))
+
+    def dump(self):
+        n = C.c_int64()
+        self.ctx.check(self.ctx.lib.tci_cache_dump_h(self.h, None, None, 0, C.byref(n)))
+        keys = np.zeros(max(n.value, 1), np.int64)
+        vals = np.zeros(max(n.value, 1))
+        self.ctx.check(self.ctx.lib.tci_cache_dump_h(self.h, self._lib.ptr(keys), self._lib.ptr(vals), n.value,
+                                                     C.byref(n)))
+        return keys[: n.value], vals[: n.value]
+
+    def pi(self, f, I, J, M):
+        """(Pi as a Fortran (|I| D) x |J| array, max|Pi|, number of misses evaluated)."""
+        ctx, _lib = self.ctx, self._lib
+        I = np.ascontiguousarray(I, np.int32)
+        J = np.ascontiguousarray(J, np.int32)
+        m, nl = I.shape
+        n, nr = J.shape
+        D = f.localdims[nl] if M == 1 else 1
+        out = np.zeros((m * D, n), order="F")
+        mx, nm = C.c_double(), C.c_int64()
+        ctx.check(ctx.lib.tci_cache_batcheval_h(ctx.h, self.h, f.h, _lib.ptr(I), m, nl, _lib.ptr(J), n, nr, M,
+                                                out.ctypes.data_as(C.c_void_p), max(m * D, 1), C.byref(mx),
+                                                C.byref(nm)))
+        return out, mx.value, nm.value
+
+
 class CachedFunction:
-    def __init__(self, f, localdims, valuetype=float):
+    def __init__(self, f, localdims, valuetype=float, device_memo=None):
+        """device_memo: None = on when f is a real device integrand and the keys fit 62 bits."""
         self.f = f
         self.localdims = [int(d) for d in localdims]
         self.L = len(self.localdims)
@@ -32,6 +90,12 @@ class CachedFunction:
         self.keytype = ("UInt32" if log2space < 31 else "UInt64" if log2space < 63 else
                         "UInt128" if log2space < 127 else "UInt256+")
         self.ctx = getattr(f, "ctx", None)
+        self.nmiss_last = 0
+        capable = (hasattr(f, "h") and not getattr(f, "is_complex", False) and self.valuetype is float
+                   and log2space < 62.5)
+        if device_memo and not capable:
+            raise ValueError("device_memo needs a real device integrand and keys below 2^62")
+        self._memo = _DeviceMemo(f.ctx, self.localdims) if (capable and device_memo is not False) else None
 
     # -- reference API
     def key(self, x):
@@ -43,12 +107,19 @@ class CachedFunction:
         return sum((v - 1) * c for v, c in zip(x, self.coeffs))
 
     def haskey(self, x):
+        if self._memo is not None:
+            return self.key(x) in set(int(k) for k in self._memo.dump()[0])
         return self.key(x) in self.cache
 
     def cacheddata(self):
         """cacheddata(cf) (:160-170): index set -> value."""
         out = {}
-        for k, v in self.cache.items():
+        if self._memo is not None:
+            keys, vals = self._memo.dump()
+            items = zip((int(k) for k in keys), (float(v) for v in vals))
+        else:
+            items = self.cache.items()
+        for k, v in items:
             x = []
             for d in self.localdims:
                 x.append(k % d + 1)
@@ -57,15 +128,19 @@ class CachedFunction:
         return out
 
     def ncacheddata(self):
-        return len(self.cache)
+        return self._memo.size() if self._memo is not None else len(self.cache)
 
     def clearcache(self):
         """clearcache!(cf) (:305-308)."""
+        if self._memo is not None:
+            self._memo.clear()
         self.cache.clear()
 
     def __call__(self, x, Jset=None, M=None):
         if Jset is not None:
             return self.batch(x, Jset, M)
+        if self._memo is not None:
+            return float(self.points(np.asarray([x]))[0])
         k = self.key(x)
         if k not in self.cache:
             self.cache[k] = self._eval(np.asarray([x], np.int64))[0]
@@ -81,6 +156,9 @@ class CachedFunction:
 
     def points(self, X):
         X = np.asarray(X, np.int64).reshape(-1, self.L)
+        if self._memo is not None:
+            out, _, self.nmiss_last = self._memo.pi(self.f, np.zeros((1, 0), np.int32), X.astype(np.int32), 0)
+            return out[0, :].copy()
         if self.keytype in ("UInt32", "UInt64"):
             keys = ((X - 1) * np.asarray(self.coeffs, np.int64)).sum(1)
         else:  # beyond int64: exact Python integers
@@ -106,6 +184,9 @@ class CachedFunction:
         m, nl = I.shape
         n, nr = J.shape
         D = self.localdims[nl] if M == 1 else 1
+        if self._memo is not None and m * D * n > 0:
+            out, mx, self.nmiss_last = self._memo.pi(self.f, I, J, M)
+            return out, mx
         if m * D * n == 0:
             dt = np.complex128 if self.valuetype is complex else np.float64
             return np.zeros((m * D, n), dt), 0.0
