@@ -59,6 +59,7 @@ typedef struct tci_ctx tci_ctx;
 typedef struct tci_func tci_func;
 typedef struct tci_comm tci_comm;
 typedef struct tci_cache tci_cache;
+typedef struct tci_tci2 tci_tci2;
 /* Host-side exchange hook of the column-sharded rrLU: all-gather `count` doubles per rank from
  * d_send into d_recv (rank-major; device pointers of the calling context). Returns 0 on success.
  * Used when no RCCL communicator is passed (e.g. ranks sharing one GPU, or a Julia Distributed
@@ -214,6 +215,29 @@ int tci_update_pivots_c128_h(tci_ctx* ctx, const tci_func* f, double cre, double
                              int leftorth, int want_factors, int64_t* rowidx, int64_t* colidx,
                              double* pivoterrors, int64_t* npivot, double* maxabs, double* left,
                              double* right);
+
+/* ------------------------------------------------------ native sweep driver
+ * The per-bond loop of sweep2site! (tensorci2.jl:1195-1258) behind one call: kronecker products
+ * (:512-529), Julia's first-seen union with the previous sweep's sets unless strictly nested
+ * (:1214-1216), the 2-site update of every bond (tci_update_pivots_h, no factors: fillsitetensors!
+ * rebuilds them), updatemaxsample! and updateerrors! (:636-638, :281-289). The TCI2 state
+ * (Isets, Jsets, the last sweep's sets, maxsamplevalue, bond and pivot errors) lives in a
+ * tci_tci2 the host fills and reads back. Sets: which = 0 Iset[p] (width p), 1 Jset[p] (width
+ * L-1-p), 2 / 3 the history's; entries row-major, 1-based. sweepstrategy: 0 backandforth,
+ * 1 forward, 2 backward. */
+int tci_tci2_create(tci_ctx* ctx, int32_t L, const int32_t* localdims, tci_tci2** out);
+int tci_tci2_destroy(tci_tci2* tci);
+int tci_tci2_set_set(tci_tci2* tci, int which, int32_t p, const int32_t* entries, int64_t count);
+int tci_tci2_get_set(tci_tci2* tci, int which, int32_t p, int32_t* entries, int64_t capacity,
+                     int64_t* count);
+int tci_tci2_clear_history(tci_tci2* tci);
+int tci_tci2_set_errors(tci_tci2* tci, double maxsample, const double* bonderrors,
+                        const double* pivoterrors, int64_t npivoterrors);
+int tci_tci2_errors(tci_tci2* tci, double* maxsample, double* bonderrors, double* pivoterrors,
+                    int64_t capacity, int64_t* npivoterrors);
+int tci_tci2_sweep2site(tci_tci2* tci, const tci_func* f, int32_t niter, int32_t iter1,
+                        double abstol, int64_t maxbonddim, int32_t sweepstrategy,
+                        int32_t strictlynested);
 
 /* ---------------------------------------------------- site-tensor solve
  * Replaces setsitetensor!(tci, f, b) (tensorci2.jl:599-629): Pi1 = f(Iset_b x d x Jset_b),

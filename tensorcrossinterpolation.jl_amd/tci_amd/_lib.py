@@ -90,6 +90,14 @@ SIGNATURES = {
     "tci_sitetensor_solve_d": ([vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_dgemm_d": ([vp, C.c_int, i64, i64, i64, dbl, vp, i64, vp, i64, dbl, vp, i64], C.c_int),
     "tci_schur_update_d": ([vp, vp, i64, i64, i64, vp, i64, vp, i64, i64], C.c_int),
+    "tci_tci2_create": ([vp, i32, i32p, C.POINTER(vp)], C.c_int),
+    "tci_tci2_destroy": ([vp], C.c_int),
+    "tci_tci2_set_set": ([vp, C.c_int, i32, vp, i64], C.c_int),
+    "tci_tci2_get_set": ([vp, C.c_int, i32, vp, i64, pi64], C.c_int),
+    "tci_tci2_clear_history": ([vp], C.c_int),
+    "tci_tci2_set_errors": ([vp, dbl, vp, vp, i64], C.c_int),
+    "tci_tci2_errors": ([vp, pdbl, vp, vp, i64, pi64], C.c_int),
+    "tci_tci2_sweep2site": ([vp, vp, i32, i32, dbl, i64, i32, i32], C.c_int),
     "tci_cache_create": ([vp, i32p, i32, i64, C.POINTER(vp)], C.c_int),
     "tci_cache_destroy": ([vp], C.c_int),
     "tci_cache_clear": ([vp], C.c_int),

@@ -308,12 +308,17 @@ class TensorCI2:
 
     def sweep2site(self, f, niter, iter1=1, abstol=1e-8, maxbonddim=INT64_MAX, sweepstrategy="backandforth",
                    pivotsearch="full", verbosity=0, strictlynested=False, fillsitetensors=True,
-                   lazy_sitetensors=False):
-        """sweep2site! (tensorci2.jl:1195-1258)."""
+                   lazy_sitetensors=False, native=None):
+        """sweep2site! (tensorci2.jl:1195-1258). For a real device integrand the per-bond loop runs
+        in C++ (tci_tci2_sweep2site, one ABI call per sweep; native=False forces this loop)."""
         if pivotsearch != "full":
             raise NotImplementedError("only pivotsearch=:full is implemented (the :rook search is random)")
         self.invalidatesitetensors()
         n = len(self)
+        if native is not False and NATIVE_SWEEP and _native_ok(f) and fillsitetensors:
+            self._sweep2site_native(f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested)
+            self.fillsitetensors(f, solve=not lazy_sitetensors)
+            return
         for it in range(iter1, iter1 + niter):
             extraI = [None] * n
             extraJ = [None] * n
@@ -335,6 +340,60 @@ class TensorCI2:
                                       extraIset=extraI[b], extraJset=extraJ[b - 1], compute_factors=cf)
         if fillsitetensors:
             self.fillsitetensors(f, solve=not lazy_sitetensors)
+
+    def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested):
+        ctx = f.ctx
+        lib = ctx.lib
+        n = len(self)
+        h = getattr(self, "_native_h", None)
+        if h is None or getattr(self, "_native_ctx", None) is not ctx:
+            h = C.c_void_p()
+            ctx.check(lib.tci_tci2_create(ctx.h, n, np.ascontiguousarray(self.localdims, np.int32), C.byref(h)))
+            self._native_h, self._native_ctx = h, ctx
+            self._native_owner = ctx.own(_NativeTCI2(ctx, h))
+
+        def push(which, p, a):
+            a = np.ascontiguousarray(a, np.int32)
+            ctx.check(lib.tci_tci2_set_set(h, which, p, a.ctypes.data_as(C.c_void_p), len(a)))
+
+        for p in range(n):
+            push(0, p, self.Iset[p])
+            push(1, p, self.Jset[p])
+        if self.Iset_history:
+            for p in range(n):
+                push(2, p, self.Iset_history[-1][p])
+                push(3, p, self.Jset_history[-1][p])
+        else:
+            ctx.check(lib.tci_tci2_clear_history(h))
+        pe = np.ascontiguousarray(self.pivoterrors, np.float64)
+        ctx.check(lib.tci_tci2_set_errors(h, float(self.maxsamplevalue),
+                                          np.ascontiguousarray(self.bonderrors, np.float64).ctypes.data_as(C.c_void_p),
+                                          pe.ctypes.data_as(C.c_void_p), len(pe)))
+        strat = {"backandforth": 0, "forward": 1, "backward": 2}[sweepstrategy]
+        ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol), int(min(maxbonddim, INT64_MAX)),
+                                          strat, int(bool(strictlynested))))
+
+        def pull(which, p, w):
+            cnt = C.c_int64()
+            ctx.check(lib.tci_tci2_get_set(h, which, p, None, 0, C.byref(cnt)))
+            a = np.zeros((cnt.value, w), np.int32)
+            if w and cnt.value:
+                ctx.check(lib.tci_tci2_get_set(h, which, p, a.ctypes.data_as(C.c_void_p), cnt.value, C.byref(cnt)))
+            return a
+
+        self.Iset = [pull(0, p, p) for p in range(n)]
+        self.Jset = [pull(1, p, n - 1 - p) for p in range(n)]
+        self.Iset_history = [[pull(2, p, p) for p in range(n)]]
+        self.Jset_history = [[pull(3, p, n - 1 - p) for p in range(n)]]
+        ms, npe = C.c_double(), C.c_int64()
+        be = np.zeros(n - 1)
+        ctx.check(lib.tci_tci2_errors(h, C.byref(ms), be.ctypes.data_as(C.c_void_p), None, 0, C.byref(npe)))
+        pe = np.zeros(max(npe.value, 1))
+        ctx.check(lib.tci_tci2_errors(h, C.byref(ms), be.ctypes.data_as(C.c_void_p), pe.ctypes.data_as(C.c_void_p),
+                                      npe.value, C.byref(npe)))
+        self.maxsamplevalue = ms.value
+        self.bonderrors = be
+        self.pivoterrors = pe[: npe.value].copy()
 
     def optimize(self, f, tolerance=None, pivottolerance=None, maxbonddim=INT64_MAX, maxiter=20,
                  sweepstrategy="backandforth", pivotsearch="full", verbosity=0, loginterval=10,
@@ -451,6 +510,30 @@ def reconstractglobalpivotsfromijset(localdims, Isets, Jsets):
 
 
 # --------------------------------------------------------------- device calls
+def _native_ok(f):
+    """The native sweep driver takes a real device integrand (a GPUBatchEvaluator's tci_func)."""
+    return (hasattr(f, "h") and getattr(f, "ctx", None) is not None and not getattr(f, "is_complex", False)
+            and not getattr(f, "shard_rrlu", False) and type(f).__name__ == "GPUBatchEvaluator")
+
+
+class _NativeTCI2:
+    """Owner of a tci_tci2 handle (released before its context)."""
+
+    def __init__(self, ctx, h):
+        self.ctx, self.h = ctx, h
+
+    def release(self):
+        if self.h and self.ctx.alive:
+            self.ctx.lib.tci_tci2_destroy(self.h)  # host memory only: no HIP call
+        self.h = None
+
+    __del__ = release
+
+
+# the native per-bond loop for device integrands (set False to run sweep2site's Python loop)
+NATIVE_SWEEP = True
+
+
 def _ctx_of(f):
     ctx = getattr(f, "ctx", None) or getattr(getattr(f, "local", None), "ctx", None)
     return ctx or _lib.context()
