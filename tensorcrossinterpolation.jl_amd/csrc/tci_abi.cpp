@@ -48,6 +48,7 @@ struct tci_ctx {
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
+    int c128_nb = 6;             // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1)
     int ncu = 0;           // compute units of the device
     double* colbuf = nullptr;  // mid path: published candidate columns
     size_t capColbuf = 0;
@@ -728,6 +729,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
+    if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
     if (const char* e = getenv("TCI_DENSE_MFMA")) c->dense = std::max(0, std::min(atoi(e), (int)tci::kDenseAll));
     {
         hipDeviceProp_t prop;
@@ -1013,7 +1015,12 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t oSt = 0, oCand = al(sizeof(tci::CState)), oCol = oCand + al(sizeof(tci::CCand) * G);
     const size_t oRow = oCol + al(16 * (size_t)std::max(mi, 1));
-    const size_t bytes = oRow + al(16 * (size_t)std::max(ni, 1));
+    // deferred updates: pending slots X (kMaxPend x ldx), Y (kMaxPend x ldy), stash
+    const int64_t ldx = round_up(std::max<int64_t>(m, 1), 16), ldy = round_up(std::max<int64_t>(n, 1), 16);
+    const size_t oX = oRow + al(16 * (size_t)std::max(ni, 1));
+    const size_t oY = oX + al(16 * (size_t)(tci::kMaxPend * ldx));
+    const size_t oS = oY + al(16 * (size_t)(tci::kMaxPend * ldy));
+    const size_t bytes = oS + al(16 * 4 * tci::kMaxPend);
     int st;
     if ((st = ensure(c, &c->cws, &c->capCws, bytes))) return st;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
@@ -1036,11 +1043,31 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     g.rowbuf = reinterpret_cast<double2*>(c->cws + oRow);
     g.rowperm = c->rowperm;
     g.colperm = c->colperm;
-    // one step per pivot; steps after the stop test fired return at once (st->done)
-    for (int t = 0; mr > 0 && t <= mr; ++t) {
-        g.t = t;
-        tci::launch_crrlu_step(c->stream, g);
-        HIPCHK(c, hipGetLastError());
+    g.X = reinterpret_cast<double2*>(c->cws + oX);
+    g.ldx = ldx;
+    g.Y = reinterpret_cast<double2*>(c->cws + oY);
+    g.ldy = ldy;
+    g.stash = reinterpret_cast<double2*>(c->cws + oS);
+    if (c->c128_nb > 0) {
+        // deferred updates (K8): pending pivots t0 .. t-1 applied on the fly, written back when
+        // nb of them pend; steps after the stop test fired return at once (st->done)
+        const int nb = std::min(c->c128_nb, tci::kMaxPend - 1);
+        int t0 = 0;
+        for (int t = 0; mr > 0 && t < mr; ++t) {
+            g.t = t;
+            const int P = t - t0;
+            const bool flush = P >= nb;
+            tci::launch_crrlu_step_d(c->stream, g, P, flush);
+            if (flush) t0 = t;
+            HIPCHK(c, hipGetLastError());
+        }
+    } else {
+        // round 1: one read + write of the trailing block per pivot (A/B switch TCI_C128_NB=0)
+        for (int t = 0; mr > 0 && t <= mr; ++t) {
+            g.t = t;
+            tci::launch_crrlu_step(c->stream, g);
+            HIPCHK(c, hipGetLastError());
+        }
     }
     tci::CState hs;
     HIPCHK(c, hipMemcpyAsync(&hs, dst, sizeof hs, hipMemcpyDeviceToHost, c->stream));

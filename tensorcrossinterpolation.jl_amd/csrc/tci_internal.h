@@ -135,8 +135,20 @@ struct CStepArgs {
     double2* rowbuf;
     int64_t* rowperm;
     int64_t* colperm;
+    // deferred updates (k_crrlu_*_d): pending slots X[s * ldx + row], Y[s * ldy + col] (s < P),
+    // P = pending count seen by reduce / swap, stash: 4 x kMaxPend entries of the swapped rows /
+    // columns' slots, read by the swap kernel while its corner thread rewrites them
+    double2* X;
+    int64_t ldx;
+    double2* Y;
+    int64_t ldy;
+    int P;
+    double2* stash;
 };
 int crrlu_grid(int m, int n, int t);
+// the deferred-update pipeline: step<P, flush> (pending applied on the fly, written back when
+// flush), then reduce + swap with the pending count P' (0 after a flush) of the step
+void launch_crrlu_step_d(hipStream_t s, CStepArgs g, int P, bool flush);
 void launch_crrlu_init(hipStream_t s, CState* st, int64_t* rowperm, int64_t* colperm, int m, int n);
 void launch_crrlu_step(hipStream_t s, CStepArgs g);
 void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, int n, int np,

@@ -545,6 +545,222 @@ __global__ __launch_bounds__(256) void k_ctt_eval(const double2* __restrict__ co
     if (threadIdx.x == 0) out[pt] = v[cur][0];
 }
 
+
+// ------------------------------------------------ deferred updates
+// The trailing block stays stale in HBM between write-backs; up to nb rank-1 updates pend as
+// per-row x_s (X[s][i]) and per-column y_s (Y[s][j]) and are applied on the fly, in pivot order
+// and with the reference's rounding (complex multiply, then componentwise subtract), so every
+// value is bitwise the reference's. Swaps stay physical: the swap kernel moves the pending
+// entries of the two rows / columns with them. It also finalises pivot t's column and row
+// (stale values minus the pending updates, normalised) into A -- the L / U storage of the
+// reference -- and into pending slot P.
+template <int P, bool FLUSH>
+__global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
+    __shared__ double2 ys[(P > 0 ? P : 1) * kCTC];
+    __shared__ CCand red[kCThreads / 64];
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t;
+    const int tiles_r = g.tiles_r;
+    const int tr = blockIdx.x % tiles_r, tc = blockIdx.x / tiles_r;
+    const int r0 = t + tr * kCTR, c0 = t + tc * kCTC;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double2* A = g.A;
+    const int64_t ld = g.ld;
+    const int i = r0 + lane;
+    double2 xr[P > 0 ? P : 1];
+    if constexpr (P > 0) {
+        for (int e = threadIdx.x; e < P * kCTC; e += kCThreads) {
+            const int s = e / kCTC, jl = e % kCTC, j = c0 + jl;
+            ys[e] = j < g.n ? g.Y[(int64_t)s * g.ldy + j] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int s = 0; s < P; ++s) xr[s] = i < g.m ? g.X[(int64_t)s * g.ldx + i] : make_double2(0.0, 0.0);
+        __syncthreads();
+    }
+    CCand best{-INFINITY, INT32_MAX, INT32_MAX};
+    if (i < g.m) {
+#pragma unroll
+        for (int cc = 0; cc < kCW; ++cc) {
+            const int jl = w * kCW + cc;
+            const int j = c0 + jl;
+            if (j >= g.n) break;
+            double2* pa = A + i + (int64_t)j * ld;
+            double2 a = *pa;
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(xr[s], ys[s * kCTC + jl]);
+                a.x = a.x - z.x;
+                a.y = a.y - z.y;
+            }
+            if constexpr (FLUSH) *pa = a;
+            const double v = a.x * a.x + a.y * a.y;
+            if (v > best.v) best = CCand{v, j, i};  // columns ascend: strict '>' keeps the first
+        }
+    }
+    best = block_reduce<kCThreads>(best, red);
+    if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
+}
+
+// value of stale element (r, c) with the P pending updates applied, in pivot order
+__device__ inline double2 cpend(double2 a, const double2* X, int64_t ldx, int r, const double2* Y,
+                                int64_t ldy, int c, int P) {
+    for (int s = 0; s < P; ++s) {
+        const double2 z = cmul(X[(int64_t)s * ldx + r], Y[(int64_t)s * ldy + c]);
+        a.x = a.x - z.x;
+        a.y = a.y - z.y;
+    }
+    return a;
+}
+
+__global__ __launch_bounds__(kRThreads) void k_crrlu_reduce_d(CStepArgs g, int ncand) {
+    __shared__ CCand red[kRThreads / 64];
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t, P = g.P;
+    CCand c{-INFINITY, INT32_MAX, INT32_MAX};
+    int b = threadIdx.x;
+    for (; b + 7 * kRThreads < ncand; b += 8 * kRThreads) {
+        CCand o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = g.cand[b + u * kRThreads];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (cbetter(o[u], c)) c = o[u];
+    }
+    for (; b < ncand; b += kRThreads) {
+        const CCand o = g.cand[b];
+        if (cbetter(o, c)) c = o;
+    }
+    c = block_reduce<kRThreads>(c, red);
+    const int p = c.col == INT32_MAX ? t : c.row;  // nothing beat -Inf (all NaN): (k, k)
+    const int q = c.col == INT32_MAX ? t : c.col;
+    // the slots of the rows / columns the swap exchanges, for the swap kernel (see CStepArgs)
+    if (threadIdx.x < P) {
+        const int s = threadIdx.x;
+        g.stash[s] = g.X[(int64_t)s * g.ldx + t];
+        g.stash[kMaxPend + s] = g.X[(int64_t)s * g.ldx + p];
+        g.stash[2 * kMaxPend + s] = g.Y[(int64_t)s * g.ldy + t];
+        g.stash[3 * kMaxPend + s] = g.Y[(int64_t)s * g.ldy + q];
+    }
+    if (threadIdx.x == 0) {
+        const double2 a = cpend(g.A[p + (int64_t)q * g.ld], g.X, g.ldx, p, g.Y, g.ldy, q, P);
+        const double err = jl_hypot(a.x, a.y);  // lu.error = abs(A[p, q])
+        st->err = err;
+        if ((err < g.reltol * st->maxerror || err < g.abstol) && t > 0) {
+            st->done = 1;
+        } else {
+            st->maxerror = jl_maxd(st->maxerror, err);
+            st->np = t + 1;
+            st->p = p;
+            st->q = q;
+            st->piv = a;
+            int64_t tmp = g.rowperm[t]; g.rowperm[t] = g.rowperm[p]; g.rowperm[p] = tmp;
+            tmp = g.colperm[t]; g.colperm[t] = g.colperm[q]; g.colperm[q] = tmp;
+        }
+    }
+}
+
+// swaprow!(t, p), swapcol!(t, q) of the stale matrix and of the pending slots; pivot t's row
+// (columns > t) and column (rows > t) finalised: pending updates applied, normalised by the
+// pivot (matrixlu.jl:302-308), stored into A and into slot P. Threads: one per column (row swap),
+// per row (column swap), one for the 2 x 2 corner {t, p} x {t, q}.
+__global__ void k_crrlu_swap_d(CStepArgs g) {
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t, p = st->p, q = st->q, P = g.P;
+    const double2 piv = st->piv;
+    double2* A = g.A;
+    const int64_t ld = g.ld;
+    const double2* sXt = g.stash;                 // X[s][t] before the swap
+    const double2* sXp = g.stash + kMaxPend;      // X[s][p]
+    const double2* sYt = g.stash + 2 * kMaxPend;  // Y[s][t]
+    const double2* sYq = g.stash + 3 * kMaxPend;  // Y[s][q]
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < g.n) {  // column j: rows t <-> p
+        const int j = e;
+        if (j == t || j == q) return;
+        double2* pt = A + t + (int64_t)j * ld;
+        double2* pp = A + p + (int64_t)j * ld;
+        const double2 at = *pt, ap = *pp;
+        *pp = at;
+        if (j < t) {
+            *pt = ap;  // the L part: final values
+        } else {  // U row t: the new row t is old row p, pending updates with old row p's x's
+            double2 y = ap;
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(sXp[s], g.Y[(int64_t)s * g.ldy + j]);
+                y.x = y.x - z.x;
+                y.y = y.y - z.y;
+            }
+            if (!g.leftorth) y = jl_cdiv(y, piv);  // A[k, k+1:end] ./= A[k, k]
+            *pt = y;
+            g.Y[(int64_t)P * g.ldy + j] = y;
+        }
+    } else if (e < g.n + g.m) {  // row r: columns t <-> q
+        const int r = e - g.n;
+        if (r == t || r == p) return;
+        double2* pt = A + r + (int64_t)t * ld;
+        double2* pq = A + r + (int64_t)q * ld;
+        const double2 at = *pt, aq = *pq;
+        *pq = at;
+        if (r < t) {
+            *pt = aq;  // the U part
+        } else {
+            double2 x = aq;
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(g.X[(int64_t)s * g.ldx + r], sYq[s]);
+                x.x = x.x - z.x;
+                x.y = x.y - z.y;
+            }
+            if (g.leftorth) x = jl_cdiv(x, piv);  // A[k+1:end, k] ./= A[k, k]
+            *pt = x;
+            g.X[(int64_t)P * g.ldx + r] = x;
+        }
+    } else if (e == g.n + g.m) {
+        // new[a, b] = old[sr(a), sc(b)] on {t, p} x {t, q}, all read before any store
+        const double2 o_tt = A[t + (int64_t)t * ld], o_tq = A[t + (int64_t)q * ld];
+        const double2 o_pt = A[p + (int64_t)t * ld];
+        A[t + (int64_t)t * ld] = piv;  // (t, t): the pivot, updated (reduce computed it)
+        if (q != t) {  // (t, q): row t = old row p, column q = old column t -> U element
+            double2 y = o_pt;
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(sXp[s], sYt[s]);
+                y.x = y.x - z.x;
+                y.y = y.y - z.y;
+            }
+            if (!g.leftorth) y = jl_cdiv(y, piv);
+            A[t + (int64_t)q * ld] = y;
+            g.Y[(int64_t)P * g.ldy + q] = y;
+        }
+        if (p != t) {  // (p, t): row p = old row t, column t = old column q -> L element
+            double2 x = o_tq;
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(sXt[s], sYq[s]);
+                x.x = x.x - z.x;
+                x.y = x.y - z.y;
+            }
+            if (g.leftorth) x = jl_cdiv(x, piv);
+            A[p + (int64_t)t * ld] = x;
+            g.X[(int64_t)P * g.ldx + p] = x;
+        }
+        if (p != t && q != t) A[p + (int64_t)q * ld] = o_tt;  // (p, q): trailing, stays stale
+        // the pending slots follow their rows / columns
+        for (int s = 0; s < P; ++s) {
+            g.X[(int64_t)s * g.ldx + t] = sXp[s];
+            g.X[(int64_t)s * g.ldx + p] = sXt[s];
+            g.Y[(int64_t)s * g.ldy + t] = sYq[s];
+            g.Y[(int64_t)s * g.ldy + q] = sYt[s];
+        }
+    }
+}
+
+template <int P>
+static void crrlu_step_p(hipStream_t s, const CStepArgs& g, bool flush, int grid) {
+    if (flush) hipLaunchKernelGGL((k_crrlu_step_d<P, true>), dim3(grid), dim3(kCThreads), 0, s, g);
+    else hipLaunchKernelGGL((k_crrlu_step_d<P, false>), dim3(grid), dim3(kCThreads), 0, s, g);
+}
+
 }  // namespace
 
 int crrlu_grid(int m, int n, int t) {
@@ -567,6 +783,24 @@ void launch_crrlu_step(hipStream_t s, CStepArgs g) {
         k_crrlu_reduce<<<1, kRThreads, 0, s>>>(g, grid);
         k_crrlu_swap<<<(g.m + g.n + 256) / 256, 256, 0, s>>>(g);
     }
+}
+
+// step<P, flush> for pivot t, then (t < mr) reduce + swap with the step's pending count after it
+void launch_crrlu_step_d(hipStream_t s, CStepArgs g, int P, bool flush) {
+    g.tiles_r = g.m - g.t > 0 ? (g.m - g.t + kCTR - 1) / kCTR : 1;
+    const int grid = crrlu_grid(g.m, g.n, g.t);
+    switch (P) {
+#define TCI_CSTEP(p) \
+    case p: crrlu_step_p<p>(s, g, flush, grid); break;
+        TCI_CSTEP(0) TCI_CSTEP(1) TCI_CSTEP(2) TCI_CSTEP(3) TCI_CSTEP(4) TCI_CSTEP(5) TCI_CSTEP(6)
+        TCI_CSTEP(7) TCI_CSTEP(8) TCI_CSTEP(9) TCI_CSTEP(10) TCI_CSTEP(11) TCI_CSTEP(12) TCI_CSTEP(13)
+        TCI_CSTEP(14) TCI_CSTEP(15)
+#undef TCI_CSTEP
+    default: break;
+    }
+    g.P = flush ? 0 : P;
+    hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, grid);
+    hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
 }
 
 void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, int n, int np,
