@@ -34,7 +34,7 @@
 #define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
 #endif
 #ifndef TCI_PASS_SH_U
-#define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (4 rows x 16-B fp32 loads per column)
+#define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (kShRL rows of fp32 loaded per column)
 #endif
 #ifndef TCI_FLUSH_NT
 #define TCI_FLUSH_NT 1  // write-back pass: fp64 stores non-temporal (the next pass reads the shadow, not them)
@@ -340,8 +340,15 @@ constexpr int kP2Slices = kRowsPerTile / 128;              // 128-row slices of 
 constexpr int kP2Reps = kP2Threads / 64 / kP2Slices;        // waves per slice
 constexpr int kP2StageCols = 512;                           // columns staged at once
 static_assert(kP2StageCols <= kP2Threads, "one staged column per thread");
-constexpr int kShSlices = kRowsPerTile / 256;               // shadow search: 256-row slices
+#ifndef TCI_SH_RL
+#define TCI_SH_RL 4  // shadow search: rows per lane (4: 16-B fp32 loads, 4P registers of x's; 2: 8-B, 2P)
+#endif
+constexpr int kShRL = TCI_SH_RL;
+static_assert(kShRL == 2 || kShRL == 4, "rows per lane");
+constexpr int kShSliceRows = 64 * kShRL;                    // shadow search: rows per slice
+constexpr int kShSlices = kRowsPerTile / kShSliceRows;
 constexpr int kShReps = kP2Threads / 64 / kShSlices;        // waves per slice
+static_assert(kShSlices <= kP2Slices, "one LDS chunk counter per slice");
 
 // Kernel view of PassArgs.
 struct PassK {
@@ -640,9 +647,11 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
     const int G = kP2StageCols / cb;
-    // four rows per lane: 16-B fp32 loads (lda, ldx and lds are multiples of 4, r0 too, so the
-    // four rows of a lane with r0 < m are inside the column)
-    const int r0 = tr * kRowsPerTile + slice * 256 + 4 * lane;
+    // kShRL rows per lane: 8-B (16-B) fp32 loads (lda, ldx and lds are multiples of 4, r0 of kShRL,
+    // so the rows of a lane with r0 < m are inside the column)
+    constexpr int RL = kShRL, RH = RL / 2;
+    typedef float fvec __attribute__((ext_vector_type(RL)));
+    const int r0 = tr * kRowsPerTile + slice * kShSliceRows + RL * lane;
     const int rb = r0 < m ? r0 : 0;
     const float* const sbase = g.S + rb;
     const int cbs = __builtin_ctz(cb);  // cb is 8 or 16
@@ -650,11 +659,11 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
         const int it = g0 + ((h * U) >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + ((h * U) & (cb - 1));
     };
-    auto load_chunk = [&](int g0, int h, float4 (&v)[U]) {
+    auto load_chunk = [&](int g0, int h, fvec (&v)[U]) {
         const int j = chunk_col(g0, h);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            v[u] = *reinterpret_cast<const float4*>(sbase + (int64_t)min(j + u, n - 1) * lds);
+            v[u] = *reinterpret_cast<const fvec*>(sbase + (int64_t)min(j + u, n - 1) * lds);
     };
     auto stage_col = [&](int g0) -> int {
         const int gn = min(G, ntc - g0);
@@ -663,13 +672,13 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
         const int it = g0 + (lc >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
     };
-    int rp[4];
+    int rp[RL];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) rp[t] = r0 + t < m ? sel.rowpos[r0 + t] : -1;
-    const int lrow = slice * 256 + 4 * lane;  // the lane's first row within the tile
+    for (int t = 0; t < RL; ++t) rp[t] = r0 + t < m ? sel.rowpos[r0 + t] : -1;
+    const int lrow = slice * kShSliceRows + RL * lane;  // the lane's first row within the tile
     int jst = ntc > 0 ? stage_col(0) : -1;
     int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
-    float4 va[U], vb[U];
+    fvec va[U], vb[U];
     const int nch0 = ntc > 0 ? min(G, ntc) * cb / U : 0;
     if (rep < nch0) load_chunk(0, rep, va);
     if (rep + kShReps < nch0) load_chunk(0, rep + kShReps, vb);
@@ -681,41 +690,44 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const double ypr0 = g.A[a + (int64_t)((jst >= 0 && jst < n) ? jst : 0) * lda];
     unsigned inm = 0;  // bit t: row r0 + t is in the trailing block
 #pragma unroll
-    for (int t = 0; t < 4; ++t) inm |= (rp[t] > k ? 1u : 0u) << t;
+    for (int t = 0; t < RL; ++t) inm |= (rp[t] > k ? 1u : 0u) << t;
     const bool active = inm != 0;
     // pending x's in fp32; x_k exact (fp64, kept for the exact examinations) and in fp32
     typedef float f2v __attribute__((ext_vector_type(2)));  // packed pairs: v_pk_fma_f32
-    f2v xf[P][2];  // rows (0, 1) and (2, 3) of the lane
+    f2v xf[P][RH];  // row pairs (0, 1) [, (2, 3)] of the lane
     {
-        double xk[4];
-        const double2 c0 = *reinterpret_cast<const double2*>(g.A + rb + (int64_t)b * lda);
-        const double2 c1 = *reinterpret_cast<const double2*>(g.A + rb + 2 + (int64_t)b * lda);
-        xk[0] = c0.x;
-        xk[1] = c0.y;
-        xk[2] = c1.x;
-        xk[3] = c1.y;
+        double xk[RL];
 #pragma unroll
-        for (int s = 0; s < P - 1; ++s) {
-            const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rb);
-            const double2 u1 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rb + 2);
-            const double yv = g.Y[(int64_t)s * ldy + b];
-            const double xs[4] = {u0.x, u0.y, u1.x, u1.y};
-            xf[s][0] = f2v{(float)xs[0], (float)xs[1]};
-            xf[s][1] = f2v{(float)xs[2], (float)xs[3]};
-#pragma unroll
-            for (int t = 0; t < 4; ++t) xk[t] = __dsub_rn(xk[t], __dmul_rn(xs[t], yv));
+        for (int hh = 0; hh < RH; ++hh) {
+            const double2 c0 = *reinterpret_cast<const double2*>(g.A + rb + 2 * hh + (int64_t)b * lda);
+            xk[2 * hh] = c0.x;
+            xk[2 * hh + 1] = c0.y;
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int s = 0; s < P - 1; ++s) {
+            double xs[RL];
+#pragma unroll
+            for (int hh = 0; hh < RH; ++hh) {
+                const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rb + 2 * hh);
+                xs[2 * hh] = u0.x;
+                xs[2 * hh + 1] = u0.y;
+                xf[s][hh] = f2v{(float)u0.x, (float)u0.y};
+            }
+            const double yv = g.Y[(int64_t)s * ldy + b];
+#pragma unroll
+            for (int t = 0; t < RL; ++t) xk[t] = __dsub_rn(xk[t], __dmul_rn(xs[t], yv));
+        }
+#pragma unroll
+        for (int t = 0; t < RL; ++t)
             if (g.leftorth) xk[t] = xk[t] / piv;
-        xf[P - 1][0] = f2v{(float)xk[0], (float)xk[1]};
-        xf[P - 1][1] = f2v{(float)xk[2], (float)xk[3]};
+#pragma unroll
+        for (int hh = 0; hh < RH; ++hh) xf[P - 1][hh] = f2v{(float)xk[2 * hh], (float)xk[2 * hh + 1]};
         if (rep == 0) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) L.xk[lrow + t] = xk[t];
+            for (int t = 0; t < RL; ++t) L.xk[lrow + t] = xk[t];
             if (q == 0) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < RL; ++t)
                     if (inm >> t & 1) {
                         g.X[(int64_t)(P - 1) * ldx + r0 + t] = xk[t];
                         g.Lp[r0 + t + (int64_t)k * g.ldl] = xk[t];
@@ -728,32 +740,37 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const float margin = 0x1p-20f;
     float tau = 0.0f;  // this lane's view of the workgroup's lower bound on the max |v|
     // chunk h's maximum |w| over the lane's trailing-block elements
-    auto approx = [&](int h, const float4 (&v)[U]) -> float {
-        float cm[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    auto approx = [&](int h, const fvec (&v)[U]) -> float {
+        float cm[RL];
+#pragma unroll
+        for (int t = 0; t < RL; ++t) cm[t] = 0.0f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int lc = h * U + u;
             if (L.cpos[lc] <= k) continue;  // wave-uniform
-            f2v w01 = {v[u].x, v[u].y}, w23 = {v[u].z, v[u].w};
+            f2v w[RH];
+#pragma unroll
+            for (int hh = 0; hh < RH; ++hh) w[hh] = f2v{v[u][2 * hh], v[u][2 * hh + 1]};
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 const float y = L.yf[lc * P + s];
                 const f2v yy = {y, y};
-                w01 = __builtin_elementwise_fma(-xf[s][0], yy, w01);
-                w23 = __builtin_elementwise_fma(-xf[s][1], yy, w23);
+#pragma unroll
+                for (int hh = 0; hh < RH; ++hh) w[hh] = __builtin_elementwise_fma(-xf[s][hh], yy, w[hh]);
             }
-            cm[0] = fmaxf(cm[0], fabsf(w01.x));
-            cm[1] = fmaxf(cm[1], fabsf(w01.y));
-            cm[2] = fmaxf(cm[2], fabsf(w23.x));
-            cm[3] = fmaxf(cm[3], fabsf(w23.y));
+#pragma unroll
+            for (int hh = 0; hh < RH; ++hh) {
+                cm[2 * hh] = fmaxf(cm[2 * hh], fabsf(w[hh].x));
+                cm[2 * hh + 1] = fmaxf(cm[2 * hh + 1], fabsf(w[hh].y));
+            }
         }
         float c = 0.0f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < RL; ++t)
             if (inm >> t & 1) c = fmaxf(c, cm[t]);
         return c;
     };
-    // exact examination of chunks e0 / e1 (< 0: none; the lane's four rows), as the exact pass
+    // exact examination of chunks e0 / e1 (< 0: none; the lane's rows), as the exact pass
     // does it. One call site and rolled loops: it runs for a handful of chunks per workgroup.
     auto examine = [&](int g0, int e0, int e1) {
 #pragma unroll 1
@@ -772,22 +789,26 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
                 if (cp <= k) continue;
                 const int j = j0 + u;
                 const double* pa = g.A + rbx + (int64_t)j * lda;
-                const double2 p0 = *reinterpret_cast<const double2*>(pa);
-                const double2 p1 = *reinterpret_cast<const double2*>(pa + 2);
-                double v[4] = {p0.x, p0.y, p1.x, p1.y};
+                double v[RL];
+#pragma unroll
+                for (int hh = 0; hh < RH; ++hh) {
+                    const double2 p0 = *reinterpret_cast<const double2*>(pa + 2 * hh);
+                    v[2 * hh] = p0.x;
+                    v[2 * hh + 1] = p0.y;
+                }
 #pragma unroll 1
                 for (int s = 0; s < P - 1; ++s) {
                     const double y = L.ys[lc * P + s];
-                    const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rbx);
-                    const double2 u1 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rbx + 2);
-                    v[0] = __dsub_rn(v[0], __dmul_rn(u0.x, y));
-                    v[1] = __dsub_rn(v[1], __dmul_rn(u0.y, y));
-                    v[2] = __dsub_rn(v[2], __dmul_rn(u1.x, y));
-                    v[3] = __dsub_rn(v[3], __dmul_rn(u1.y, y));
+#pragma unroll
+                    for (int hh = 0; hh < RH; ++hh) {
+                        const double2 u0 = *reinterpret_cast<const double2*>(g.X + (int64_t)s * ldx + rbx + 2 * hh);
+                        v[2 * hh] = __dsub_rn(v[2 * hh], __dmul_rn(u0.x, y));
+                        v[2 * hh + 1] = __dsub_rn(v[2 * hh + 1], __dmul_rn(u0.y, y));
+                    }
                 }
                 const double yk = L.ys[lc * P + P - 1];
 #pragma unroll 1
-                for (int t = 0; t < 4; ++t) {
+                for (int t = 0; t < RL; ++t) {
                     if (!(inm >> t & 1)) continue;
                     const double vt = __dsub_rn(v[t], __dmul_rn(L.xk[lrow + t], yk));
                     const double a2 = __dmul_rn(vt, vt);
