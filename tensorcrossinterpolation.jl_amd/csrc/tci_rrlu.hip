@@ -1762,30 +1762,42 @@ __global__ __launch_bounds__(256) void k_shard_gather(const Cand* __restrict__ l
     const Cand c = *lout;
     const bool has = c.v >= 0.0;
     const int tid = threadIdx.x;
-    if (tid == 0) {
-        send[0] = c.v;
-        send[1] = c.val;
-        send[2] = bits_dbl((uint64_t)(uint32_t)c.cpos | ((uint64_t)(uint32_t)c.rpos << 32));
-        const int32_t pcg = has ? (int32_t)(c0 + c.pcol) : -1;
-        send[3] = bits_dbl((uint64_t)(uint32_t)pcg | ((uint64_t)(uint32_t)c.prow << 32));
+    if (blockIdx.x == 0) {
+        if (tid == 0) {
+            send[0] = c.v;
+            send[1] = c.val;
+            send[2] = bits_dbl((uint64_t)(uint32_t)c.cpos | ((uint64_t)(uint32_t)c.rpos << 32));
+            const int32_t pcg = has ? (int32_t)(c0 + c.pcol) : -1;
+            send[3] = bits_dbl((uint64_t)(uint32_t)pcg | ((uint64_t)(uint32_t)c.prow << 32));
+        }
+        if (tid < kMaxPend) send[4 + tid] = has ? Y[(int64_t)tid * ldy + c.pcol] : 0.0;
     }
-    if (tid < kMaxPend) send[4 + tid] = has ? Y[(int64_t)tid * ldy + c.pcol] : 0.0;
+    // the column: every block a 1024-row slice, 4 independent loads per thread
     const double* col = A + (int64_t)(has ? c.pcol : 0) * lda;
-    for (int i = tid; i < m; i += blockDim.x) send[kShardHdr + i] = has ? col[i] : 0.0;
+    const int i0 = blockIdx.x * 1024 + tid;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < m) send[kShardHdr + i] = has ? col[i] : 0.0;
+    }
 }
 
 void launch_shard_gather(hipStream_t s, const Cand* lout, const double* A, int64_t lda, int m,
                          const double* Y, int64_t ldy, int64_t c0, double* send) {
-    hipLaunchKernelGGL(k_shard_gather, dim3(1), dim3(256), 0, s, lout, A, lda, m, Y, ldy, c0, send);
+    hipLaunchKernelGGL(k_shard_gather, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, lout, A,
+                       lda, m, Y, ldy, c0, send);
 }
 
+// Every block reduces the N records (rank order, the reference's tie order) to the same winner and
+// installs its slice of the ghost column; block 0 alone commits (stop test, maps, st). A ghost
+// installed after a stop is never read (the passes return at once).
 __global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__ recv, int nranks, int64_t rec,
                                                       int m, int k, RrluState* st, double reltol, double abstol,
                                                       int32_t* rowpos, int32_t* colpos_g, int64_t* rowphys,
                                                       int64_t* colphys_g, double* pivvals, int32_t* colpos_loc,
                                                       int64_t c0, int nloc, double* A, int64_t lda, double* Y,
                                                       int64_t ldy) {
-    __shared__ int win, ok;
+    __shared__ int win;
     if (threadIdx.x == 0) {
         CandR w = cand_none();
         int wr = -1;
@@ -1799,12 +1811,11 @@ __global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__
                 wr = r;
             }
         }
-        int accepted = 0;
-        if (!st->done) {
+        win = wr;
+        if (blockIdx.x == 0 && !st->done) {
             const int64_t rk = rowphys[k], ck = colphys_g[k];
             commit_pivot(k, w, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals, rk, ck);
             if (!st->done) {
-                accepted = 1;
                 const int64_t pcg = st->q;  // global physical column of the pivot
                 if (pcg >= c0 && pcg < c0 + nloc) colpos_loc[pcg - c0] = k;
                 if (ck >= c0 && ck < c0 + nloc) colpos_loc[ck - c0] = colpos_g[ck];
@@ -1812,18 +1823,22 @@ __global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__
                 st->q = nloc;  // the passes take the pivot column from the ghost
             }
         }
-        win = wr;
-        ok = accepted;
     }
     __syncthreads();
-    if (!ok) return;
     // the ghost: the winner's stale column and its pending y's (every trailing value NaN: no winner,
     // pivot NaN, the column is NaN as the reference's would be after the division)
-    const double* src = win >= 0 ? recv + (int64_t)win * rec : nullptr;
-    double* g = A + (int64_t)nloc * lda;
+    const int wr = win;
+    const double* src = wr >= 0 ? recv + (int64_t)wr * rec : nullptr;
+    double* gcol = A + (int64_t)nloc * lda;
     const double qnan = __longlong_as_double(0x7ff8000000000000LL);
-    for (int i = threadIdx.x; i < m; i += blockDim.x) g[i] = src ? src[kShardHdr + i] : qnan;
-    if (threadIdx.x < kMaxPend) Y[(int64_t)threadIdx.x * ldy + nloc] = src ? src[4 + threadIdx.x] : 0.0;
+    const int i0 = blockIdx.x * 1024 + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < m) gcol[i] = src ? src[kShardHdr + i] : qnan;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPend)
+        Y[(int64_t)threadIdx.x * ldy + nloc] = src ? src[4 + threadIdx.x] : 0.0;
 }
 
 void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t rec, int m, int k,
@@ -1831,7 +1846,8 @@ void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t 
                          int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
                          int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
                          int64_t ldy) {
-    hipLaunchKernelGGL(k_shard_commit, dim3(1), dim3(256), 0, s, recv, nranks, rec, m, k, st, reltol, abstol,
+    hipLaunchKernelGGL(k_shard_commit, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, recv,
+                       nranks, rec, m, k, st, reltol, abstol,
                        rowpos, colpos_g, rowphys, colphys_g, pivvals, colpos_loc, c0, nloc, A, lda, Y, ldy);
 }
 
