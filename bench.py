@@ -220,6 +220,7 @@ def main():
             shr = sharded_extras(T, ctx, dist, world, rank, dev_res if rank == 0 else None)
         except Exception as e:  # noqa: BLE001
             shr = {"sharded_extras_error": f"{type(e).__name__}: {e}"}
+            sys.stderr.write(f"rank {rank}: sharded extras failed: {shr['sharded_extras_error']}\n")
         if rank == 0:
             out["extras"] = extras(T, ctx)
             out["extras"]["pi_lorentz_sharded"] = sh
@@ -270,6 +271,10 @@ def sharded_extras(T, ctx, dist, world, rank, full_res):
     from tci_amd.distributed import Comm, DeviceComm, column_blocks, rrlu_sharded
 
     host = Comm(device="cpu") if dist is not None else None
+    if dist is not None:  # every rank reaches the communicator's creation, or none does (no hang)
+        import torch
+        t = torch.tensor([1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
     dcomm = DeviceComm(ctx, host)
 
     def barrier():
