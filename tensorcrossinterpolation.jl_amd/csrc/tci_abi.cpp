@@ -221,6 +221,15 @@ int ensure(tci_ctx* c, T** p, size_t* cap, size_t n) {
     return TCI_OK;
 }
 
+// fp16 shadow: its padding rows [m, lds) of every column are read by the MFMA search (as part of
+// a lane's 16-row load) and must be zero; no pass writes them
+int zero_shadow_pad(tci_ctx* c, int64_t lds, int64_t m, int64_t n) {
+    if (tci::shadow_elem_bytes() != 2 || lds <= m || n <= 0) return TCI_OK;
+    HIPCHK(c, hipMemset2DAsync(reinterpret_cast<char*>(c->sbuf) + 2 * m, (size_t)(2 * lds), 0,
+                               (size_t)(2 * (lds - m)), (size_t)n, c->stream));
+    return TCI_OK;
+}
+
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 // mapped pinned host buffer (zero-copy results of the small path; the stream is idle whenever it
@@ -417,6 +426,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         g.lds = round_up(m, 16);
         if ((st = ensure(c, &c->sbuf, &c->capS, (size_t)(g.lds * n)))) return st;
         g.S = c->sbuf;
+        if ((st = zero_shadow_pad(c, g.lds, m, n))) return st;
     }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
                                       std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
@@ -661,6 +671,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
         g.lds = round_up(m, 16);
         if ((st = ensure(c, &c->sbuf, &c->capS, (size_t)(g.lds * nl1)))) return st;
         g.S = c->sbuf;
+        if ((st = zero_shadow_pad(c, g.lds, m, nl1))) return st;
     }
     const int grid = tci::argmax_grid(mi, nl1, -1, g.cb, std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
     auto select = [&](int selk) -> int {

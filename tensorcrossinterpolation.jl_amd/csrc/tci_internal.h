@@ -105,6 +105,8 @@ struct FuncDev {
 
 // ---- rrLU (tci_rrlu.hip)
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
+// bytes per element of the rrLU passes' shadow (2: fp16, scaled per epoch; 4: fp32)
+int shadow_elem_bytes();
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
 // One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).

@@ -33,8 +33,17 @@
 #ifndef TCI_PASS2_U
 #define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
 #endif
+#ifndef TCI_SH_HALF
+#define TCI_SH_HALF 1  // shadow of the stale values in fp16, scaled per write-back epoch (0: fp32)
+#endif
 #ifndef TCI_PASS_SH_U
-#define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (kShRL rows of fp32 loaded per column)
+#define TCI_PASS_SH_U 2  // k_pass_sh: columns per chunk (kShRL rows of the shadow loaded per column)
+#endif
+#ifndef TCI_SH_MFMA
+#define TCI_SH_MFMA TCI_SH_HALF  // fp16 shadow: pending updates applied on the matrix cores (k_pass_mf)
+#endif
+#ifndef TCI_SH_TIGHT
+#define TCI_SH_TIGHT 7  // shadow search only while its error bound is below 2^-TCI_SH_TIGHT |pivot k|
 #endif
 #ifndef TCI_FLUSH_NT
 #define TCI_FLUSH_NT 1  // write-back pass: fp64 stores non-temporal (the next pass reads the shadow, not them)
@@ -43,6 +52,32 @@
 namespace tci {
 
 static constexpr int32_t kBig = 0x7fffffff;
+
+// Shadow element: fp16 (2 B) or fp32 (4 B). The fp16 shadow holds s * v with a power-of-two scale
+// s per epoch (the pivots between two write-backs): the stale trailing values of an epoch are
+// bounded by B (below), and s = 2^(14 - ilogb B) maps them below 2^15 < 65504. The scale is a
+// pure function of the committed pivot values, so the pass that writes the shadow and the passes
+// that read it derive the same s. 0 (search off) when B is outside [2^-100, 2^100] or not finite.
+constexpr bool kShHalf = TCI_SH_HALF != 0;
+#if TCI_SH_HALF
+typedef _Float16 shT;
+#else
+typedef float shT;
+#endif
+
+__device__ __forceinline__ double sh_scale(double B) {
+    if (!kShHalf) return 1.0;
+    if (!(B >= 0x1p-100 && B <= 0x1p100)) return 0.0;
+    return ldexp(1.0, 14 - ilogb(B));
+}
+
+// Bound on the stale trailing values of the epoch whose first pending pivot is t0. t0 = 0: the
+// stale values are A itself, bounded by |pivot 0| (the maximum of A). Otherwise they are the
+// Schur complement after pivot t0 - 1: a - x y with |a| <= |pivot t0-1| (the argmax) and
+// |x y| <= |pivot t0-1| (one factor normalised by it, the other bounded by it), so <= 2 |pivot t0-1|.
+__device__ __forceinline__ double sh_bound(const double* pv, int t0) {
+    return t0 == 0 ? fabs(pv[0]) : 2.0 * fabs(pv[t0 - 1]);
+}
 
 __device__ __forceinline__ double jl_max(double x, double y) {
     bool ysel = (y > x) || (signbit(y) < signbit(x));
@@ -465,6 +500,10 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
     }
     const bool in0 = rp0 > k, in1 = rp1 > k;
     const bool active = in0 || in1;
+    // fp16 shadow scale: of the epoch this write-back starts (first pending pivot k + 1), or of
+    // epoch 0 when pass 0 writes the shadow of A
+    [[maybe_unused]] const double shs =
+        (SH && kShHalf && P > 0) ? sh_scale(sh_bound(sel.pivvals, FLUSH ? k + 1 : 0)) : 1.0;
     if constexpr (P > 0) {
         // x_k of this thread's rows (pivot k's column, pending updates applied)
         const double2 cb2 = *reinterpret_cast<const double2*>(A + (rowok ? r0 : 0) + (int64_t)b * lda);
@@ -494,7 +533,9 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
         }
     }
     PPROF(1);
-    const bool wact = __any(active);  // wave-uniform: the slice has rows in the trailing block
+    // wave-uniform: the slice has rows in the trailing block (the passes that write the fp16
+    // shadow visit every row: non-trailing rows get shadow 0)
+    const bool wact = (SH && kShHalf && P > 0) || __any(active);
     for (int g0 = 0; g0 < ntc; g0 += G) {
         const int gn = min(G, ntc - g0);
         const int nch = gn * cb / U;
@@ -533,6 +574,21 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
         auto column = [&](double2 v, int lc, int j) {
             const int cp = cpos_s[lc];
             if (cp <= k) return;
+            if constexpr (SH && kShHalf && !FLUSH && P > 0) {
+                // pass 0 of an fp16 shadow: the shadow of the stale values (A itself), whose bound
+                // |pivot 0| is known only now. Every row: the epoch starts at pivot 0, so pivot
+                // 0's own row counts as pivoted during it (see k_pass_mf)
+                if (rowok) {
+                    _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
+                    const _Float16 h0 = (_Float16)(float)(v.x * shs);
+                    if (pair) {
+                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                        *reinterpret_cast<h2v*>(ps) = h2v{h0, (_Float16)(float)(v.y * shs)};
+                    } else {
+                        ps[0] = h0;
+                    }
+                }
+            }
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 const double y = ys[lc * PP + s];
@@ -557,7 +613,19 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                     *pa = v;
                 }
             }
-            if constexpr (SH) {
+            if constexpr (SH && kShHalf && FLUSH) {
+                if (rowok) {  // rows outside the trailing block: 0 (the MFMA search masks by data)
+                    _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
+                    const _Float16 h0 = in0 ? (_Float16)(float)(v.x * shs) : (_Float16)0.0f;
+                    if (pair) {
+                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                        *reinterpret_cast<h2v*>(ps) =
+                            h2v{h0, in1 ? (_Float16)(float)(v.y * shs) : (_Float16)0.0f};
+                    } else {
+                        ps[0] = h0;
+                    }
+                }
+            } else if constexpr (SH && !kShHalf) {
                 if ((FLUSH || P == 0) && rowok) {
                     float* ps = g.S + r0 + (int64_t)j * g.lds;
                     if (pair)
@@ -631,7 +699,8 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(PassK g, SelArgs sel) {
 // block) or fp32 could overflow, the kernel runs the exact body instead (uniform decision).
 template <int P>
 __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel, P2Lds<P>& L,
-                                             CandR& best, float eps, unsigned long long (&pt)[6]) {
+                                             CandR& best, float eps, double shs,
+                                             unsigned long long (&pt)[6]) {
     RrluState* st = sel.st;
     const int32_t* colpos = sel.colpos;
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev;
@@ -651,19 +720,20 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     // so the rows of a lane with r0 < m are inside the column)
     constexpr int RL = kShRL, RH = RL / 2;
     typedef float fvec __attribute__((ext_vector_type(RL)));
+    typedef shT svec __attribute__((ext_vector_type(RL)));
     const int r0 = tr * kRowsPerTile + slice * kShSliceRows + RL * lane;
     const int rb = r0 < m ? r0 : 0;
-    const float* const sbase = g.S + rb;
+    const shT* const sbase = reinterpret_cast<const shT*>(g.S) + rb;
     const int cbs = __builtin_ctz(cb);  // cb is 8 or 16
     auto chunk_col = [&](int g0, int h) -> int {
         const int it = g0 + ((h * U) >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + ((h * U) & (cb - 1));
     };
-    auto load_chunk = [&](int g0, int h, fvec (&v)[U]) {
+    auto load_chunk = [&](int g0, int h, svec (&v)[U]) {
         const int j = chunk_col(g0, h);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            v[u] = *reinterpret_cast<const fvec*>(sbase + (int64_t)min(j + u, n - 1) * lds);
+            v[u] = *reinterpret_cast<const svec*>(sbase + (int64_t)min(j + u, n - 1) * lds);
     };
     auto stage_col = [&](int g0) -> int {
         const int gn = min(G, ntc - g0);
@@ -678,7 +748,7 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const int lrow = slice * kShSliceRows + RL * lane;  // the lane's first row within the tile
     int jst = ntc > 0 ? stage_col(0) : -1;
     int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
-    fvec va[U], vb[U];
+    svec va[U], vb[U];
     const int nch0 = ntc > 0 ? min(G, ntc) * cb / U : 0;
     if (rep < nch0) load_chunk(0, rep, va);
     if (rep + kShReps < nch0) load_chunk(0, rep + kShReps, vb);
@@ -740,7 +810,7 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
     const float margin = 0x1p-20f;
     float tau = 0.0f;  // this lane's view of the workgroup's lower bound on the max |v|
     // chunk h's maximum |w| over the lane's trailing-block elements
-    auto approx = [&](int h, const fvec (&v)[U]) -> float {
+    auto approx = [&](int h, const svec (&v)[U]) -> float {
         float cm[RL];
 #pragma unroll
         for (int t = 0; t < RL; ++t) cm[t] = 0.0f;
@@ -748,9 +818,10 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
         for (int u = 0; u < U; ++u) {
             const int lc = h * U + u;
             if (L.cpos[lc] <= k) continue;  // wave-uniform
+            const fvec vf = __builtin_convertvector(v[u], fvec);
             f2v w[RH];
 #pragma unroll
-            for (int hh = 0; hh < RH; ++hh) w[hh] = f2v{v[u][2 * hh], v[u][2 * hh + 1]};
+            for (int hh = 0; hh < RH; ++hh) w[hh] = f2v{vf[2 * hh], vf[2 * hh + 1]};
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 const float y = L.yf[lc * P + s];
@@ -850,12 +921,12 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
                 for (int s = 0; s < P - 1; ++s) {
                     const double ysv = g.Y[(int64_t)s * ldy + jst];
                     L.ys[lc * P + s] = ysv;
-                    L.yf[lc * P + s] = (float)ysv;
+                    L.yf[lc * P + s] = (float)(ysv * shs);  // in the shadow's scale (exact: 2^e)
                     yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv));
                 }
                 if (!g.leftorth) yk = yk / piv;
                 L.ys[lc * P + P - 1] = yk;
-                L.yf[lc * P + P - 1] = (float)yk;
+                L.yf[lc * P + P - 1] = (float)(yk * shs);
                 if (tr == 0) {
                     g.Y[(int64_t)(P - 1) * ldy + jst] = yk;
                     g.Up[k + (int64_t)jst * g.ldu] = yk;
@@ -933,17 +1004,24 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_sh(PassK g, SelArgs sel) {
     PPROF(0);
     // error bound of the fp32 search over pending pivots k-P+1 .. k (uniform)
     const double* pv = sel.pivvals;
-    const double Mf = fabs(pv[g.k - P + 1]);
+    const int t0 = g.k - P + 1;  // first pending pivot; the shadow holds the stale values after t0 - 1
+    const double Mf = fabs(pv[t0]);
     double sumM = 0.0;
 #pragma unroll
-    for (int s = 0; s < P; ++s) sumM += fabs(pv[g.k - P + 1 + s]);
+    for (int s = 0; s < P; ++s) sumM += fabs(pv[t0 + s]);
     const double mag = Mf + 2.0 * sumM;
-    const double epsd = (double)(P + 3) * 0x1p-23 * mag + (double)(P + 2) * 0x1p-124;
-    const bool shok = mag < 0x1p100 && epsd < 0x1p-10 * fabs(pv[g.k]);
+    // fp16 shadow: everything below runs in the shadow's scale shs (a power of two), and the
+    // stored value adds one fp16 rounding of s v (|v| <= Mf): 2^-11 relative via fp32 (double
+    // rounding covered by the 2^-10 margin) or half an fp16 subnormal ulp, 2^-25
+    const double shs = sh_scale(sh_bound(pv, t0));
+    double epsd = (double)(P + 3) * 0x1p-23 * mag * shs + (double)(P + 2) * 0x1p-124;
+    if (kShHalf) epsd += 0x1p-11 * (1.0 + 0x1p-10) * Mf * shs + 0x1p-25;
+    const bool shok = shs > 0.0 && mag < 0x1p100 &&
+                      epsd < ldexp(fabs(pv[g.k]) * shs, -(kShHalf ? TCI_SH_TIGHT : 10));
     CandR best = cand_none();
     bool go;
     if (shok)
-        go = pass_sh_body<P>(g, sel, L, best, (float)(epsd * (1.0 + 0x1p-20)), pt);
+        go = pass_sh_body<P>(g, sel, L, best, (float)(epsd * (1.0 + 0x1p-20)), shs, pt);
     else
         go = pass2_body<P, false, false>(g, sel, L, best, pt);
     if (!go) return;
@@ -951,8 +1029,402 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_sh(PassK g, SelArgs sel) {
     pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, 0);
 }
 
+// ------------------------------------------------------------------ shadow search on MFMA
+// The read-only pass of k_pass_sh spends one fp32 FMA per element per pending update on the VALU
+// (measured ~2.5 us per pending update per pass at 8192^2), which is what bounded nb. Here the P
+// pending updates are one small GEMM per 16 x 16 tile on the matrix cores:
+//     W = S - X Y,   v_mfma_f32_16x16x32_f16, C = the fp16 shadow tile converted to fp32,
+// with X (16 rows x 3P) and Y (3P x 16 columns) the f16 two-term splits of the pending x's and
+// y's (x = xh + xl, y = yh + yl: slots (xh, yh), (xh, yl), (xl, yh) per update; the dropped xl yl
+// and the splits' own roundings are ~2^-21 |x y|). Products of f16 are exact in fp32; the MFMA
+// accumulates in fp32. One of x, y carries the shadow's scale, so both operands stay below 2^15.
+//
+// Geometry: a wave owns a 64-row slice (4 MFMA blocks) of its workgroup's 512-row tile, 2 waves
+// per slice take 16-column chunks from the slice's LDS counter. Lane l loads 16 consecutive fp16
+// rows (32 B) of the chunk's column l & 15; MFMA block b takes rows 16 (l >> 4) + 4 b + t of the
+// slice -- i.e. block b's D row i is slice row 16 (i >> 2) + 4 b + (i & 3), and the A fragment
+// (x's, registers for the whole pass) follows the same map.
+//
+// Row masking by data: rows pivoted before the epoch hold shadow 0 (the write-backs store 0 for
+// non-trailing rows) and x = 0, so W = 0; a row pivoted during the epoch at step t gets x_s for
+// s < t, x_t = 1 (leftorth; the pivot's own x) or pivot t (otherwise) and 0 after, so W is the
+// shadow image of its value after update t -- exactly 0 in the reference's arithmetic, |W| <= eps
+// here (the row was trailing for every update applied). Neither can raise a chunk's lower bound
+// above the true maximum. Rows past m: shadow rows [m, lds) are zero (memset once), x = 0; lanes
+// past lds load nothing. Columns are one per lane: a non-trailing column's lane reports no
+// maximum.
+//
+// Error bound (scaled units; |v| <= Mf the stale bound of the epoch, sumM = sum |pivot_s|):
+//   fp16 storage of s v:             2^-11 (1 + 2^-9) s Mf + 2^-25
+//   f16 splits and dropped xl yl:    2^-19 s sumM + P 2^-24 (subnormal halves)
+//   fp32 accumulation, <= 3P + 2 roundings of partial sums <= s (Mf + 2 sumM):  (3P + 4) 2^-23 s mag
+// (twice the rounding counts as margin), evaluated below as eps.
+constexpr int kMfRows = 64;                            // rows per wave slice
+constexpr int kMfBlk = kMfRows / 16;                   // MFMA row blocks per slice
+constexpr int kMfSlices = kRowsPerTile / kMfRows;      // slices per tile
+constexpr int kMfReps = kP2Threads / 64 / kMfSlices;   // waves per slice
+static_assert(kMfBlk == 4, "a lane's 16 loaded rows are 4 blocks of 4");
+
+// P <= 10 pending updates: 3P <= 30 split slots, one MFMA (K = 32) per tile; deeper passes use
+// k_pass_sh.
+constexpr int kMfMaxP = 10;
+constexpr int kMfKS = 32;                             // split slots per row / column
+constexpr int kMfKSP = kMfKS + 8;                     // LDS stride in halves (80 B: spreads banks)
+
+template <int P>
+struct P2MfLds {
+    double ys[kP2StageCols * P];                      // exact y's of the staged columns (examinations)
+    _Float16 yb[kP2StageCols * kMfKSP];               // their B fragments (y splits)
+    _Float16 xa[kRowsPerTile * kMfKSP];               // the tile's rows' A fragments (-x splits)
+    int cpos[kP2StageCols];
+    int cnt[kMfSlices];
+    unsigned tau;
+    double xk[kRowsPerTile];                          // x_k of the tile's rows
+};
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void f16_split(double v, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)(float)v;
+    lo = (_Float16)(float)(v - (double)hi);
+}
+
+template <int P>
+__device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P>& L,
+                                             CandR& best, float eps, double shs,
+                                             unsigned long long (&pt)[6]) {
+    static_assert(P >= 1 && P <= kMfMaxP, "one MFMA per tile");
+    RrluState* st = sel.st;
+    const int32_t* colpos = sel.colpos;
+    const int32_t* rowpos = sel.rowpos;
+    const double* pv = sel.pivvals;
+    const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
+    const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy, lds = g.lds;
+    const int t0 = k - P + 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slice = wave % kMfSlices, rep = wave / kMfSlices;
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const int tiles_c = (n + cb - 1) / cb;
+    const int nq = gridDim.x / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int tr = wid % tiles_r;
+    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    const int G = kP2StageCols / cb;
+    const int cbs = __builtin_ctz(cb);  // cb is 8 or 16
+    const int tb = tr * kRowsPerTile;
+    const int sb = tb + slice * kMfRows;        // the slice's first row
+    const int gq = lane >> 4, lcol = lane & 15;  // lane's row quad / column within a chunk
+    const int rl = sb + 16 * gq;                 // first of the lane's 16 loaded rows
+    const bool rload = rl < lds;                 // lds is a multiple of 16
+    const _Float16* const sbase = reinterpret_cast<const _Float16*>(g.S) + (rload ? rl : 0);
+    auto col_of = [&](int g0, int lc) -> int {  // global column of staged local column lc
+        const int it = g0 + (lc >> cbs);
+        return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
+    };
+    auto load_chunk = [&](int g0, int gcols, int h, h8v (&v)[2]) {
+        const int lc = h * 16 + lcol;
+        const int j = lc < gcols ? col_of(g0, lc) : n;
+        if (rload && j < n) {
+            const h8v* p = reinterpret_cast<const h8v*>(sbase + (int64_t)j * lds);
+            v[0] = p[0];
+            v[1] = p[1];
+        } else {
+            v[0] = h8v{};
+            v[1] = h8v{};
+        }
+    };
+    // staging: threads 0 .. 511 (one staged column each); the tile's rows: threads 512 .. 1023
+    const bool stager = threadIdx.x < kP2StageCols;
+    auto stage_col = [&](int g0) -> int {
+        const int gn = min(G, ntc - g0);
+        const int lc = threadIdx.x;
+        if (!stager || lc >= gn * cb) return -1;
+        return col_of(g0, lc);
+    };
+    // wave activity from the rows of its slice (lanes 0..15 x 4: every row once)
+    bool act = false;
+#pragma unroll
+    for (int b = 0; b < kMfBlk; ++b) {
+        const int r = sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
+        act |= (r < m && rowpos[r] > k);
+    }
+    int jst = ntc > 0 ? stage_col(0) : -1;
+    int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+    const int prow = threadIdx.x - kP2StageCols;  // this thread's tile row (row threads)
+    const int rrow = tb + (prow >= 0 ? prow : 0);
+    const int rpos = (!stager && rrow < m) ? rowpos[rrow] : -1;
+    h8v va[2], vb[2];
+    const int gc0 = ntc > 0 ? min(G, ntc) * cb : 0;
+    const int nch0 = (gc0 + 15) / 16;
+    if (rep < nch0) load_chunk(0, gc0, rep, va);
+    if (rep + kMfReps < nch0) load_chunk(0, gc0, rep + kMfReps, vb);
+    if (st->done) return false;
+    const int a = (int)st->p, bq = (int)st->q;
+    const double piv = st->pval;
+    if (!stager) {
+        // row thread: x_k of its row (the reference's operation order), the split A fragment row
+        // -(x_0 .. x_{P-1}) with the data masking of rows outside the trailing block
+        const int rr = rrow < m ? rrow : 0;
+        double xs[P];
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)s * ldx + rr];
+        double xk = g.A[rr + (int64_t)bq * lda];
+#pragma unroll
+        for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
+        if (leftorth) xk = xk / piv;
+        L.xk[prow] = xk;
+        if (q == 0 && rpos > k) {
+            g.X[(int64_t)(P - 1) * ldx + rrow] = xk;
+            g.Lp[rrow + (int64_t)k * g.ldl] = xk;
+        }
+        xs[P - 1] = xk;
+        // rows pivoted before this epoch (and rows past m): 0; pivoted at step rp of it: x_s for
+        // s < rp - t0, then the pivot's own x (1, or the pivot when not leftorth), then 0
+        const int dd = rpos > k ? P : (rpos >= t0 ? rpos - t0 : -1);
+        const double own = leftorth ? 1.0 : (rpos >= t0 && rpos <= k ? pv[rpos] : 0.0);
+        _Float16 sl[kMfKS];
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            double x = s < dd ? xs[s] : (s == dd ? own : 0.0);
+            x = -(leftorth ? x : x * shs);
+            f16_split(x, sl[3 * s], sl[3 * s + 2]);
+            sl[3 * s + 1] = sl[3 * s];
+        }
+#pragma unroll
+        for (int z = 3 * P; z < kMfKS; ++z) sl[z] = (_Float16)0.0f;
+#pragma unroll
+        for (int z = 0; z < kMfKS / 8; ++z) {
+            h8v w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = sl[8 * z + e];
+            *reinterpret_cast<h8v*>(&L.xa[prow * kMfKSP + 8 * z]) = w;
+        }
+    }
+    PPROF(1);
+    const bool wact = __any(act);
+    const float margin = 0x1p-20f;
+    float tau = 0.0f;
+    h8v af[kMfBlk];  // A fragments (registers for the whole pass)
+    // chunk h: the lane's column's maximum |w| over its 16 rows (-1: no trailing column), and
+    // the blocks whose maximum reaches the lane's current threshold (exact examination)
+    auto approx = [&](int h, int gcols, const h8v (&v)[2], unsigned& bm) -> float {
+        const int lc = h * 16 + lcol;
+        const int cp = lc < gcols ? L.cpos[lc] : -1;
+        const h8v bf = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * kMfKSP + 8 * gq]);
+        const float thr = tau - tau * margin - eps;
+        float c = 0.0f;
+        bm = 0;
+#pragma unroll
+        for (int b = 0; b < kMfBlk; ++b) {
+            const h8v& hv = v[b >> 1];
+            const int o = 4 * (b & 1);
+            f4v acc = {(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bf, acc, 0, 0, 0);
+            const float mb = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
+                                             __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
+            bm |= (mb >= thr ? 1u : 0u) << b;
+            c = __builtin_fmaxf(c, mb);
+        }
+        return cp > k ? c : -1.0f;
+    };
+    // exact examination of the lane's column in chunk h, blocks bm (4 rows each), as the exact
+    // pass does it
+    auto examine = [&](int g0, int h, unsigned bm) {
+        const int lc = h * 16 + lcol;
+        const int cp = L.cpos[lc];
+        const int j = col_of(g0, lc);
+        int rbx = rl;
+        asm volatile("" : "+v"(rbx));
+        const double yk = L.ys[lc * P + P - 1];
+#pragma unroll 1
+        for (int t = 0; t < 16; ++t) {
+            if (!(bm >> (t >> 2) & 1)) continue;
+            const int r = rbx + t;
+            if (r >= m) continue;
+            const int rp = rowpos[r];
+            double xv[P];
+#pragma unroll
+            for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
+            double v = g.A[r + (int64_t)j * lda];
+            if (rp <= k) continue;
+#pragma unroll
+            for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+            v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], yk));
+            const double a2 = __dmul_rn(v, v);
+            if (a2 >= best.v) cand_take(best, CandR{a2, v, cp, rp, j, r});
+        }
+    };
+    auto test = [&](float c) -> bool {
+        if (c < 0.0f) return false;
+        const float lb = fmaxf(c - eps, 0.0f);
+        const float ts = __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        tau = fmaxf(tau, ts);
+        if (lb > tau) {
+            tau = lb;
+            atomicMax(&L.tau, __float_as_uint(lb));
+        }
+        return c + eps >= tau - tau * margin;
+    };
+    for (int g0 = 0; g0 < ntc; g0 += G) {
+        const int gn = min(G, ntc - g0);
+        const int gcols = gn * cb;
+        const int nch = (gcols + 15) / 16;
+        if (g0 > 0) {
+            jst = stage_col(g0);
+            cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+            if (wact) {
+                if (rep < nch) load_chunk(g0, gcols, rep, va);
+                if (rep + kMfReps < nch) load_chunk(g0, gcols, rep + kMfReps, vb);
+            }
+            __syncthreads();
+        }
+        if (jst >= 0) {
+            int lc = threadIdx.x;
+            asm volatile("" : "+v"(lc));
+            L.cpos[lc] = cpst;
+            if (cpst > k) {
+                double ysv[P];
+#pragma unroll
+                for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)s * ldy + jst];
+                double yk = g.A[a + (int64_t)jst * lda];
+#pragma unroll
+                for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
+                if (!leftorth) yk = yk / piv;
+                ysv[P - 1] = yk;
+                if (tr == 0) {
+                    g.Y[(int64_t)(P - 1) * ldy + jst] = yk;
+                    g.Up[k + (int64_t)jst * g.ldu] = yk;
+                }
+                // B fragment: slots (yh_s, yl_s, yh_s) for s < P, zero after
+                _Float16 sl[kMfKS];
+#pragma unroll
+                for (int s = 0; s < P; ++s) {
+                    L.ys[lc * P + s] = ysv[s];
+                    f16_split(leftorth ? ysv[s] * shs : ysv[s], sl[3 * s], sl[3 * s + 1]);
+                    sl[3 * s + 2] = sl[3 * s];
+                }
+#pragma unroll
+                for (int z = 3 * P; z < kMfKS; ++z) sl[z] = (_Float16)0.0f;
+#pragma unroll
+                for (int z = 0; z < kMfKS / 8; ++z) {
+                    h8v w;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) w[e] = sl[8 * z + e];
+                    *reinterpret_cast<h8v*>(&L.yb[lc * kMfKSP + 8 * z]) = w;
+                }
+            }
+        }
+        if (threadIdx.x < kMfSlices) L.cnt[threadIdx.x] = 2 * kMfReps;
+        if (g0 == 0 && threadIdx.x == 0) L.tau = 0u;
+        __syncthreads();
+        if (g0 == 0) {
+#pragma unroll
+            for (int b = 0; b < kMfBlk; ++b) {
+                const int pr = slice * kMfRows + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
+                af[b] = *reinterpret_cast<const h8v*>(&L.xa[pr * kMfKSP + 8 * gq]);
+            }
+            PPROF(2);
+        }
+        auto grab = [&]() -> int {
+            int h = 0;
+            if (lane == 0) h = atomicAdd(&L.cnt[slice], 1);
+            return __shfl(h, 0);
+        };
+        int h0 = rep, h1 = rep + kMfReps;
+        int ex0 = -1, ex1 = -1;
+        unsigned bm0 = 0, bm1 = 0;
+        if (g0 == 0) {
+            float c0 = -1.0f, c1 = -1.0f;
+            const int e0 = h0, e1 = h1;
+            if (wact) {
+                if (h0 < nch) {
+                    c0 = approx(h0, gcols, va, bm0);
+                    h0 = grab();
+                    if (h0 < nch) load_chunk(g0, gcols, h0, va);
+                }
+                if (h1 < nch) {
+                    c1 = approx(h1, gcols, vb, bm1);
+                    h1 = grab();
+                    if (h1 < nch) load_chunk(g0, gcols, h1, vb);
+                }
+                float lb = fmaxf(fmaxf(c0, c1) - eps, 0.0f);
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) lb = fmaxf(lb, __shfl_xor(lb, off));
+                if (lane == 0) atomicMax(&L.tau, __float_as_uint(lb));
+            }
+            __syncthreads();
+            if (!wact) continue;
+            tau = __uint_as_float(L.tau);
+            if (c0 >= 0.0f && c0 + eps >= tau - tau * margin) ex0 = e0;
+            if (c1 >= 0.0f && c1 + eps >= tau - tau * margin) ex1 = e1;
+        } else if (!wact) {
+            continue;
+        }
+        for (;;) {
+            if (ex0 >= 0) examine(g0, ex0, bm0);
+            if (ex1 >= 0) examine(g0, ex1, bm1);
+            ex0 = ex1 = -1;
+            if (h0 >= nch) break;
+            {
+                const float c = approx(h0, gcols, va, bm0);
+                const int e = h0;
+                h0 = grab();
+                if (h0 < nch) load_chunk(g0, gcols, h0, va);
+                if (test(c)) ex0 = e;
+            }
+            if (h1 < nch) {
+                const float c = approx(h1, gcols, vb, bm1);
+                const int e = h1;
+                h1 = grab();
+                if (h1 < nch) load_chunk(g0, gcols, h1, vb);
+                if (test(c)) ex1 = e;
+            }
+        }
+    }
+    return true;
+}
+
+template <int P>
+__global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
+    __shared__ union {
+        P2Lds<P> x;
+        P2MfLds<P> f;
+    } L;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
+    const double* pv = sel.pivvals;
+    const int t0 = g.k - P + 1;
+    const double Mf = fabs(pv[t0]);
+    double sumM = 0.0, maxM = 0.0;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+        sumM += fabs(pv[t0 + s]);
+        maxM = fmax(maxM, fabs(pv[t0 + s]));
+    }
+    const double mag = Mf + 2.0 * sumM;
+    const double shs = sh_scale(sh_bound(pv, t0));
+    const double epsd = 0x1p-11 * (1.0 + 0x1p-9) * Mf * shs + 0x1p-25 + 0x1p-19 * sumM * shs +
+                        (double)P * 0x1p-24 + (double)(3 * P + 4) * 0x1p-23 * mag * shs;
+    // the f16 operands (the scaled factor <= s |pivot_s|) must stay below 2^15
+    const bool shok = shs > 0.0 && mag < 0x1p100 && maxM * shs <= 0x1p15 &&
+                      epsd < ldexp(fabs(pv[g.k]) * shs, -TCI_SH_TIGHT);
+    CandR best = cand_none();
+    bool go;
+    if (shok)
+        go = pass_mf_body<P>(g, sel, L.f, best, (float)(epsd * (1.0 + 0x1p-20)), shs, pt);
+    else
+        go = pass2_body<P, false, false>(g, sel, L.x, best, pt);
+    if (!go) return;
+    PPROF(3);
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, 0);
+}
+
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
 // column tiles (at least one; the host rejects tiles_r > kMaxPassGrid).
+int shadow_elem_bytes() { return kShHalf ? 2 : 4; }
+
 int argmax_grid(int m, int n, int k, int cb, int max_grid) {
     (void)k;
     const long long tiles_r = m > 0 ? (m + kRowsPerTile - 1) / kRowsPerTile : 1;
@@ -969,7 +1441,22 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
                       g.ticket, g.reltol, g.abstol,  g.selk,    g.lout};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
                   g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
-    if (shadow) {
+    if (shadow && kShHalf) {
+        // fp16: the shadow's scale needs |pivot 0|, so the initial pass only selects, and pass 0
+        // (exact) writes the shadow of A; write-backs write the shadow of the new stale values
+        if (P == 0)
+            hipLaunchKernelGGL((k_pass2<0, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        else if (flush)
+            hipLaunchKernelGGL((k_pass2<P, true, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        else if (P == 1 && g.k == 0)
+            hipLaunchKernelGGL((k_pass2<1, false, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        else if constexpr (P > 0) {
+            if constexpr (TCI_SH_MFMA && P <= kMfMaxP)
+                hipLaunchKernelGGL((k_pass_mf<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            else
+                hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        }
+    } else if (shadow) {
         if (flush || P == 0)
             hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
         else if constexpr (P > 0)
