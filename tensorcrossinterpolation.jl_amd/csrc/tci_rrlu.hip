@@ -42,6 +42,9 @@
 #ifndef TCI_SH_MFMA
 #define TCI_SH_MFMA TCI_SH_HALF  // fp16 shadow: pending updates applied on the matrix cores (k_pass_mf)
 #endif
+#ifndef TCI_SH_NT
+#define TCI_SH_NT 0  // write-back pass: fp16 shadow stores non-temporal
+#endif
 #ifndef TCI_SH_TIGHT
 #define TCI_SH_TIGHT 7  // shadow search only while its error bound is below 2^-TCI_SH_TIGHT |pivot k|
 #endif
@@ -619,8 +622,11 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                     const _Float16 h0 = in0 ? (_Float16)(float)(v.x * shs) : (_Float16)0.0f;
                     if (pair) {
                         typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                        *reinterpret_cast<h2v*>(ps) =
-                            h2v{h0, in1 ? (_Float16)(float)(v.y * shs) : (_Float16)0.0f};
+                        const h2v hw = h2v{h0, in1 ? (_Float16)(float)(v.y * shs) : (_Float16)0.0f};
+                        if (TCI_SH_NT)
+                            __builtin_nontemporal_store(hw, reinterpret_cast<h2v*>(ps));
+                        else
+                            *reinterpret_cast<h2v*>(ps) = hw;
                     } else {
                         ps[0] = h0;
                     }
@@ -1070,6 +1076,7 @@ static_assert(kMfBlk == 4, "a lane's 16 loaded rows are 4 blocks of 4");
 constexpr int kMfMaxP = 10;
 constexpr int kMfKS = 32;                             // split slots per row / column
 constexpr int kMfKSP = kMfKS + 8;                     // LDS stride in halves (80 B: spreads banks)
+constexpr int kMfExCap = 128;                         // deferred examinations per wave
 
 template <int P>
 struct P2MfLds {
@@ -1080,6 +1087,8 @@ struct P2MfLds {
     int cnt[kMfSlices];
     unsigned tau;
     double xk[kRowsPerTile];                          // x_k of the tile's rows
+    unsigned ex[kP2Threads / 64 * kMfExCap];          // per-wave lists of blocks to examine exactly
+    float exm[kP2Threads / 64 * kMfExCap];            // their approximate maxima
 };
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -1207,57 +1216,81 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     const float margin = 0x1p-20f;
     float tau = 0.0f;
     h8v af[kMfBlk];  // A fragments (registers for the whole pass)
-    // chunk h: the lane's column's maximum |w| over its 16 rows (-1: no trailing column), and
-    // the blocks whose maximum reaches the lane's current threshold (exact examination)
-    auto approx = [&](int h, int gcols, const h8v (&v)[2], unsigned& bm) -> float {
+    // chunk h: the lane's column's maximum |w| over its 16 rows and per 4-row block (-1: not a
+    // trailing column)
+    auto approx = [&](int h, int gcols, const h8v (&v)[2], float (&mbs)[kMfBlk]) -> float {
         const int lc = h * 16 + lcol;
         const int cp = lc < gcols ? L.cpos[lc] : -1;
         const h8v bf = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * kMfKSP + 8 * gq]);
-        const float thr = tau - tau * margin - eps;
         float c = 0.0f;
-        bm = 0;
 #pragma unroll
         for (int b = 0; b < kMfBlk; ++b) {
             const h8v& hv = v[b >> 1];
             const int o = 4 * (b & 1);
             f4v acc = {(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
             acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bf, acc, 0, 0, 0);
-            const float mb = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
-                                             __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
-            bm |= (mb >= thr ? 1u : 0u) << b;
-            c = __builtin_fmaxf(c, mb);
+            mbs[b] = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
+                                     __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
+            c = __builtin_fmaxf(c, mbs[b]);
         }
-        return cp > k ? c : -1.0f;
+        if (cp <= k) {
+#pragma unroll
+            for (int b = 0; b < kMfBlk; ++b) mbs[b] = -1.0f;
+            c = -1.0f;
+        }
+        return c;
     };
-    // exact examination of the lane's column in chunk h, blocks bm (4 rows each), as the exact
-    // pass does it
-    auto examine = [&](int g0, int h, unsigned bm) {
-        const int lc = h * 16 + lcol;
-        const int cp = L.cpos[lc];
-        const int j = col_of(g0, lc);
-        int rbx = rl;
-        asm volatile("" : "+v"(rbx));
-        const double yk = L.ys[lc * P + P - 1];
-#pragma unroll 1
-        for (int t = 0; t < 16; ++t) {
-            if (!(bm >> (t >> 2) & 1)) continue;
-            const int r = rbx + t;
+    // Exact examinations are deferred: blocks (4 rows of one column) that may hold the maximum
+    // or a tie with it go to the wave's list in LDS, and the whole wave examines them together
+    // -- one element per lane, all its loads in flight at once -- when the list fills and at the
+    // end of each staged group, after pruning them against the latest bound tau.
+    unsigned* const exl = L.ex + wave * kMfExCap;
+    float* const exm = L.exm + wave * kMfExCap;
+    int nex = 0;  // wave-uniform list length
+    auto flush = [&](int g0) {
+        const float thr = tau - tau * margin;
+        for (int e = lane; e < 4 * nex; e += 64) {
+            const unsigned key = exl[e >> 2];
+            if (exm[e >> 2] + eps < thr) continue;
+            const int lc = (int)(key & 1023u), rq = (int)(key >> 10);
+            const int r = sb + 4 * rq + (e & 3);
             if (r >= m) continue;
-            const int rp = rowpos[r];
+            const int j = col_of(g0, lc);
             double xv[P];
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
             double v = g.A[r + (int64_t)j * lda];
+            const int rp = rowpos[r];
             if (rp <= k) continue;
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
-            v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], yk));
+            v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * P + P - 1]));
             const double a2 = __dmul_rn(v, v);
-            if (a2 >= best.v) cand_take(best, CandR{a2, v, cp, rp, j, r});
+            if (a2 >= best.v) cand_take(best, CandR{a2, v, L.cpos[lc], rp, j, r});
+        }
+        nex = 0;
+    };
+    // append the lane's blocks whose maximum reaches bound (chunk h); flushes first if needed
+    auto append = [&](int g0, int h, const float (&mbs)[kMfBlk], float bound) {
+        const unsigned lc = (unsigned)(h * 16 + lcol);
+#pragma unroll
+        for (int b = 0; b < kMfBlk; ++b) {
+            const bool f = mbs[b] >= 0.0f && mbs[b] + eps >= bound;
+            const uint64_t bal = __ballot(f);
+            if (bal == 0) continue;
+            const int cnt = __popcll(bal);
+            if (nex + cnt > kMfExCap) flush(g0);
+            if (f) {
+                const int at = nex + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                exl[at] = lc | (unsigned)(4 * gq + b) << 10;
+                exm[at] = mbs[b];
+            }
+            nex += cnt;
         }
     };
-    auto test = [&](float c) -> bool {
-        if (c < 0.0f) return false;
+    auto test = [&](float c) {
+        if (c < 0.0f) return;
         const float lb = fmaxf(c - eps, 0.0f);
         const float ts = __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         tau = fmaxf(tau, ts);
@@ -1265,7 +1298,6 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             tau = lb;
             atomicMax(&L.tau, __float_as_uint(lb));
         }
-        return c + eps >= tau - tau * margin;
     };
     for (int g0 = 0; g0 < ntc; g0 += G) {
         const int gn = min(G, ntc - g0);
@@ -1333,19 +1365,21 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             return __shfl(h, 0);
         };
         int h0 = rep, h1 = rep + kMfReps;
-        int ex0 = -1, ex1 = -1;
-        unsigned bm0 = 0, bm1 = 0;
+        float mb0[kMfBlk], mb1[kMfBlk];
         if (g0 == 0) {
+            // seed: the first two chunks of every wave set the workgroup's bound first
             float c0 = -1.0f, c1 = -1.0f;
             const int e0 = h0, e1 = h1;
+#pragma unroll
+            for (int b = 0; b < kMfBlk; ++b) mb0[b] = mb1[b] = -1.0f;
             if (wact) {
                 if (h0 < nch) {
-                    c0 = approx(h0, gcols, va, bm0);
+                    c0 = approx(h0, gcols, va, mb0);
                     h0 = grab();
                     if (h0 < nch) load_chunk(g0, gcols, h0, va);
                 }
                 if (h1 < nch) {
-                    c1 = approx(h1, gcols, vb, bm1);
+                    c1 = approx(h1, gcols, vb, mb1);
                     h1 = grab();
                     if (h1 < nch) load_chunk(g0, gcols, h1, vb);
                 }
@@ -1357,31 +1391,34 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             __syncthreads();
             if (!wact) continue;
             tau = __uint_as_float(L.tau);
-            if (c0 >= 0.0f && c0 + eps >= tau - tau * margin) ex0 = e0;
-            if (c1 >= 0.0f && c1 + eps >= tau - tau * margin) ex1 = e1;
+            const float bound = tau - tau * margin;
+            if (e0 < nch) append(g0, e0, mb0, bound);
+            if (e1 < nch) append(g0, e1, mb1, bound);
         } else if (!wact) {
             continue;
         }
-        for (;;) {
-            if (ex0 >= 0) examine(g0, ex0, bm0);
-            if (ex1 >= 0) examine(g0, ex1, bm1);
-            ex0 = ex1 = -1;
-            if (h0 >= nch) break;
+        // h0's values in va, h1's in vb; every grab returns a larger index than both
+        while (h0 < nch) {
             {
-                const float c = approx(h0, gcols, va, bm0);
+                const float c = approx(h0, gcols, va, mb0);
                 const int e = h0;
                 h0 = grab();
                 if (h0 < nch) load_chunk(g0, gcols, h0, va);
-                if (test(c)) ex0 = e;
+                test(c);
+                append(g0, e, mb0, tau - tau * margin);
             }
             if (h1 < nch) {
-                const float c = approx(h1, gcols, vb, bm1);
+                const float c = approx(h1, gcols, vb, mb1);
                 const int e = h1;
                 h1 = grab();
                 if (h1 < nch) load_chunk(g0, gcols, h1, vb);
-                if (test(c)) ex1 = e;
+                test(c);
+                append(g0, e, mb1, tau - tau * margin);
             }
         }
+        // the latest bound of the workgroup prunes the list
+        tau = fmaxf(tau, __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+        flush(g0);
     }
     return true;
 }
