@@ -28,6 +28,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tci_internal.h"
 
 #ifndef TCI_PASS2_U
@@ -1247,7 +1249,9 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     unsigned* const exl = L.ex + wave * kMfExCap;
     float* const exm = L.exm + wave * kMfExCap;
     int nex = 0;  // wave-uniform list length
-    auto flush = [&](int g0) {
+    // FAST: all P - 1 pending x's of an element in flight at once (the final flush, when the
+    // streaming registers are dead); otherwise one at a time (a full list mid-stream: rare)
+    auto flush = [&](int g0, auto fast) {
         const float thr = tau - tau * margin;
         for (int e = lane; e < 4 * nex; e += 64) {
             const unsigned key = exl[e >> 2];
@@ -1256,14 +1260,20 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const int r = sb + 4 * rq + (e & 3);
             if (r >= m) continue;
             const int j = col_of(g0, lc);
-            double xv[P];
-#pragma unroll
-            for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
             double v = g.A[r + (int64_t)j * lda];
             const int rp = rowpos[r];
             if (rp <= k) continue;
+            if constexpr (decltype(fast)::value) {
+                double xv[P];
 #pragma unroll
-            for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+                for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
+#pragma unroll
+                for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+            } else {
+#pragma unroll 1
+                for (int s = 0; s < P - 1; ++s)
+                    v = __dsub_rn(v, __dmul_rn(g.X[(int64_t)s * ldx + r], L.ys[lc * P + s]));
+            }
             v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * P + P - 1]));
             const double a2 = __dmul_rn(v, v);
             if (a2 >= best.v) cand_take(best, CandR{a2, v, L.cpos[lc], rp, j, r});
@@ -1279,7 +1289,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const uint64_t bal = __ballot(f);
             if (bal == 0) continue;
             const int cnt = __popcll(bal);
-            if (nex + cnt > kMfExCap) flush(g0);
+            if (nex + cnt > kMfExCap) flush(g0, std::false_type{});
             if (f) {
                 const int at = nex + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
@@ -1418,7 +1428,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         }
         // the latest bound of the workgroup prunes the list
         tau = fmaxf(tau, __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
-        flush(g0);
+        flush(g0, std::true_type{});
     }
     return true;
 }
