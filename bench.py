@@ -29,15 +29,16 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def pass_bytes(m, n, r, nb, stride=1, shadow=True):
+def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2):
     """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-1 with k % stride == 0
     (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block. Exact passes: a
     read-only pass reads 8 B/element, every nb-th pass (pending count reaches nb; never the last)
-    also writes 8 B/element back. With the certified fp32 shadow search a
-    read-only pass streams the 4-B shadow instead, and a write-back pass also writes the shadow
-    (8 + 8 + 4 B/element); the exact re-reads of candidate chunks are data-dependent and not
-    counted. Returns (read_only, write_back) as (bytes, launches)."""
-    ro_per, wb_per = (4.0, 20.0) if shadow else (8.0, 16.0)
+    also writes 8 B/element back. With the certified shadow search (sh_bytes = 2
+    for the fp16 shadow, 4 for fp32) a read-only pass streams the shadow instead, and a
+    write-back pass also writes it (8 + 8 + sh_bytes B/element); with the fp16 shadow pass 0 is
+    exact and writes the shadow of A (8 + 2). The exact re-reads of candidate elements are
+    data-dependent and not counted. Returns (read_only, write_back) as (bytes, launches)."""
+    ro_per, wb_per = (float(sh_bytes), 16.0 + sh_bytes) if shadow else (8.0, 16.0)
     ro_b = wb_b = 0.0
     ro_n = wb_n = 0
     pend = 0
@@ -53,7 +54,7 @@ def pass_bytes(m, n, r, nb, stride=1, shadow=True):
             wb_b += wb_per * elems
             wb_n += 1
         else:
-            ro_b += ro_per * elems
+            ro_b += (8.0 + sh_bytes if (shadow and sh_bytes == 2 and k == 0) else ro_per) * elems
             ro_n += 1
     return (ro_b, ro_n), (wb_b, wb_n)
 
@@ -151,13 +152,17 @@ def main():
     flops = rrlu_flops(m, n, r)
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
-    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride, shadow)
+    sh_bytes = int(ctx.lib.tci_rrlu_shadow_bytes())
+    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride, shadow, sh_bytes)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
         dom, dom_ms, dom_launches, dom_bytes, dom_n = (
-            ("k_pass_sh<P> (read-only: fp32 shadow streamed, pending updates applied in fp32, "
-             "certified abs2 argmax with exact fp64 re-reads of candidate chunks)") if shadow else
+            (("k_pass_mf<P> (read-only: fp16 shadow streamed, pending updates applied by f16-split "
+              "MFMA with fp32 accumulation, certified abs2 argmax with exact fp64 re-reads of "
+              "candidate elements)") if sh_bytes == 2 else
+             ("k_pass_sh<P> (read-only: fp32 shadow streamed, pending updates applied in fp32, "
+              "certified abs2 argmax with exact fp64 re-reads of candidate chunks)")) if shadow else
             "k_pass2<P,false> (read-only: pending updates applied on the fly + abs2 argmax)",
             ro_ms, ro_launches, ro_b, ro_n)
     else:
@@ -195,11 +200,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
-                     "deferred_depth_nb": nb, "shadow_search": shadow},
+                     "deferred_depth_nb": nb, "shadow_search": shadow, "shadow_bytes": sh_bytes},
     }
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
-    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, shadow))
+    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, shadow, sh_bytes))
     # roofline calibration on the same buffers: 16-B stream read and stream copy, best grid
     import ctypes as C
     nel = A.ld * n
@@ -240,13 +245,13 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 11, "shadow": True}  # the profiled command
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_fp16_pmc_summary.json")
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 11, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 
-def pmc_traffic(fam, m, n, r, nb, shadow):
+def pmc_traffic(fam, m, n, r, nb, shadow, sh_bytes):
     """HBM bytes per launch of kernel family `fam` from the committed rocprofv3 PMC summary."""
-    if ({"m": m, "n": n, "r": r, "nb": nb, "shadow": shadow} != PMC_CONFIG
+    if ({"m": m, "n": n, "r": r, "nb": nb, "shadow": shadow, "sh_bytes": sh_bytes} != PMC_CONFIG
             or not os.path.exists(PMC_SUMMARY)):
         return {"traffic": None}
     with open(PMC_SUMMARY) as fh:

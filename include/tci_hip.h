@@ -97,12 +97,16 @@ int tci_set_rrlu_small(tci_ctx* ctx, int enabled);
  * enabled = 0 forces the pass pipeline. Bitwise identical results. Default on (env
  * TCI_RRLU_MID=0: off). */
 int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
-/* Certified fp32 search in the read-only passes of the pass pipeline: the write-back passes also
- * keep an fp32 shadow of the stale values (+4 B/element of device memory), and a read-only pass
- * streams it (4 B/element instead of 8), bounds the fp32 error, and re-reads in fp64 only the
- * chunks that can hold the argmax. Bitwise identical results (same argmax, same tie order as
- * submatrixargmax, matrixlu.jl:46-87). Default on (env TCI_RRLU_SHADOW=0: off). */
+/* Certified shadow search in the read-only passes of the pass pipeline: the write-back passes also
+ * keep a shadow of the stale values -- fp16 scaled per write-back epoch (2 B/element; fp32 in
+ * the TCI_SH_HALF=0 build) -- and a read-only pass streams it instead of the fp64 values, applies
+ * the pending updates on the matrix cores (f16-split MFMA, fp32 accumulation), bounds the error,
+ * and re-reads in fp64 only the elements that can hold the argmax. Bitwise identical results (same
+ * argmax, same tie order as submatrixargmax, matrixlu.jl:46-87). Default on (env
+ * TCI_RRLU_SHADOW=0: off). */
 int tci_set_rrlu_shadow(tci_ctx* ctx, int enabled);
+/* Bytes per element of that shadow in this build (2: fp16, 4: fp32). */
+int tci_rrlu_shadow_bytes(void);
 
 /* fp64 MFMA forms of the MatrixLUCI factors (bit 1), the site-tensor getrf
  * (bit 2) and getrs (bit 4); default 7 (env TCI_DENSE_MFMA). 0 restores the round-1 scalar

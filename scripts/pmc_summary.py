@@ -18,7 +18,7 @@ from collections import defaultdict
 
 def family(name):
     short = name.split("(")[0].replace("void ", "").strip()
-    if short.startswith("tci::k_pass_sh<"):
+    if short.startswith(("tci::k_pass_sh<", "tci::k_pass_mf<")):
         return "rrlu_read_only_pass"
     if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
         targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]

@@ -817,6 +817,8 @@ int tci_set_rrlu_shadow(tci_ctx* c, int enabled) {
     return TCI_OK;
 }
 
+int tci_rrlu_shadow_bytes(void) { return tci::shadow_elem_bytes(); }
+
 int tci_set_dense_mfma(tci_ctx* c, int mask) {
     if (!c || mask < 0 || mask > tci::kDenseAll) return TCI_ERR_ARG;
     c->dense = mask;
