@@ -107,6 +107,10 @@ int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
 int tci_set_rrlu_shadow(tci_ctx* ctx, int enabled);
 /* Bytes per element of that shadow in this build (2: fp16, 4: fp32). */
 int tci_rrlu_shadow_bytes(void);
+/* ComplexF64 rrLU: the same certified shadow search (fp16 planes of the real and imaginary parts,
+ * pending updates on f16-split MFMA, exact fp64 re-reads). Bitwise identical
+ * results. Default on (env TCI_C128_SH=0: off). */
+int tci_set_c128_shadow(tci_ctx* ctx, int enabled);
 
 /* fp64 MFMA forms of the MatrixLUCI factors (bit 1), the site-tensor getrf
  * (bit 2) and getrs (bit 4); default 7 (env TCI_DENSE_MFMA). 0 restores the round-1 scalar

@@ -49,6 +49,7 @@ struct tci_ctx {
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
     int c128_nb = 6;             // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1)
+    int c128_sh = 1;             // ComplexF64 rrLU certified shadow search (env TCI_C128_SH)
     int ncu = 0;           // compute units of the device
     double* colbuf = nullptr;  // mid path: published candidate columns
     size_t capColbuf = 0;
@@ -741,6 +742,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
+    if (const char* e = getenv("TCI_C128_SH")) c->c128_sh = atoi(e) != 0;
     if (const char* e = getenv("TCI_DENSE_MFMA")) c->dense = std::max(0, std::min(atoi(e), (int)tci::kDenseAll));
     {
         hipDeviceProp_t prop;
@@ -818,6 +820,11 @@ int tci_set_rrlu_shadow(tci_ctx* c, int enabled) {
 }
 
 int tci_rrlu_shadow_bytes(void) { return tci::shadow_elem_bytes(); }
+
+int tci_set_c128_shadow(tci_ctx* c, int enabled) {
+    c->c128_sh = enabled != 0;
+    return TCI_OK;
+}
 
 int tci_set_dense_mfma(tci_ctx* c, int mask) {
     if (!c || mask < 0 || mask > tci::kDenseAll) return TCI_ERR_ARG;
@@ -1033,7 +1040,11 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     const size_t oX = oRow + al(16 * (size_t)std::max(ni, 1));
     const size_t oY = oX + al(16 * (size_t)(tci::kMaxPend * ldx));
     const size_t oS = oY + al(16 * (size_t)(tci::kMaxPend * ldy));
-    const size_t bytes = oS + al(16 * 4 * tci::kMaxPend);
+    // shadow search: |pivot t|, the MFMA fragments (32 halves per row, 64 per column)
+    const size_t oPm = oS + al(16 * 4 * tci::kMaxPend);
+    const size_t oXA = oPm + al(8 * (size_t)(mr + 1));
+    const size_t oYB = oXA + al(64 * (size_t)std::max(mi, 1));
+    const size_t bytes = oYB + al(128 * (size_t)std::max(ni, 1));
     int st;
     if ((st = ensure(c, &c->cws, &c->capCws, bytes))) return st;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
@@ -1061,16 +1072,45 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     g.Y = reinterpret_cast<double2*>(c->cws + oY);
     g.ldy = ldy;
     g.stash = reinterpret_cast<double2*>(c->cws + oS);
+    g.pmod = reinterpret_cast<double*>(c->cws + oPm);
+    g.sh = 0;
+    if (c->c128_nb > 0 && c->c128_sh && m >= 64 && n >= 64) {
+        // certified shadow search (K8): fp16 planes of Re / Im (the Float64 path's shadow buffer,
+        // same size), fragments zeroed, shadow padding rows [m, lds) zeroed
+        g.lds = round_up(m, 16);
+        if ((st = ensure(c, &c->sbuf, &c->capS, (size_t)(g.lds * n)))) return st;
+        g.SR = reinterpret_cast<uint16_t*>(c->sbuf);
+        g.SI = g.SR + g.lds * n;
+        g.XA = reinterpret_cast<uint16_t*>(c->cws + oXA);
+        g.YB = reinterpret_cast<uint16_t*>(c->cws + oYB);
+        HIPCHK(c, hipMemsetAsync(g.XA, 0, oYB - oXA + 128 * (size_t)std::max(ni, 1), c->stream));
+        if (g.lds > m) {
+            HIPCHK(c, hipMemset2DAsync(g.SR + m, (size_t)(2 * g.lds), 0, (size_t)(2 * (g.lds - m)), (size_t)n,
+                                       c->stream));
+            HIPCHK(c, hipMemset2DAsync(g.SI + m, (size_t)(2 * g.lds), 0, (size_t)(2 * (g.lds - m)), (size_t)n,
+                                       c->stream));
+        }
+        g.sh = 1;
+    }
     if (c->c128_nb > 0) {
         // deferred updates (K8): pending pivots t0 .. t-1 applied on the fly, written back when
-        // nb of them pend; steps after the stop test fired return at once (st->done)
+        // nb of them pend; steps after the stop test fired return at once (st->done). With the
+        // shadow search, steps with 1..kCShMaxP pending read the fp16 shadow (step 1 is exact and
+        // writes the shadow of A's stale values)
         const int nb = std::min(c->c128_nb, tci::kMaxPend - 1);
         int t0 = 0;
         for (int t = 0; mr > 0 && t < mr; ++t) {
             g.t = t;
             const int P = t - t0;
             const bool flush = P >= nb;
-            tci::launch_crrlu_step_d(c->stream, g, P, flush);
+            if (g.sh && !flush && P >= 1 && P <= tci::kCShMaxP) {
+                if (t0 == 0 && t == 1)
+                    tci::launch_crrlu_step_stale_sh(c->stream, g);
+                else
+                    tci::launch_crrlu_step_sh(c->stream, g, P);
+            } else {
+                tci::launch_crrlu_step_d(c->stream, g, P, flush);
+            }
             if (flush) t0 = t;
             HIPCHK(c, hipGetLastError());
         }

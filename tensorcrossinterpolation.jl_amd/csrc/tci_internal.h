@@ -146,8 +146,24 @@ struct CStepArgs {
     int64_t ldy;
     int P;
     double2* stash;
+    // certified shadow search (k_crrlu_step_sh): fp16 planes of the stale values'
+    // real / imaginary parts (ld lds, scaled per epoch), the pending x's / y's as f16-split MFMA
+    // fragments (XA: 32 halves per row, YB: 2 x 32 per column) and |pivot t| per pivot
+    uint16_t* SR;
+    uint16_t* SI;
+    int64_t lds;
+    uint16_t* XA;
+    uint16_t* YB;
+    double* pmod;
+    int sh;  // shadow search on: the swaps maintain the shadow and the fragments
 };
 int crrlu_grid(int m, int n, int t);
+// the shadow search's step for pivot t with P pending (1 <= P <= kCShMaxP), then reduce + swap;
+// stale = 1: exact step that also writes the shadow of the stale values (epoch 0)
+constexpr int kCShMaxP = 5;
+void launch_crrlu_step_sh(hipStream_t s, CStepArgs g, int P);
+void launch_crrlu_step_stale_sh(hipStream_t s, CStepArgs g);
+int crrlu_sh_grid(int m, int n, int t);
 // the deferred-update pipeline: step<P, flush> (pending applied on the fly, written back when
 // flush), then reduce + swap with the pending count P' (0 after a flush) of the step
 void launch_crrlu_step_d(hipStream_t s, CStepArgs g, int P, bool flush);

@@ -105,6 +105,62 @@ __device__ inline double2 cmul(double2 x, double2 y) {
     return make_double2(x.x * y.x - x.y * y.y, x.x * y.y + x.y * y.x);
 }
 
+// ------------------------------------------------ shadow search helpers
+constexpr int kCShK = 32;  // split slots per row / column plane: 6 per pending update, P <= 5
+
+__device__ inline uint16_t f16_bits(double v) {
+    const _Float16 h = (_Float16)(float)v;
+    return __builtin_bit_cast(uint16_t, h);
+}
+
+// scale of an epoch whose stale values have modulus <= B: s = 2^(14 - ilogb B), so the real and
+// imaginary parts stay below 2^15 in fp16; 0 (search off) outside [2^-100, 2^100] or not finite
+__device__ inline double c_sh_scale(double B) {
+    if (!(B >= 0x1p-100 && B <= 0x1p100)) return 0.0;
+    return ldexp(1.0, 14 - ilogb(B));
+}
+
+// bound on the stale values' modulus of the epoch whose first pending pivot is t0: A itself
+// (|pivot 0| is its maximum) or the Schur complement after t0 - 1 (a - x y, each <= |pivot t0-1|)
+__device__ inline double c_sh_bound(const double* pm, int t0) {
+    return t0 == 0 ? pm[0] : 2.0 * pm[t0 - 1];
+}
+
+// f16 split of v (v = hi + lo to ~2^-22)
+__device__ inline void c_split(double v, uint16_t& hi, uint16_t& lo) {
+    const _Float16 h = (_Float16)(float)v;
+    const _Float16 l = (_Float16)(float)(v - (double)h);
+    hi = __builtin_bit_cast(uint16_t, h);
+    lo = __builtin_bit_cast(uint16_t, l);
+}
+
+// fragment slots 6 slot .. 6 slot + 5 of pending update `slot`: row side -(x) (scaled unless
+// leftorth) as (xr_h, xr_h, xr_l, xi_h, xi_h, xi_l); column side y (scaled if leftorth) as
+// re-plane (yr_h, yr_l, yr_h, -yi_h, -yi_l, -yi_h) and im-plane (yi_h, yi_l, yi_h, yr_h, yr_l, yr_h):
+// sum over the slots of A * B_re = Re(-x y), A * B_im = Im(-x y)
+__device__ inline void c_frag_x(uint16_t* XA, int r, int slot, double2 x, double s, int leftorth) {
+    if (slot >= kCShK / 6) return;
+    const double xr = -(leftorth ? x.x : x.x * s), xi = -(leftorth ? x.y : x.y * s);
+    uint16_t rh, rl, ih, il;
+    c_split(xr, rh, rl);
+    c_split(xi, ih, il);
+    uint16_t* d = XA + (int64_t)r * kCShK + 6 * slot;
+    d[0] = rh; d[1] = rh; d[2] = rl; d[3] = ih; d[4] = ih; d[5] = il;
+}
+
+__device__ inline void c_frag_y(uint16_t* YB, int c, int slot, double2 y, double s, int leftorth) {
+    if (slot >= kCShK / 6) return;
+    const double yr = leftorth ? y.x * s : y.x, yi = leftorth ? y.y * s : y.y;
+    uint16_t rh, rl, ih, il, nih, nil;
+    c_split(yr, rh, rl);
+    c_split(yi, ih, il);
+    c_split(-yi, nih, nil);
+    uint16_t* d = YB + (int64_t)c * 2 * kCShK + 6 * slot;
+    d[0] = rh; d[1] = rl; d[2] = rh; d[3] = nih; d[4] = nil; d[5] = nih;
+    d += kCShK;
+    d[0] = ih; d[1] = il; d[2] = ih; d[3] = rh; d[4] = rl; d[5] = rh;
+}
+
 __device__ inline CCand shfl_cand(const CCand& c, int mask) {
     CCand o;
     o.v = __shfl_xor(c.v, mask);
@@ -554,7 +610,10 @@ __global__ __launch_bounds__(256) void k_ctt_eval(const double2* __restrict__ co
 // entries of the two rows / columns with them. It also finalises pivot t's column and row
 // (stale values minus the pending updates, normalised) into A -- the L / U storage of the
 // reference -- and into pending slot P.
-template <int P, bool FLUSH>
+// SHW (shadow search): 1 = a write-back that also writes the fp16 shadow of the new stale values
+// and clears the MFMA fragments of the epoch it starts; 2 = step 1, which writes the shadow of A's
+// stale values (epoch 0: its scale needs |pivot 0|)
+template <int P, bool FLUSH, int SHW = 0>
 __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
     __shared__ double2 ys[(P > 0 ? P : 1) * kCTC];
     __shared__ CCand red[kCThreads / 64];
@@ -568,6 +627,17 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
     double2* A = g.A;
     const int64_t ld = g.ld;
     const int i = r0 + lane;
+    [[maybe_unused]] double shs = 0.0;
+    if constexpr (SHW != 0) {
+        shs = c_sh_scale(SHW == 1 ? 2.0 * g.pmod[t - 1] : g.pmod[0]);
+        if (SHW == 1) {  // fragments of the epoch starting here: every slot zero
+            const int e = threadIdx.x;
+            if (tc == 0 && r0 + e / 4 < g.m)
+                reinterpret_cast<uint4*>(g.XA + (int64_t)(r0 + e / 4) * kCShK)[e % 4] = uint4{0, 0, 0, 0};
+            if (tr == 0 && c0 + e / 8 < g.n)
+                reinterpret_cast<uint4*>(g.YB + (int64_t)(c0 + e / 8) * 2 * kCShK)[e % 8] = uint4{0, 0, 0, 0};
+        }
+    }
     double2 xr[P > 0 ? P : 1];
     if constexpr (P > 0) {
         for (int e = threadIdx.x; e < P * kCTC; e += kCThreads) {
@@ -587,6 +657,10 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
             if (j >= g.n) break;
             double2* pa = A + i + (int64_t)j * ld;
             double2 a = *pa;
+            if constexpr (SHW == 2) {
+                g.SR[i + (int64_t)j * g.lds] = f16_bits(a.x * shs);
+                g.SI[i + (int64_t)j * g.lds] = f16_bits(a.y * shs);
+            }
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 const double2 z = cmul(xr[s], ys[s * kCTC + jl]);
@@ -594,6 +668,10 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
                 a.y = a.y - z.y;
             }
             if constexpr (FLUSH) *pa = a;
+            if constexpr (SHW == 1) {
+                g.SR[i + (int64_t)j * g.lds] = f16_bits(a.x * shs);
+                g.SI[i + (int64_t)j * g.lds] = f16_bits(a.y * shs);
+            }
             const double v = a.x * a.x + a.y * a.y;
             if (v > best.v) best = CCand{v, j, i};  // columns ascend: strict '>' keeps the first
         }
@@ -650,6 +728,7 @@ __global__ __launch_bounds__(kRThreads) void k_crrlu_reduce_d(CStepArgs g, int n
         if ((err < g.reltol * st->maxerror || err < g.abstol) && t > 0) {
             st->done = 1;
         } else {
+            if (g.pmod) g.pmod[t] = err;
             st->maxerror = jl_maxd(st->maxerror, err);
             st->np = t + 1;
             st->p = p;
@@ -677,6 +756,8 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
     const double2* sYt = g.stash + 2 * kMaxPend;  // Y[s][t]
     const double2* sYq = g.stash + 3 * kMaxPend;  // Y[s][q]
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    // shadow search: the epoch's scale for the fragments of the new pending slot P (pivot t)
+    const double fs = g.sh ? c_sh_scale(c_sh_bound(g.pmod, t - P)) : 0.0;
     if (e < g.n) {  // column j: rows t <-> p
         const int j = e;
         if (j == t || j == q) return;
@@ -696,6 +777,13 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
             if (!g.leftorth) y = jl_cdiv(y, piv);  // A[k, k+1:end] ./= A[k, k]
             *pt = y;
             g.Y[(int64_t)P * g.ldy + j] = y;
+            if (g.sh) {
+                c_frag_y(g.YB, j, P, y, fs, g.leftorth);
+                if (p != t) {  // the shadow's row p takes old row t (column q: the corner)
+                    g.SR[p + (int64_t)j * g.lds] = g.SR[t + (int64_t)j * g.lds];
+                    g.SI[p + (int64_t)j * g.lds] = g.SI[t + (int64_t)j * g.lds];
+                }
+            }
         }
     } else if (e < g.n + g.m) {  // row r: columns t <-> q
         const int r = e - g.n;
@@ -716,6 +804,13 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
             if (g.leftorth) x = jl_cdiv(x, piv);  // A[k+1:end, k] ./= A[k, k]
             *pt = x;
             g.X[(int64_t)P * g.ldx + r] = x;
+            if (g.sh) {
+                c_frag_x(g.XA, r, P, x, fs, g.leftorth);
+                if (q != t) {  // the shadow's column q takes old column t
+                    g.SR[r + (int64_t)q * g.lds] = g.SR[r + (int64_t)t * g.lds];
+                    g.SI[r + (int64_t)q * g.lds] = g.SI[r + (int64_t)t * g.lds];
+                }
+            }
         }
     } else if (e == g.n + g.m) {
         // new[a, b] = old[sr(a), sc(b)] on {t, p} x {t, q}, all read before any store
@@ -752,13 +847,275 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
             g.Y[(int64_t)s * g.ldy + t] = sYq[s];
             g.Y[(int64_t)s * g.ldy + q] = sYt[s];
         }
+        if (g.sh) {
+            // shadow corner (p, q) = old (t, t); the fragments of rows t / p and columns t / q
+            // follow them like the slots, then pivot t's own entries of row p / column q
+            if (p != t && q != t) {
+                g.SR[p + (int64_t)q * g.lds] = g.SR[t + (int64_t)t * g.lds];
+                g.SI[p + (int64_t)q * g.lds] = g.SI[t + (int64_t)t * g.lds];
+            }
+            if (p != t) {
+                uint4* ft = reinterpret_cast<uint4*>(g.XA + (int64_t)t * kCShK);
+                uint4* fp = reinterpret_cast<uint4*>(g.XA + (int64_t)p * kCShK);
+                for (int z = 0; z < kCShK / 8; ++z) {
+                    const uint4 u = ft[z];
+                    ft[z] = fp[z];
+                    fp[z] = u;
+                }
+                c_frag_x(g.XA, p, P, A[p + (int64_t)t * ld], fs, g.leftorth);
+            }
+            if (q != t) {
+                uint4* ft = reinterpret_cast<uint4*>(g.YB + (int64_t)t * 2 * kCShK);
+                uint4* fq = reinterpret_cast<uint4*>(g.YB + (int64_t)q * 2 * kCShK);
+                for (int z = 0; z < 2 * kCShK / 8; ++z) {
+                    const uint4 u = ft[z];
+                    ft[z] = fq[z];
+                    fq[z] = u;
+                }
+                c_frag_y(g.YB, q, P, A[t + (int64_t)q * ld], fs, g.leftorth);
+            }
+        }
     }
 }
 
+
+// ------------------------------------------------ certified shadow search
+// Read-only step t with P pending updates (1 <= P <= 5): instead of the 16-B complex values it
+// streams the fp16 planes of their real and imaginary parts (4 B/element) and applies the
+// pending updates on the matrix cores: per 16 x 16 tile two v_mfma_f32_16x16x32_f16 with the
+// same A fragment (the rows' -x splits) and the columns' B fragments of Re and Im (6 slots per
+// update, see c_frag_x / c_frag_y), C = the converted shadow tiles. With |v| <= Mf (the epoch's
+// stale bound) every part of W is within epsc of s * v, the fp32 modulus within epsm of s |v|:
+//   fp16 storage 2^-11 (1 + 2^-9) s Mf + 2^-25, splits 2^-18 s sumM + 2P 2^-24,
+//   fp32 accumulation (6P + 4) 2^-23 s (Mf + 2 sumM);  epsm = sqrt(2) epsc + 2^-21 s mag.
+// Blocks (4 rows x 1 column) whose approximate maximum can reach the workgroup's lower bound are
+// re-read in fp64 and examined exactly (the reference's operations and tie order), deferred to a
+// per-wave list and pruned against the latest bound. Rows and columns before t (the L / U part
+// of the physically swapped matrix) are masked by position. Workgroup: 64 rows x 512 columns,
+// 4 waves taking 16-column chunks.
+constexpr int kCSRows = 64, kCSCols = 512, kCSThreads = 256, kCSExCap = 64;
+typedef _Float16 ch8 __attribute__((ext_vector_type(8)));
+typedef float cf4 __attribute__((ext_vector_type(4)));
+
+template <int P>
+__global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
+    static_assert(P >= 1 && P <= kCShMaxP, "6P split slots in one K = 32 MFMA");
+    __shared__ unsigned tau_s;
+    __shared__ unsigned exl[kCSThreads / 64 * kCSExCap];
+    __shared__ float exm[kCSThreads / 64 * kCSExCap];
+    __shared__ CCand red[kCSThreads / 64];
+    CState* st = g.st;
+    if (st->done) return;
+    const int t = g.t, m = g.m, n = g.n, t0 = t - P;
+    const double* pm = g.pmod;
+    const double shs = c_sh_scale(c_sh_bound(pm, t0));
+    const double Mf = pm[t0];
+    double sumM = 0.0, maxM = 0.0;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+        sumM += pm[t0 + s];
+        maxM = fmax(maxM, pm[t0 + s]);
+    }
+    const double mag = Mf + 2.0 * sumM;
+    const double epsc = 0x1p-11 * (1.0 + 0x1p-9) * Mf * shs + 0x1p-25 + 0x1p-18 * sumM * shs +
+                        2.0 * P * 0x1p-24 + (6.0 * P + 4.0) * 0x1p-23 * mag * shs;
+    const double epsd = 1.4142135623730951 * (1.0 + 0x1p-20) * epsc + 0x1p-21 * mag * shs;
+    const bool shok = shs > 0.0 && mag < 0x1p100 && maxM * shs <= 0x1p15 &&
+                      epsd < ldexp(pm[t - 1] * shs, -7);
+    const int rb0 = t & ~15, cb0 = t & ~15;
+    const int ntr = (m - rb0 + kCSRows - 1) / kCSRows;
+    const int tr = blockIdx.x % ntr, tcw = blockIdx.x / ntr;
+    const int r0 = rb0 + tr * kCSRows, c0 = cb0 + tcw * kCSCols;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double2* A = g.A;
+    const int64_t ld = g.ld;
+    CCand best{-INFINITY, INT32_MAX, INT32_MAX};
+    // exact value of element (i, j): the stale value minus the pending updates in pivot order
+    auto exact = [&](int i, int j) {
+        double2 a = A[i + (int64_t)j * ld];
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            const double2 z = cmul(g.X[(int64_t)s * g.ldx + i], g.Y[(int64_t)s * g.ldy + j]);
+            a.x = a.x - z.x;
+            a.y = a.y - z.y;
+        }
+        const CCand c{a.x * a.x + a.y * a.y, j, i};
+        if (cbetter(c, best)) best = c;
+    };
+    if (!shok) {
+        // the bound is not tight (decaying pivots) or fp16 could overflow: every element exactly
+        for (int e = threadIdx.x; e < kCSRows * kCSCols; e += kCSThreads) {
+            const int i = r0 + (e & (kCSRows - 1)), j = c0 + e / kCSRows;
+            if (i >= t && i < m && j >= t && j < n) exact(i, j);
+        }
+    } else {
+        const float eps = (float)(epsd * (1.0 + 0x1p-20));
+        const float margin = 0x1p-20f;
+        const int gq = lane >> 4, lcol = lane & 15;
+        const int rl = r0 + 16 * gq;  // the lane's 16 loaded rows
+        const bool rload = rl < g.lds;
+        const bool rmask = __any(rl < t);  // the wave holds rows before t: masked per element
+        ch8 af[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int rho = r0 + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
+            af[b] = rho < m ? *reinterpret_cast<const ch8*>(g.XA + (int64_t)rho * kCShK + 8 * gq) : ch8{};
+        }
+        const _Float16* SR = reinterpret_cast<const _Float16*>(g.SR);
+        const _Float16* SI = reinterpret_cast<const _Float16*>(g.SI);
+        const int nch = kCSCols / 16;
+        auto load = [&](int h, ch8 (&vr)[2], ch8 (&vi)[2]) {
+            const int j = c0 + 16 * h + lcol;
+            if (rload && j < n) {
+                const ch8* pr = reinterpret_cast<const ch8*>(SR + rl + (int64_t)j * g.lds);
+                const ch8* pi = reinterpret_cast<const ch8*>(SI + rl + (int64_t)j * g.lds);
+                vr[0] = pr[0];
+                vr[1] = pr[1];
+                vi[0] = pi[0];
+                vi[1] = pi[1];
+            } else {
+                vr[0] = vr[1] = vi[0] = vi[1] = ch8{};
+            }
+        };
+        // chunk h: the lane's column's maximum modulus over its 16 rows, per 4-row block
+        auto approx = [&](int h, const ch8 (&vr)[2], const ch8 (&vi)[2], float (&mbs)[4]) -> float {
+            const int j = c0 + 16 * h + lcol;
+            const bool jok = j >= t && j < n;
+            const int jj = j < n ? j : 0;
+            const ch8 bre = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + 8 * gq);
+            const ch8 bim = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + kCShK + 8 * gq);
+            float c = 0.0f;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int o = 4 * (b & 1);
+                const ch8& hr = vr[b >> 1];
+                const ch8& hi = vi[b >> 1];
+                cf4 dr = {(float)hr[o], (float)hr[o + 1], (float)hr[o + 2], (float)hr[o + 3]};
+                cf4 di = {(float)hi[o], (float)hi[o + 1], (float)hi[o + 2], (float)hi[o + 3]};
+                dr = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bre, dr, 0, 0, 0);
+                di = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bim, di, 0, 0, 0);
+                float q2[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) q2[e] = dr[e] * dr[e] + di[e] * di[e];
+                if (rmask) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (rl + 4 * b + e < t) q2[e] = 0.0f;
+                }
+                mbs[b] = sqrtf(__builtin_fmaxf(__builtin_fmaxf(q2[0], q2[1]), __builtin_fmaxf(q2[2], q2[3])));
+                c = __builtin_fmaxf(c, mbs[b]);
+            }
+            if (!jok) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) mbs[b] = -1.0f;
+                c = -1.0f;
+            }
+            return c;
+        };
+        float tau = 0.0f;
+        unsigned* const wl = exl + wave * kCSExCap;
+        float* const wm = exm + wave * kCSExCap;
+        int nex = 0;
+        auto flush = [&]() {
+            const float thr = tau - tau * margin;
+            for (int e = lane; e < 4 * nex; e += 64) {
+                if (wm[e >> 2] + eps < thr) continue;
+                const unsigned key = wl[e >> 2];
+                const int j = (int)(key & 0xffffffu) , i = (int)(key >> 24) * 4 + (e & 3) + r0;
+                if (i >= t && i < m) exact(i, j);
+            }
+            nex = 0;
+        };
+        auto append = [&](int h, const float (&mbs)[4], float bound) {
+            const int j = c0 + 16 * h + lcol;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const bool f = mbs[b] >= 0.0f && mbs[b] + eps >= bound;
+                const uint64_t bal = __ballot(f);
+                if (bal == 0) continue;
+                const int cnt = __popcll(bal);
+                if (nex + cnt > kCSExCap) flush();
+                if (f) {
+                    const int at = nex + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                    wl[at] = (unsigned)j | (unsigned)(4 * gq + b) << 24;
+                    wm[at] = mbs[b];
+                }
+                nex += cnt;
+            }
+        };
+        auto test = [&](float c) {
+            if (c < 0.0f) return;
+            const float lb = fmaxf(c - eps, 0.0f);
+            const float ts = __uint_as_float(__hip_atomic_load(&tau_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            tau = fmaxf(tau, ts);
+            if (lb > tau) {
+                tau = lb;
+                atomicMax(&tau_s, __float_as_uint(lb));
+            }
+        };
+        if (threadIdx.x == 0) tau_s = 0u;
+        ch8 ar[2], ai[2], br[2], bi[2];
+        float mb0[4], mb1[4];
+        int h0 = wave, h1 = wave + 4;
+        load(h0, ar, ai);
+        load(h1, br, bi);
+        __syncthreads();
+        // seed: every wave's first chunk sets the workgroup's bound before anything is listed
+        const float cs = approx(h0, ar, ai, mb0);
+        {
+            float lb = fmaxf(cs - eps, 0.0f);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) lb = fmaxf(lb, __shfl_xor(lb, off));
+            if (lane == 0) atomicMax(&tau_s, __float_as_uint(lb));
+        }
+        h0 += 8;
+        if (h0 < nch) load(h0, ar, ai);
+        __syncthreads();
+        tau = __uint_as_float(tau_s);
+        append(h0 - 8, mb0, tau - tau * margin);
+        for (;;) {
+            if (h1 >= nch) break;
+            {
+                const float c = approx(h1, br, bi, mb1);
+                const int e = h1;
+                h1 += 8;
+                if (h1 < nch) load(h1, br, bi);
+                test(c);
+                append(e, mb1, tau - tau * margin);
+            }
+            if (h0 >= nch) break;
+            {
+                const float c = approx(h0, ar, ai, mb0);
+                const int e = h0;
+                h0 += 8;
+                if (h0 < nch) load(h0, ar, ai);
+                test(c);
+                append(e, mb0, tau - tau * margin);
+            }
+        }
+        tau = fmaxf(tau, __uint_as_float(__hip_atomic_load(&tau_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+        flush();
+    }
+    best = block_reduce<kCSThreads>(best, red);
+    if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
+}
+
+
 template <int P>
 static void crrlu_step_p(hipStream_t s, const CStepArgs& g, bool flush, int grid) {
-    if (flush) hipLaunchKernelGGL((k_crrlu_step_d<P, true>), dim3(grid), dim3(kCThreads), 0, s, g);
-    else hipLaunchKernelGGL((k_crrlu_step_d<P, false>), dim3(grid), dim3(kCThreads), 0, s, g);
+    if (flush && g.sh && P > 0)
+        hipLaunchKernelGGL((k_crrlu_step_d<P, true, 1>), dim3(grid), dim3(kCThreads), 0, s, g);
+    else if (flush)
+        hipLaunchKernelGGL((k_crrlu_step_d<P, true>), dim3(grid), dim3(kCThreads), 0, s, g);
+    else
+        hipLaunchKernelGGL((k_crrlu_step_d<P, false>), dim3(grid), dim3(kCThreads), 0, s, g);
+}
+
+template <int P>
+static void crrlu_step_sh_p(hipStream_t s, const CStepArgs& g, int grid) {
+    if constexpr (P >= 1 && P <= kCShMaxP)
+        hipLaunchKernelGGL((k_crrlu_step_sh<P>), dim3(grid), dim3(kCSThreads), 0, s, g);
 }
 
 }  // namespace
@@ -799,6 +1156,40 @@ void launch_crrlu_step_d(hipStream_t s, CStepArgs g, int P, bool flush) {
     default: break;
     }
     g.P = flush ? 0 : P;
+    hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, grid);
+    hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
+}
+
+int crrlu_sh_grid(int m, int n, int t) {
+    const int rb0 = t & ~15;
+    const int ntr = m - rb0 > 0 ? (m - rb0 + kCSRows - 1) / kCSRows : 1;
+    const int ntc = n - rb0 > 0 ? (n - rb0 + kCSCols - 1) / kCSCols : 1;
+    return ntr * ntc;
+}
+
+// shadow-search step for pivot t (P pending, 1..kCShMaxP), then reduce + swap (pending P after)
+void launch_crrlu_step_sh(hipStream_t s, CStepArgs g, int P) {
+    const int grid = crrlu_sh_grid(g.m, g.n, g.t);
+    switch (P) {
+        case 1: crrlu_step_sh_p<1>(s, g, grid); break;
+        case 2: crrlu_step_sh_p<2>(s, g, grid); break;
+        case 3: crrlu_step_sh_p<3>(s, g, grid); break;
+        case 4: crrlu_step_sh_p<4>(s, g, grid); break;
+        case 5: crrlu_step_sh_p<5>(s, g, grid); break;
+        default: return;
+    }
+    g.P = P;
+    hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, grid);
+    hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
+}
+
+// step 1 of the shadow search: exact (one pending update), and it writes the shadow of the stale
+// values with epoch 0's scale (|pivot 0|, known since step 0)
+void launch_crrlu_step_stale_sh(hipStream_t s, CStepArgs g) {
+    g.tiles_r = g.m - g.t > 0 ? (g.m - g.t + kCTR - 1) / kCTR : 1;
+    const int grid = crrlu_grid(g.m, g.n, g.t);
+    hipLaunchKernelGGL((k_crrlu_step_d<1, false, 2>), dim3(grid), dim3(kCThreads), 0, s, g);
+    g.P = 1;
     hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, grid);
     hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
 }

@@ -57,6 +57,7 @@ SIGNATURES = {
     "tci_set_rrlu_mid": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_shadow": ([vp, C.c_int], C.c_int),
     "tci_rrlu_shadow_bytes": ([], C.c_int),
+    "tci_set_c128_shadow": ([vp, C.c_int], C.c_int),
     "tci_set_dense_mfma": ([vp, C.c_int], C.c_int),
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),

@@ -68,6 +68,33 @@ def test_crrlu_lorentz_ties_bitwise(ctx, leftorth):
         assert_c_bitwise(lu, ref)
 
 
+@pytest.mark.parametrize("shadow", [1, 0])
+@pytest.mark.parametrize("leftorth", [True, False])
+def test_crrlu_shadow_search_bitwise(ctx, shadow, leftorth):
+    """Sizes the certified shadow search runs on (>= 64 x 64), both settings: ties of a complex
+    Lorentzian over 9^2 legs, a rapidly decaying (numerically low-rank) block, NaN-free random
+    matrices through two write-back epochs, and an odd row count (shadow padding rows)."""
+    ctx.check(ctx.lib.tci_set_c128_shadow(ctx.h, shadow))
+    try:
+        d = 9
+        I = np.array(list(np.ndindex(d, d))) + 1
+        s = (I ** 2).sum(1)[:, None] + (I ** 2).sum(1)[None, :]
+        cases = [((0.5 - 1.0j) / (s + 1.0), {"maxrank": 30})]
+        rng = np.random.default_rng(5)
+        U, _ = np.linalg.qr(crand(rng, 160, 160))
+        V, _ = np.linalg.qr(crand(rng, 150, 150))
+        sv = 2.0 ** -np.arange(150, dtype=float)
+        cases.append(((U[:, :150] * sv) @ V.conj().T, {"maxrank": 60, "reltol": 0.0}))
+        cases.append((crand(rng, 333, 290), {"maxrank": 40}))
+        cases.append((crand(rng, 517, 700) * 1e-30, {"maxrank": 25}))
+        for A, kw in cases:
+            lu = T.rrlu(A, leftorthogonal=leftorth, ctx=ctx, **kw)
+            ref = O.OracleLUc(A, leftorthogonal=leftorth, **kw)
+            assert_c_bitwise(lu, ref)
+    finally:
+        ctx.check(ctx.lib.tci_set_c128_shadow(ctx.h, 1))
+
+
 def test_crrlu_rank_deficient_and_abstol(ctx):
     rng = np.random.default_rng(3)
     B = crand(rng, 120, 4) @ crand(rng, 4, 90)
