@@ -1,6 +1,6 @@
 """ComplexF64 rrLU on device matrices with the certified shadow search on and off:
 time per factorisation and equality of the pivots / pivot errors between the two settings at the
-benchmarked sizes. python scripts/crrlu_shadow_ab.py"""
+benchmarked sizes. python scripts/crrlu_shadow_ab.py [m,n,r ...]"""
 import ctypes as C
 import os
 import sys
@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "tensorcrossinterpolation.jl_amd"))
 import tci_amd as T  # noqa: E402
 
 ctx = T.Context(0)
-for m, n, r in ((4096, 4096, 256), (8192, 8192, 256)):
+sizes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or [(4096, 4096, 256), (8192, 8192, 256)]
+for m, n, r in sizes:
     A = T.DeviceMatrix(2 * m, n, ctx=ctx)
     A.fill_uniform(seed=0)
     W = T.DeviceMatrix(2 * m, n, ctx=ctx)

@@ -48,7 +48,8 @@ struct tci_ctx {
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
-    int c128_nb = 6;             // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1)
+    int c128_nb = -1;            // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1;
+                                 // -1: 11 with the shadow search, 6 without -- measured best)
     int c128_sh = 1;             // ComplexF64 rrLU certified shadow search (env TCI_C128_SH)
     int ncu = 0;           // compute units of the device
     double* colbuf = nullptr;  // mid path: published candidate columns
@@ -1040,11 +1041,11 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     const size_t oX = oRow + al(16 * (size_t)std::max(ni, 1));
     const size_t oY = oX + al(16 * (size_t)(tci::kMaxPend * ldx));
     const size_t oS = oY + al(16 * (size_t)(tci::kMaxPend * ldy));
-    // shadow search: |pivot t|, the MFMA fragments (32 halves per row, 64 per column)
+    // shadow search: |pivot t|, the MFMA fragments (64 halves per row, 128 per column)
     const size_t oPm = oS + al(16 * 4 * tci::kMaxPend);
     const size_t oXA = oPm + al(8 * (size_t)(mr + 1));
-    const size_t oYB = oXA + al(64 * (size_t)std::max(mi, 1));
-    const size_t bytes = oYB + al(128 * (size_t)std::max(ni, 1));
+    const size_t oYB = oXA + al(128 * (size_t)std::max(mi, 1));
+    const size_t bytes = oYB + al(256 * (size_t)std::max(ni, 1));
     int st;
     if ((st = ensure(c, &c->cws, &c->capCws, bytes))) return st;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
@@ -1074,7 +1075,7 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
     g.stash = reinterpret_cast<double2*>(c->cws + oS);
     g.pmod = reinterpret_cast<double*>(c->cws + oPm);
     g.sh = 0;
-    if (c->c128_nb > 0 && c->c128_sh && m >= 64 && n >= 64) {
+    if (c->c128_nb != 0 && c->c128_sh && m >= 64 && n >= 64) {
         // certified shadow search (K8): fp16 planes of Re / Im (the Float64 path's shadow buffer,
         // same size), fragments zeroed, shadow padding rows [m, lds) zeroed
         g.lds = round_up(m, 16);
@@ -1083,7 +1084,7 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
         g.SI = g.SR + g.lds * n;
         g.XA = reinterpret_cast<uint16_t*>(c->cws + oXA);
         g.YB = reinterpret_cast<uint16_t*>(c->cws + oYB);
-        HIPCHK(c, hipMemsetAsync(g.XA, 0, oYB - oXA + 128 * (size_t)std::max(ni, 1), c->stream));
+        HIPCHK(c, hipMemsetAsync(g.XA, 0, oYB - oXA + 256 * (size_t)std::max(ni, 1), c->stream));
         if (g.lds > m) {
             HIPCHK(c, hipMemset2DAsync(g.SR + m, (size_t)(2 * g.lds), 0, (size_t)(2 * (g.lds - m)), (size_t)n,
                                        c->stream));
@@ -1092,12 +1093,12 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
         }
         g.sh = 1;
     }
-    if (c->c128_nb > 0) {
+    if (c->c128_nb != 0) {
         // deferred updates (K8): pending pivots t0 .. t-1 applied on the fly, written back when
         // nb of them pend; steps after the stop test fired return at once (st->done). With the
         // shadow search, steps with 1..kCShMaxP pending read the fp16 shadow (step 1 is exact and
         // writes the shadow of A's stale values)
-        const int nb = std::min(c->c128_nb, tci::kMaxPend - 1);
+        const int nb = std::min(c->c128_nb > 0 ? c->c128_nb : (g.sh ? 11 : 6), tci::kMaxPend - 1);
         int t0 = 0;
         for (int t = 0; mr > 0 && t < mr; ++t) {
             g.t = t;
@@ -1106,6 +1107,8 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
             if (g.sh && !flush && P >= 1 && P <= tci::kCShMaxP) {
                 if (t0 == 0 && t == 1)
                     tci::launch_crrlu_step_stale_sh(c->stream, g);
+                else if (getenv("TCI_CSH_CHECK"))
+                    tci::debug_crrlu_check_sh(c->stream, g, P);
                 else
                     tci::launch_crrlu_step_sh(c->stream, g, P);
             } else {

@@ -148,7 +148,7 @@ struct CStepArgs {
     double2* stash;
     // certified shadow search (k_crrlu_step_sh): fp16 planes of the stale values'
     // real / imaginary parts (ld lds, scaled per epoch), the pending x's / y's as f16-split MFMA
-    // fragments (XA: 32 halves per row, YB: 2 x 32 per column) and |pivot t| per pivot
+    // fragments (XA: 64 halves per row, YB: 2 x 64 per column) and |pivot t| per pivot
     uint16_t* SR;
     uint16_t* SI;
     int64_t lds;
@@ -160,9 +160,10 @@ struct CStepArgs {
 int crrlu_grid(int m, int n, int t);
 // the shadow search's step for pivot t with P pending (1 <= P <= kCShMaxP), then reduce + swap;
 // stale = 1: exact step that also writes the shadow of the stale values (epoch 0)
-constexpr int kCShMaxP = 5;
+constexpr int kCShMaxP = 10;
 void launch_crrlu_step_sh(hipStream_t s, CStepArgs g, int P);
 void launch_crrlu_step_stale_sh(hipStream_t s, CStepArgs g);
+void debug_crrlu_check_sh(hipStream_t s, CStepArgs g, int P);
 int crrlu_sh_grid(int m, int n, int t);
 // the deferred-update pipeline: step<P, flush> (pending applied on the fly, written back when
 // flush), then reduce + swap with the pending count P' (0 after a flush) of the step

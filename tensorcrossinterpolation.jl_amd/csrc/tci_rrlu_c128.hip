@@ -22,6 +22,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
+
+#include <type_traits>
 
 #include "tci_internal.h"
 
@@ -106,7 +109,7 @@ __device__ inline double2 cmul(double2 x, double2 y) {
 }
 
 // ------------------------------------------------ shadow search helpers
-constexpr int kCShK = 32;  // split slots per row / column plane: 6 per pending update, P <= 5
+constexpr int kCShK = 64;  // split slots per row / column plane: 6 per pending update, P <= 10
 
 __device__ inline uint16_t f16_bits(double v) {
     const _Float16 h = (_Float16)(float)v;
@@ -631,11 +634,13 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
     if constexpr (SHW != 0) {
         shs = c_sh_scale(SHW == 1 ? 2.0 * g.pmod[t - 1] : g.pmod[0]);
         if (SHW == 1) {  // fragments of the epoch starting here: every slot zero
-            const int e = threadIdx.x;
-            if (tc == 0 && r0 + e / 4 < g.m)
-                reinterpret_cast<uint4*>(g.XA + (int64_t)(r0 + e / 4) * kCShK)[e % 4] = uint4{0, 0, 0, 0};
-            if (tr == 0 && c0 + e / 8 < g.n)
-                reinterpret_cast<uint4*>(g.YB + (int64_t)(c0 + e / 8) * 2 * kCShK)[e % 8] = uint4{0, 0, 0, 0};
+            constexpr int RQ = kCShK / 8, CQ = 2 * kCShK / 8;  // 16-B stores per row / column
+            for (int e = threadIdx.x; e < kCTR * RQ; e += kCThreads)
+                if (tc == 0 && r0 + e / RQ < g.m)
+                    reinterpret_cast<uint4*>(g.XA + (int64_t)(r0 + e / RQ) * kCShK)[e % RQ] = uint4{0, 0, 0, 0};
+            for (int e = threadIdx.x; e < kCTC * CQ; e += kCThreads)
+                if (tr == 0 && c0 + e / CQ < g.n)
+                    reinterpret_cast<uint4*>(g.YB + (int64_t)(c0 + e / CQ) * 2 * kCShK)[e % CQ] = uint4{0, 0, 0, 0};
         }
     }
     double2 xr[P > 0 ? P : 1];
@@ -680,13 +685,67 @@ __global__ __launch_bounds__(kCThreads) void k_crrlu_step_d(CStepArgs g) {
     if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
 }
 
-// value of stale element (r, c) with the P pending updates applied, in pivot order
+// value of stale element (r, c) with the P pending updates applied, in pivot order (all the
+// slots' loads in flight at once, then the chain: P is a runtime count here)
 __device__ inline double2 cpend(double2 a, const double2* X, int64_t ldx, int r, const double2* Y,
                                 int64_t ldy, int c, int P) {
-    for (int s = 0; s < P; ++s) {
-        const double2 z = cmul(X[(int64_t)s * ldx + r], Y[(int64_t)s * ldy + c]);
-        a.x = a.x - z.x;
-        a.y = a.y - z.y;
+    double2 xv[kMaxPend], yv[kMaxPend];
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            xv[s] = X[(int64_t)s * ldx + r];
+            yv[s] = Y[(int64_t)s * ldy + c];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            const double2 z = cmul(xv[s], yv[s]);
+            a.x = a.x - z.x;
+            a.y = a.y - z.y;
+        }
+    }
+    return a;
+}
+
+// a - sum_s x_s * ys[s * ld], x_s from a short array (the stash), same order and rounding
+__device__ inline double2 cpend_xs(double2 a, const double2* xs, const double2* Y, int64_t ldy, int c, int P) {
+    double2 xv[kMaxPend], yv[kMaxPend];
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            xv[s] = xs[s];
+            yv[s] = Y[(int64_t)s * ldy + c];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            const double2 z = cmul(xv[s], yv[s]);
+            a.x = a.x - z.x;
+            a.y = a.y - z.y;
+        }
+    }
+    return a;
+}
+
+// a - sum_s X[s * ldx + r] * ys_s, the y's from a short array
+__device__ inline double2 cpend_ys(double2 a, const double2* X, int64_t ldx, int r, const double2* ys, int P) {
+    double2 xv[kMaxPend], yv[kMaxPend];
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            xv[s] = X[(int64_t)s * ldx + r];
+            yv[s] = ys[s];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxPend; ++s) {
+        if (s < P) {
+            const double2 z = cmul(xv[s], yv[s]);
+            a.x = a.x - z.x;
+            a.y = a.y - z.y;
+        }
     }
     return a;
 }
@@ -768,12 +827,7 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
         if (j < t) {
             *pt = ap;  // the L part: final values
         } else {  // U row t: the new row t is old row p, pending updates with old row p's x's
-            double2 y = ap;
-            for (int s = 0; s < P; ++s) {
-                const double2 z = cmul(sXp[s], g.Y[(int64_t)s * g.ldy + j]);
-                y.x = y.x - z.x;
-                y.y = y.y - z.y;
-            }
+            double2 y = cpend_xs(ap, sXp, g.Y, g.ldy, j, P);
             if (!g.leftorth) y = jl_cdiv(y, piv);  // A[k, k+1:end] ./= A[k, k]
             *pt = y;
             g.Y[(int64_t)P * g.ldy + j] = y;
@@ -795,12 +849,7 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
         if (r < t) {
             *pt = aq;  // the U part
         } else {
-            double2 x = aq;
-            for (int s = 0; s < P; ++s) {
-                const double2 z = cmul(g.X[(int64_t)s * g.ldx + r], sYq[s]);
-                x.x = x.x - z.x;
-                x.y = x.y - z.y;
-            }
+            double2 x = cpend_ys(aq, g.X, g.ldx, r, sYq, P);
             if (g.leftorth) x = jl_cdiv(x, piv);  // A[k+1:end, k] ./= A[k, k]
             *pt = x;
             g.X[(int64_t)P * g.ldx + r] = x;
@@ -893,14 +942,39 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
 // per-wave list and pruned against the latest bound. Rows and columns before t (the L / U part
 // of the physically swapped matrix) are masked by position. Workgroup: 64 rows x 512 columns,
 // 4 waves taking 16-column chunks.
-constexpr int kCSRows = 64, kCSCols = 512, kCSThreads = 256, kCSExCap = 64;
+// Geometry (the Float64 k_pass_mf's): one 1024-thread workgroup per CU owns a 512-row tile
+// (8 slices of 64 rows, 2 waves per slice; the A fragments of a wave's slice stay in registers)
+// and the 16-column chunks q, q + nq, ... of the trailing columns, staged 32 chunks at a time:
+// the chunks' B fragments (built by the swaps, YB) are copied into LDS once per workgroup, so
+// they cost ~0.5 B per element instead of one 256-B load per 64-row tile and column.
+#ifndef TCI_CSH_DBG
+#define TCI_CSH_DBG 0
+#endif
+#ifndef TCI_CSH_TAU_SLICE
+#define TCI_CSH_TAU_SLICE 0
+#endif
+#ifndef TCI_CSH_GB
+#define TCI_CSH_GB 0  // debug: B fragments from global memory instead of LDS
+#endif
+#ifndef TCI_CSH_ALL
+#define TCI_CSH_ALL 0  // debug: examine every element exactly
+#endif
+#ifndef TCI_CSH_REPS
+#define TCI_CSH_REPS 2  // waves per 64-row slice of the complex shadow step
+#endif
+constexpr int kCSSlices = 8, kCSReps = TCI_CSH_REPS, kCSThreads = 64 * kCSSlices * kCSReps, kCSGroup = 32,
+              kCSExCap = 64;
 typedef _Float16 ch8 __attribute__((ext_vector_type(8)));
 typedef float cf4 __attribute__((ext_vector_type(4)));
 
 template <int P>
 __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
-    static_assert(P >= 1 && P <= kCShMaxP, "6P split slots in one K = 32 MFMA");
-    __shared__ unsigned tau_s;
+    static_assert(P >= 1 && P <= kCShMaxP && 6 * kCShMaxP <= kCShK, "6P split slots");
+    constexpr int NK = (6 * P + 31) / 32;  // MFMAs (K = 32) per tile and plane
+    constexpr int BS = 2 * NK * 4 + 1;     // ch8 per staged column: [plane][u][row quad], padded
+    constexpr int GR = NK == 1 ? kCSGroup : kCSGroup / 2;  // chunks staged at once
+    __shared__ ch8 lb[GR * 16 * BS];
+    __shared__ unsigned tau_sl[kCSSlices];
     __shared__ unsigned exl[kCSThreads / 64 * kCSExCap];
     __shared__ float exm[kCSThreads / 64 * kCSExCap];
     __shared__ CCand red[kCSThreads / 64];
@@ -923,49 +997,89 @@ __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
     const bool shok = shs > 0.0 && mag < 0x1p100 && maxM * shs <= 0x1p15 &&
                       epsd < ldexp(pm[t - 1] * shs, -7);
     const int rb0 = t & ~15, cb0 = t & ~15;
-    const int ntr = (m - rb0 + kCSRows - 1) / kCSRows;
-    const int tr = blockIdx.x % ntr, tcw = blockIdx.x / ntr;
-    const int r0 = rb0 + tr * kCSRows, c0 = cb0 + tcw * kCSCols;
+    const int tiles_r = (m - rb0 + 511) / 512;
+    const int nck = (n - cb0 + 15) / 16;
+    const int nq = gridDim.x / tiles_r;
+    const int tr = blockIdx.x % tiles_r, q = blockIdx.x / tiles_r;
+    const int myck = q < nck ? (nck - 1 - q) / nq + 1 : 0;  // chunks q, q + nq, ...
+    const int r0 = rb0 + 512 * tr;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slice = wave % kCSSlices, rep = wave / kCSSlices;
+#if TCI_CSH_TAU_SLICE
+    unsigned& tau_s = tau_sl[slice];  // debug: the lower bound shared by a slice's waves only
+#else
+    unsigned& tau_s = tau_sl[0];
+#endif
     const double2* A = g.A;
     const int64_t ld = g.ld;
     CCand best{-INFINITY, INT32_MAX, INT32_MAX};
-    // exact value of element (i, j): the stale value minus the pending updates in pivot order
-    auto exact = [&](int i, int j) {
+    // exact value of element (i, j): the stale value minus the pending updates in pivot order.
+    // FAST: every slot's loads in flight at once (no streaming registers live); otherwise one
+    // slot at a time (a full list mid-stream)
+    auto exact = [&](int i, int j, auto fast) {
         double2 a = A[i + (int64_t)j * ld];
+        if constexpr (decltype(fast)::value) {
+            double2 xv[P], yv[P];
 #pragma unroll
-        for (int s = 0; s < P; ++s) {
-            const double2 z = cmul(g.X[(int64_t)s * g.ldx + i], g.Y[(int64_t)s * g.ldy + j]);
-            a.x = a.x - z.x;
-            a.y = a.y - z.y;
+            for (int s = 0; s < P; ++s) {
+                xv[s] = g.X[(int64_t)s * g.ldx + i];
+                yv[s] = g.Y[(int64_t)s * g.ldy + j];
+            }
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(xv[s], yv[s]);
+                a.x = a.x - z.x;
+                a.y = a.y - z.y;
+            }
+        } else {
+#pragma unroll 1
+            for (int s = 0; s < P; ++s) {
+                const double2 z = cmul(g.X[(int64_t)s * g.ldx + i], g.Y[(int64_t)s * g.ldy + j]);
+                a.x = a.x - z.x;
+                a.y = a.y - z.y;
+            }
         }
         const CCand c{a.x * a.x + a.y * a.y, j, i};
+#if TCI_CSH_DBG
+        if (t >= 7 && t <= 8 && j == t + 2)
+            printf("[dbg-exact t=%d] i=%d j=%d v=%.17g best=(%.17g,%d,%d)\n", t, i, j, c.v, best.v, best.col, best.row);
+#endif
         if (cbetter(c, best)) best = c;
     };
     if (!shok) {
         // the bound is not tight (decaying pivots) or fp16 could overflow: every element exactly
-        for (int e = threadIdx.x; e < kCSRows * kCSCols; e += kCSThreads) {
-            const int i = r0 + (e & (kCSRows - 1)), j = c0 + e / kCSRows;
-            if (i >= t && i < m && j >= t && j < n) exact(i, j);
+        for (int ci = 0; ci < myck; ++ci) {
+            const int cj = cb0 + 16 * (q + nq * ci);
+            for (int e = threadIdx.x; e < 512 * 16; e += kCSThreads) {
+                const int i = r0 + (e & 511), j = cj + (e >> 9);
+                if (i >= t && i < m && j >= t && j < n) exact(i, j, std::true_type{});
+            }
         }
     } else {
-        const float eps = (float)(epsd * (1.0 + 0x1p-20));
+        const float eps = TCI_CSH_ALL ? 1e30f : (float)(epsd * (1.0 + 0x1p-20));
         const float margin = 0x1p-20f;
         const int gq = lane >> 4, lcol = lane & 15;
-        const int rl = r0 + 16 * gq;  // the lane's 16 loaded rows
+        const int sb = r0 + 64 * slice;  // the wave's slice
+        const int rl = sb + 16 * gq;     // the lane's 16 loaded rows
         const bool rload = rl < g.lds;
-        const bool rmask = __any(rl < t);  // the wave holds rows before t: masked per element
-        ch8 af[4];
+        const bool rmask = __any(rl < t);  // rows before t in the wave: masked per element
+        ch8 af[4][NK];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int rho = r0 + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
-            af[b] = rho < m ? *reinterpret_cast<const ch8*>(g.XA + (int64_t)rho * kCShK + 8 * gq) : ch8{};
+            const int rho = sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
+#pragma unroll
+            for (int u = 0; u < NK; ++u)
+                af[b][u] = rho < m ? *reinterpret_cast<const ch8*>(g.XA + (int64_t)rho * kCShK + 32 * u + 8 * gq)
+                                   : ch8{};
         }
+        bool act = false;
+        for (int z = 0; z < 16; ++z) act |= (rl + z >= t && rl + z < m);
+        const bool wact = __any(act);
         const _Float16* SR = reinterpret_cast<const _Float16*>(g.SR);
         const _Float16* SI = reinterpret_cast<const _Float16*>(g.SI);
-        const int nch = kCSCols / 16;
-        auto load = [&](int h, ch8 (&vr)[2], ch8 (&vi)[2]) {
-            const int j = c0 + 16 * h + lcol;
+        auto colof = [&](int ci) { return cb0 + 16 * (q + nq * ci) + lcol; };  // chunk ci, this lane
+        auto load = [&](int ci, ch8 (&vr)[2], ch8 (&vi)[2]) {
+            const int j = colof(ci);
             if (rload && j < n) {
                 const ch8* pr = reinterpret_cast<const ch8*>(SR + rl + (int64_t)j * g.lds);
                 const ch8* pi = reinterpret_cast<const ch8*>(SI + rl + (int64_t)j * g.lds);
@@ -977,13 +1091,24 @@ __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
                 vr[0] = vr[1] = vi[0] = vi[1] = ch8{};
             }
         };
-        // chunk h: the lane's column's maximum modulus over its 16 rows, per 4-row block
-        auto approx = [&](int h, const ch8 (&vr)[2], const ch8 (&vi)[2], float (&mbs)[4]) -> float {
-            const int j = c0 + 16 * h + lcol;
+        // chunk ci (local li in the staged group): the lane's column's maximum modulus over its 16
+        // rows, per 4-row block (-1: not a trailing column)
+        auto approx = [&](int ci, int li, const ch8 (&vr)[2], const ch8 (&vi)[2], float (&mbs)[4]) -> float {
+            const int j = colof(ci);
             const bool jok = j >= t && j < n;
-            const int jj = j < n ? j : 0;
-            const ch8 bre = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + 8 * gq);
-            const ch8 bim = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + kCShK + 8 * gq);
+            const ch8* lp = lb + (li * 16 + lcol) * BS;
+            ch8 bre[NK], bim[NK];
+#pragma unroll
+            for (int u = 0; u < NK; ++u) {
+#if TCI_CSH_GB
+                const int jj = j < n ? j : 0;
+                bre[u] = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + 32 * u + 8 * gq);
+                bim[u] = *reinterpret_cast<const ch8*>(g.YB + (int64_t)jj * 2 * kCShK + kCShK + 32 * u + 8 * gq);
+#else
+                bre[u] = lp[u * 4 + gq];
+                bim[u] = lp[NK * 4 + u * 4 + gq];
+#endif
+            }
             float c = 0.0f;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -992,8 +1117,11 @@ __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
                 const ch8& hi = vi[b >> 1];
                 cf4 dr = {(float)hr[o], (float)hr[o + 1], (float)hr[o + 2], (float)hr[o + 3]};
                 cf4 di = {(float)hi[o], (float)hi[o + 1], (float)hi[o + 2], (float)hi[o + 3]};
-                dr = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bre, dr, 0, 0, 0);
-                di = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bim, di, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < NK; ++u) {
+                    dr = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b][u], bre[u], dr, 0, 0, 0);
+                    di = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b][u], bim[u], di, 0, 0, 0);
+                }
                 float q2[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) q2[e] = dr[e] * dr[e] + di[e] * di[e];
@@ -1010,31 +1138,41 @@ __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
                 for (int b = 0; b < 4; ++b) mbs[b] = -1.0f;
                 c = -1.0f;
             }
+#if TCI_CSH_DBG
+            if (t >= 7 && t <= 8 && j == t + 2 && rl <= t + 2 && t + 2 < rl + 16)
+                printf("[dbg t=%d wg=%d wave=%d lane=%d] j=%d rl=%d mbs %g %g %g %g c=%g eps=%g shs=%g\n", t,
+                       (int)blockIdx.x, wave, lane, j, rl, mbs[0], mbs[1], mbs[2], mbs[3], c, eps, shs);
+#endif
             return c;
         };
         float tau = 0.0f;
         unsigned* const wl = exl + wave * kCSExCap;
         float* const wm = exm + wave * kCSExCap;
         int nex = 0;
-        auto flush = [&]() {
+        auto flush = [&](auto fast) {
             const float thr = tau - tau * margin;
             for (int e = lane; e < 4 * nex; e += 64) {
                 if (wm[e >> 2] + eps < thr) continue;
                 const unsigned key = wl[e >> 2];
-                const int j = (int)(key & 0xffffffu) , i = (int)(key >> 24) * 4 + (e & 3) + r0;
-                if (i >= t && i < m) exact(i, j);
+                const int j = (int)(key & 0xffffffu), i = sb + 4 * (int)(key >> 24) + (e & 3);
+#if TCI_CSH_DBG
+                if (t >= 7 && t <= 8 && j == t + 2 && i >= t && i < t + 30)
+                    printf("[dbg-flush t=%d wg=%d wave=%d lane=%d] e=%d nex=%d i=%d j=%d wm=%g thr=%g\n", t, (int)blockIdx.x,
+                           wave, lane, e, nex, i, j, wm[e >> 2], thr);
+#endif
+                if (i >= t && i < m) exact(i, j, fast);
             }
             nex = 0;
         };
-        auto append = [&](int h, const float (&mbs)[4], float bound) {
-            const int j = c0 + 16 * h + lcol;
+        auto append = [&](int ci, const float (&mbs)[4], float bound) {
+            const int j = colof(ci);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const bool f = mbs[b] >= 0.0f && mbs[b] + eps >= bound;
                 const uint64_t bal = __ballot(f);
                 if (bal == 0) continue;
                 const int cnt = __popcll(bal);
-                if (nex + cnt > kCSExCap) flush();
+                if (nex + cnt > kCSExCap) flush(std::false_type{});
                 if (f) {
                     const int at = nex + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                                         __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
@@ -1046,61 +1184,86 @@ __global__ __launch_bounds__(kCSThreads) void k_crrlu_step_sh(CStepArgs g) {
         };
         auto test = [&](float c) {
             if (c < 0.0f) return;
-            const float lb = fmaxf(c - eps, 0.0f);
-            const float ts = __uint_as_float(__hip_atomic_load(&tau_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            const float lbd = fmaxf(c - eps, 0.0f);
+            const float ts = __uint_as_float(__hip_atomic_load(&tau_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));  // slice
             tau = fmaxf(tau, ts);
-            if (lb > tau) {
-                tau = lb;
-                atomicMax(&tau_s, __float_as_uint(lb));
+            if (lbd > tau) {
+                tau = lbd;
+                atomicMax(&tau_s, __float_as_uint(lbd));
             }
         };
-        if (threadIdx.x == 0) tau_s = 0u;
         ch8 ar[2], ai[2], br[2], bi[2];
         float mb0[4], mb1[4];
-        int h0 = wave, h1 = wave + 4;
-        load(h0, ar, ai);
-        load(h1, br, bi);
-        __syncthreads();
-        // seed: every wave's first chunk sets the workgroup's bound before anything is listed
-        const float cs = approx(h0, ar, ai, mb0);
-        {
-            float lb = fmaxf(cs - eps, 0.0f);
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) lb = fmaxf(lb, __shfl_xor(lb, off));
-            if (lane == 0) atomicMax(&tau_s, __float_as_uint(lb));
-        }
-        h0 += 8;
-        if (h0 < nch) load(h0, ar, ai);
-        __syncthreads();
-        tau = __uint_as_float(tau_s);
-        append(h0 - 8, mb0, tau - tau * margin);
-        for (;;) {
-            if (h1 >= nch) break;
-            {
-                const float c = approx(h1, br, bi, mb1);
-                const int e = h1;
-                h1 += 8;
-                if (h1 < nch) load(h1, br, bi);
-                test(c);
-                append(e, mb1, tau - tau * margin);
+        for (int g0 = 0; g0 < myck; g0 += GR) {
+            const int gn = min(GR, myck - g0);
+            int h0 = g0 + rep, h1 = g0 + rep + kCSReps;  // this wave's chunks: rep, rep + 2, ...
+            if (wact) {
+                if (h0 < g0 + gn) load(h0, ar, ai);
+                if (h1 < g0 + gn) load(h1, br, bi);
             }
-            if (h0 >= nch) break;
-            {
-                const float c = approx(h0, ar, ai, mb0);
-                const int e = h0;
-                h0 += 8;
-                if (h0 < nch) load(h0, ar, ai);
-                test(c);
-                append(e, mb0, tau - tau * margin);
+            if (g0 > 0) __syncthreads();  // the previous group's readers are done with lb
+            // stage the group's B fragments: one column per thread (16 B loads)
+            if (threadIdx.x < gn * 16) {
+                const int li = threadIdx.x >> 4, c = threadIdx.x & 15;
+                const int j = cb0 + 16 * (q + nq * (g0 + li)) + c;
+                const ch8* src = reinterpret_cast<const ch8*>(g.YB + (int64_t)(j < n ? j : 0) * 2 * kCShK);
+                ch8* dst = lb + (li * 16 + c) * BS;
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+                    for (int z = 0; z < NK * 4; ++z) dst[pl * NK * 4 + z] = j < n ? src[pl * 8 + z] : ch8{};
+            }
+            if (g0 == 0 && threadIdx.x < kCSSlices) tau_sl[threadIdx.x] = 0u;
+            __syncthreads();
+            if (g0 == 0) {
+                // seed: every wave's first chunk sets the workgroup's bound before anything is listed
+                float c0 = -1.0f;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) mb0[b] = -1.0f;
+                const int e0 = h0;
+                if (wact && h0 < g0 + gn) {
+                    c0 = approx(h0, h0 - g0, ar, ai, mb0);
+                    h0 += 2 * kCSReps;
+                    if (h0 < g0 + gn) load(h0, ar, ai);
+                    float lbd = fmaxf(c0 - eps, 0.0f);
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) lbd = fmaxf(lbd, __shfl_xor(lbd, off));
+                    if (lane == 0) atomicMax(&tau_s, __float_as_uint(lbd));
+                }
+                __syncthreads();
+                tau = __uint_as_float(tau_s);
+                // wave-uniform call: the list length nex must stay the same in every lane (lanes
+                // of non-trailing columns carry mb0 = -1 and append nothing)
+                if (wact) append(e0, mb0, tau - tau * margin);
+            }
+            if (!wact) continue;
+            // h0's values in ar/ai, h1's in br/bi; the next chunk is always the smaller index
+            for (;;) {
+                if (h1 < h0) {
+                    if (h1 >= g0 + gn) break;
+                    const float c = approx(h1, h1 - g0, br, bi, mb1);
+                    const int e = h1;
+                    h1 += 2 * kCSReps;
+                    if (h1 < g0 + gn) load(h1, br, bi);
+                    test(c);
+                    append(e, mb1, tau - tau * margin);
+                } else {
+                    if (h0 >= g0 + gn) break;
+                    const float c = approx(h0, h0 - g0, ar, ai, mb0);
+                    const int e = h0;
+                    h0 += 2 * kCSReps;
+                    if (h0 < g0 + gn) load(h0, ar, ai);
+                    test(c);
+                    append(e, mb0, tau - tau * margin);
+                }
             }
         }
         tau = fmaxf(tau, __uint_as_float(__hip_atomic_load(&tau_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
-        flush();
+        flush(std::true_type{});
     }
     best = block_reduce<kCSThreads>(best, red);
     if (threadIdx.x == 0) g.cand[blockIdx.x] = best;
 }
-
 
 template <int P>
 static void crrlu_step_p(hipStream_t s, const CStepArgs& g, bool flush, int grid) {
@@ -1162,9 +1325,12 @@ void launch_crrlu_step_d(hipStream_t s, CStepArgs g, int P, bool flush) {
 
 int crrlu_sh_grid(int m, int n, int t) {
     const int rb0 = t & ~15;
-    const int ntr = m - rb0 > 0 ? (m - rb0 + kCSRows - 1) / kCSRows : 1;
-    const int ntc = n - rb0 > 0 ? (n - rb0 + kCSCols - 1) / kCSCols : 1;
-    return ntr * ntc;
+    const int tiles_r = m - rb0 > 0 ? (m - rb0 + 511) / 512 : 1;
+    const int nck = n - rb0 > 0 ? (n - rb0 + 15) / 16 : 1;
+    int nq = 256 / tiles_r;  // one 1024-thread workgroup per CU
+    if (nq > nck) nq = nck;
+    if (nq < 1) nq = 1;
+    return tiles_r * nq;
 }
 
 // shadow-search step for pivot t (P pending, 1..kCShMaxP), then reduce + swap (pending P after)
@@ -1176,10 +1342,68 @@ void launch_crrlu_step_sh(hipStream_t s, CStepArgs g, int P) {
         case 3: crrlu_step_sh_p<3>(s, g, grid); break;
         case 4: crrlu_step_sh_p<4>(s, g, grid); break;
         case 5: crrlu_step_sh_p<5>(s, g, grid); break;
+        case 6: crrlu_step_sh_p<6>(s, g, grid); break;
+        case 7: crrlu_step_sh_p<7>(s, g, grid); break;
+        case 8: crrlu_step_sh_p<8>(s, g, grid); break;
+        case 9: crrlu_step_sh_p<9>(s, g, grid); break;
+        case 10: crrlu_step_sh_p<10>(s, g, grid); break;
         default: return;
     }
     g.P = P;
     hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, grid);
+    hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
+}
+
+// debug (env TCI_CSH_CHECK): the shadow step's winner against the exact step's, on the host
+void debug_crrlu_check_sh(hipStream_t s, CStepArgs g, int P) {
+    const int g1 = crrlu_sh_grid(g.m, g.n, g.t);
+    switch (P) {
+        case 1: crrlu_step_sh_p<1>(s, g, g1); break;
+        case 2: crrlu_step_sh_p<2>(s, g, g1); break;
+        case 3: crrlu_step_sh_p<3>(s, g, g1); break;
+        case 4: crrlu_step_sh_p<4>(s, g, g1); break;
+        case 5: crrlu_step_sh_p<5>(s, g, g1); break;
+        case 6: crrlu_step_sh_p<6>(s, g, g1); break;
+        case 7: crrlu_step_sh_p<7>(s, g, g1); break;
+        case 8: crrlu_step_sh_p<8>(s, g, g1); break;
+        case 9: crrlu_step_sh_p<9>(s, g, g1); break;
+        case 10: crrlu_step_sh_p<10>(s, g, g1); break;
+        default: return;
+    }
+    static CCand h1[1 << 16], h2[1 << 16];
+    hipMemcpyAsync(h1, g.cand, sizeof(CCand) * g1, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    g.tiles_r = g.m - g.t > 0 ? (g.m - g.t + kCTR - 1) / kCTR : 1;
+    const int g2 = crrlu_grid(g.m, g.n, g.t);
+    switch (P) {
+        case 1: crrlu_step_p<1>(s, g, false, g2); break;
+        case 2: crrlu_step_p<2>(s, g, false, g2); break;
+        case 3: crrlu_step_p<3>(s, g, false, g2); break;
+        case 4: crrlu_step_p<4>(s, g, false, g2); break;
+        case 5: crrlu_step_p<5>(s, g, false, g2); break;
+        case 6: crrlu_step_p<6>(s, g, false, g2); break;
+        case 7: crrlu_step_p<7>(s, g, false, g2); break;
+        case 8: crrlu_step_p<8>(s, g, false, g2); break;
+        case 9: crrlu_step_p<9>(s, g, false, g2); break;
+        case 10: crrlu_step_p<10>(s, g, false, g2); break;
+    }
+    hipMemcpyAsync(h2, g.cand, sizeof(CCand) * g2, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    auto better = [](const CCand& b, const CCand& a) {
+        return b.v > a.v || (b.v == a.v && (b.col < a.col || (b.col == a.col && b.row < a.row)));
+    };
+    CCand w1{-INFINITY, INT32_MAX, INT32_MAX}, w2 = w1;
+    for (int i = 0; i < g1; ++i) if (better(h1[i], w1)) w1 = h1[i];
+    for (int i = 0; i < g2; ++i) if (better(h2[i], w2)) w2 = h2[i];
+    if (w1.v != w2.v || w1.col != w2.col || w1.row != w2.row) {
+        printf("[csh-check] t=%d P=%d shadow (%.17g, col %d, row %d) exact (%.17g, col %d, row %d)\n", g.t, P,
+               w1.v, w1.col, w1.row, w2.v, w2.col, w2.row);
+        // the shadow step's candidates of the workgroups that hold the exact winner's column
+        for (int i = 0; i < g1; ++i)
+            if (h1[i].col / 16 == w2.col / 16) printf("   wg %d: (%.17g, col %d, row %d)\n", i, h1[i].v, h1[i].col, h1[i].row);
+    }
+    g.P = P;
+    hipLaunchKernelGGL(k_crrlu_reduce_d, dim3(1), dim3(kRThreads), 0, s, g, g2);
     hipLaunchKernelGGL(k_crrlu_swap_d, dim3((g.m + g.n + 256) / 256), dim3(256), 0, s, g);
 }
 
