@@ -529,7 +529,7 @@ def extras(T, ctx):
     tc = min(walls[1:])
     res["rrlu_c128"] = {"m": mc, "n": nc, "r": int(npv.value), "ms": round(tc * 1e3, 2),
                         "complex_GFLOPs": round(8 * elc / tc / 1e9, 1),
-                        "algorithmic_GBps": round(32 * elc / tc / 1e9, 1)}
+                        "search": "certified fp16 shadow (Re/Im planes) + f16-split MFMA, nb = 11 (DESIGN.md K8)"}
     # other rrLU configurations of SURVEY 8(d): config 2 (4096^2), right-orthogonal pivots, and a
     # 16384^2 matrix (2 GiB) for the scale curve
     res["rrlu_configs"] = []

@@ -960,7 +960,7 @@ __global__ void k_crrlu_swap_d(CStepArgs g) {
 #define TCI_CSH_ALL 0  // debug: examine every element exactly
 #endif
 #ifndef TCI_CSH_REPS
-#define TCI_CSH_REPS 2  // waves per 64-row slice of the complex shadow step
+#define TCI_CSH_REPS 1  // waves per 64-row slice of the complex shadow step (2: 1024 threads, spills; measured 34.6 vs 38.9 ms)
 #endif
 constexpr int kCSSlices = 8, kCSReps = TCI_CSH_REPS, kCSThreads = 64 * kCSSlices * kCSReps, kCSGroup = 32,
               kCSExCap = 64;
