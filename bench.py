@@ -170,6 +170,10 @@ def main():
         dom, dom_ms, dom_launches, dom_bytes, dom_n = ("k_pass2<P,true> (pending updates applied and "
                                                        "written back + abs2 argmax)", wb_ms, wb_launches,
                                                        wb_b, wb_n)
+    # whole-step context: every pass's algorithmic bytes (stride 1), the initial argmax pass (8 B)
+    # and the copy rrlu makes (16 B per element), over the measured step time
+    (ro_all, _), (wb_all, _) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes)
+    step_bytes = ro_all + wb_all + 24.0 * m * n
     avg_launch_ms = dom_ms / max(dom_launches, 1)
     bytes_per_launch = dom_bytes / max(dom_n, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -200,7 +204,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
-                     "deferred_depth_nb": nb, "shadow_search": shadow, "shadow_bytes": sh_bytes},
+                     "deferred_depth_nb": nb, "shadow_search": shadow, "shadow_bytes": sh_bytes,
+                     "step_algorithmic_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                     "step_note": "all passes' algorithmic bytes + initial pass + copy, per measured step; "
+                                  "frac above is the dominant (read-only) kernel alone, half of whose "
+                                  "~40 us is fixed per-pass cost (DESIGN.md K2)"},
     }
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
