@@ -93,7 +93,7 @@ int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
  * Both paths give bitwise identical results. Default on (env TCI_RRLU_SMALL=0: off). */
 int tci_set_rrlu_small(tci_ctx* ctx, int enabled);
 /* Matrices with m*n <= 2^21 whose column blocks fit the LDS of one workgroup per CU are factorised
- * by a persistent cooperative grid holding the matrix on chip (one grid barrier per pivot);
+ * by a persistent grid holding the matrix on chip (one grid barrier per pivot);
  * enabled = 0 forces the pass pipeline. Bitwise identical results. Default on (env
  * TCI_RRLU_MID=0: off). */
 int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);

@@ -376,10 +376,13 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->hflag, c->fault, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (*c->hflag) return set_err(c, TCI_ERR_DEVICE, "rrlu: grid barrier timed out (mid-size path)");
-        *np_out = c->hst->np;
-        *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;
-        return TCI_OK;
+        if (!*c->hflag) {
+            *np_out = c->hst->np;
+            *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;
+            return TCI_OK;
+        }
+        // the grid barrier timed out (workgroups not co-resident): the input is untouched, so the
+        // pass pipeline below recomputes the same factorisation
     }
     // pending rank-1 updates, slot-major: X[s * ldx + i] (slot s, physical row i), Y[s * ldy + j];
     // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
@@ -748,9 +751,6 @@ int tci_ctx_create(int device, tci_ctx** out) {
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->ncu = prop.multiProcessorCount;
-        int coop = 0;
-        if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop)
-            c->mid_path = 0;
     }
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -834,9 +834,7 @@ int tci_set_dense_mfma(tci_ctx* c, int mask) {
 }
 
 int tci_set_rrlu_mid(tci_ctx* c, int enabled) {
-    int coop = 0;
-    hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device);
-    c->mid_path = enabled != 0 && coop;
+    c->mid_path = enabled != 0;
     return TCI_OK;
 }
 

@@ -199,7 +199,7 @@ struct SmallOut {
     unsigned long long* maxout;
 };
 bool rrlu_small_fits(int64_t m, int64_t n);
-// mid-size matrices: persistent cooperative grid (one workgroup per CU, matrix in LDS), one grid
+// mid-size matrices: persistent grid (one workgroup per CU, matrix in LDS), one grid
 // barrier per pivot. colbuf: min(ncu, 256) x m doubles; count / fault: device words.
 bool rrlu_mid_fits(int64_t m, int64_t n, int ncu);
 hipError_t launch_rrlu_mid(hipStream_t s, int ncu, const double* A, int64_t lda, int m, int n, int mr,

@@ -1963,7 +1963,7 @@ hipError_t launch_rrlu_small(hipStream_t s, const double* A, int64_t lda, int m,
 // ------------------------------------------------------------ mid-size rrLU
 // Pi matrices of a few MiB (C3': 1024^2 at rank 64) are too big for one workgroup's LDS and too
 // small for the pass pipeline, whose ~16 us per pivot is a chain of dependent memory round trips
-// plus a launch. Here the matrix lives in the LDS of a persistent cooperative grid (one
+// plus a launch. Here the matrix lives in the LDS of a persistent grid (one
 // workgroup per CU), split by column blocks; each pivot costs one grid barrier:
 //   1. every workgroup publishes its local argmax candidate and that candidate's (current,
 //      updated) column (sc1 stores), then arrives at the barrier (agent-scope atomic counter);
@@ -2209,9 +2209,12 @@ hipError_t launch_rrlu_mid(hipStream_t s, int ncu, const double* A, int64_t lda,
     if ((int64_t)per_cu * ncu < G) return hipErrorCooperativeLaunchTooLarge;
     if ((e = hipMemsetAsync(count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fault, 0, sizeof(int), s)) != hipSuccess) return e;
-    void* args[] = {&g};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_rrlu_mid), dim3(G), dim3(kMidThreads),
-                                      args, (unsigned)bytes, s);
+    // An ordinary launch, not hipLaunchCooperativeKernel: G <= one workgroup per CU fits the chip
+    // at once, and the barrier's timeout + fault flag bound the wait if another stream's kernels
+    // hold CUs (the host then reruns the factorisation on the pass pipeline). HIP's cooperative
+    // queue was also what faulted in exit() after rocprofv3's finalisation.
+    hipLaunchKernelGGL(k_rrlu_mid, dim3(G), dim3(kMidThreads), bytes, s, g);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------ extraction

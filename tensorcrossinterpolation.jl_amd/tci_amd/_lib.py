@@ -169,13 +169,35 @@ def shutting_down():
 
 @atexit.register
 def _shutdown():
-    global _shutting_down
+    global _shutting_down, _lib
     for c in list(_live_contexts):
         try:
             c.close()
         except Exception:
             pass
     _shutting_down = True
+    # The compiler-generated module destructor of libtci_hip.so (it unregisters the embedded code
+    # objects from the HIP runtime) is a C atexit handler of the library; left to exit(), it would
+    # run after the C-level shutdown of whatever registered later (rocprofv3's tool finalisation is
+    # one). Unloading the library here runs it now, while the runtime and any profiler are intact.
+    # (The exit-time SIGSEGV of VERDICT r2 #6 itself was HIP's cooperative queue, see
+    # tci_rrlu.hip launch_rrlu_mid.) Nothing calls into the library after this point: every
+    # release()/__del__ checks Context.alive, which is False from here on.
+    diag = os.environ.get("TCI_EXIT_DIAG")
+    if diag:  # the process map before the unload, to resolve frames of an exit-time fault
+        with open("/proc/self/maps") as src, open(diag, "w") as dst:
+            dst.write(src.read())
+    if _lib is not None and os.environ.get("TCI_UNLOAD_AT_EXIT", "1") == "1":
+        try:
+            import _ctypes
+            handle, _lib = _lib._handle, None
+            _ctypes.dlclose(handle)
+        except Exception:
+            pass
+    if diag:
+        import sys
+        print(f"[tci_amd] atexit teardown done (unloaded: {_lib is None}); maps in {diag}",
+              file=sys.stderr, flush=True)
 
 
 class Context:
