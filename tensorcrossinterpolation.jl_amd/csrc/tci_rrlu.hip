@@ -1073,24 +1073,40 @@ constexpr int kMfSlices = kRowsPerTile / kMfRows;      // slices per tile
 constexpr int kMfReps = kP2Threads / 64 / kMfSlices;   // waves per slice
 static_assert(kMfBlk == 4, "a lane's 16 loaded rows are 4 blocks of 4");
 
-// P <= 10 pending updates: 3P <= 30 split slots, one MFMA (K = 32) per tile; deeper passes use
-// k_pass_sh.
-constexpr int kMfMaxP = 10;
-constexpr int kMfKS = 32;                             // split slots per row / column
-constexpr int kMfKSP = kMfKS + 8;                     // LDS stride in halves (80 B: spreads banks)
+// P <= 10 pending updates: 3P <= 30 split slots, one MFMA (K = 32) per tile; P <= 15 (the
+// deepest read pass at kMaxPend = 16): 3P <= 45 slots, two MFMAs (K = 64). Deep passes keep only
+// y_k per staged column in LDS (examinations read the pending y's from Y) so that the 64-slot
+// fragments fit.
+constexpr int kMfMaxP = 15;
 constexpr int kMfExCap = 128;                         // deferred examinations per wave
+static_assert(3 * kMfMaxP <= 64 && kMfMaxP < kMaxPend, "two MFMA K-steps per tile");
+
+template <int P>
+struct MfGeom {
+    static constexpr bool deep = P > 10;
+    static constexpr int KS = deep ? 64 : 32;         // split slots per row / column
+    static constexpr int KSP = KS + 8;                // LDS stride in halves (spreads banks)
+    static constexpr int YS = deep ? 1 : P;           // exact y's kept per staged column
+};
 
 template <int P>
 struct P2MfLds {
-    double ys[kP2StageCols * P];                      // exact y's of the staged columns (examinations)
-    _Float16 yb[kP2StageCols * kMfKSP];               // their B fragments (y splits)
-    _Float16 xa[kRowsPerTile * kMfKSP];               // the tile's rows' A fragments (-x splits)
+    using Gm = MfGeom<P>;
+    double ys[kP2StageCols * Gm::YS];                 // exact y's of the staged columns (examinations)
+    _Float16 yb[kP2StageCols * Gm::KSP];              // their B fragments (y splits)
     int cpos[kP2StageCols];
     int cnt[kMfSlices];
     unsigned tau;
     double xk[kRowsPerTile];                          // x_k of the tile's rows
-    unsigned ex[kP2Threads / 64 * kMfExCap];          // per-wave lists of blocks to examine exactly
-    float exm[kP2Threads / 64 * kMfExCap];            // their approximate maxima
+    // the tile's rows' A fragments are read into registers before the first examination list
+    // entry is written (a barrier lies between), so the two share the space
+    union {
+        _Float16 xa[kRowsPerTile * Gm::KSP];          // -x splits
+        struct {
+            unsigned ex[kP2Threads / 64 * kMfExCap];  // per-wave lists of blocks to examine exactly
+            float exm[kP2Threads / 64 * kMfExCap];    // their approximate maxima
+        } e;
+    } u;
 };
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -1105,7 +1121,9 @@ template <int P>
 __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P>& L,
                                              CandR& best, float eps, double shs,
                                              unsigned long long (&pt)[6]) {
-    static_assert(P >= 1 && P <= kMfMaxP, "one MFMA per tile");
+    static_assert(P >= 1 && P <= kMfMaxP, "at most two MFMA K-steps per tile");
+    using Gm = MfGeom<P>;
+    constexpr int KS = Gm::KS, KSP = Gm::KSP, KSt = KS / 32;
     RrluState* st = sel.st;
     const int32_t* colpos = sel.colpos;
     const int32_t* rowpos = sel.rowpos;
@@ -1195,7 +1213,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         // s < rp - t0, then the pivot's own x (1, or the pivot when not leftorth), then 0
         const int dd = rpos > k ? P : (rpos >= t0 ? rpos - t0 : -1);
         const double own = leftorth ? 1.0 : (rpos >= t0 && rpos <= k ? pv[rpos] : 0.0);
-        _Float16 sl[kMfKS];
+        _Float16 sl[KS];
 #pragma unroll
         for (int s = 0; s < P; ++s) {
             double x = s < dd ? xs[s] : (s == dd ? own : 0.0);
@@ -1204,33 +1222,37 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             sl[3 * s + 1] = sl[3 * s];
         }
 #pragma unroll
-        for (int z = 3 * P; z < kMfKS; ++z) sl[z] = (_Float16)0.0f;
+        for (int z = 3 * P; z < KS; ++z) sl[z] = (_Float16)0.0f;
 #pragma unroll
-        for (int z = 0; z < kMfKS / 8; ++z) {
+        for (int z = 0; z < KS / 8; ++z) {
             h8v w;
 #pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = sl[8 * z + e];
-            *reinterpret_cast<h8v*>(&L.xa[prow * kMfKSP + 8 * z]) = w;
+            *reinterpret_cast<h8v*>(&L.u.xa[prow * KSP + 8 * z]) = w;
         }
     }
     PPROF(1);
     const bool wact = __any(act);
     const float margin = 0x1p-20f;
     float tau = 0.0f;
-    h8v af[kMfBlk];  // A fragments (registers for the whole pass)
+    h8v af[kMfBlk][KSt];  // A fragments (registers for the whole pass)
     // chunk h: the lane's column's maximum |w| over its 16 rows and per 4-row block (-1: not a
     // trailing column)
     auto approx = [&](int h, int gcols, const h8v (&v)[2], float (&mbs)[kMfBlk]) -> float {
         const int lc = h * 16 + lcol;
         const int cp = lc < gcols ? L.cpos[lc] : -1;
-        const h8v bf = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * kMfKSP + 8 * gq]);
+        h8v bf[KSt];
+#pragma unroll
+        for (int u = 0; u < KSt; ++u)
+            bf[u] = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * KSP + 32 * u + 8 * gq]);
         float c = 0.0f;
 #pragma unroll
         for (int b = 0; b < kMfBlk; ++b) {
             const h8v& hv = v[b >> 1];
             const int o = 4 * (b & 1);
             f4v acc = {(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b], bf, acc, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < KSt; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b][u], bf[u], acc, 0, 0, 0);
             mbs[b] = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
                                      __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
             c = __builtin_fmaxf(c, mbs[b]);
@@ -1246,8 +1268,8 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     // or a tie with it go to the wave's list in LDS, and the whole wave examines them together
     // -- one element per lane, all its loads in flight at once -- when the list fills and at the
     // end of each staged group, after pruning them against the latest bound tau.
-    unsigned* const exl = L.ex + wave * kMfExCap;
-    float* const exm = L.exm + wave * kMfExCap;
+    unsigned* const exl = L.u.e.ex + wave * kMfExCap;
+    float* const exm = L.u.e.exm + wave * kMfExCap;
     int nex = 0;  // wave-uniform list length
     // FAST: all P - 1 pending x's of an element in flight at once (the final flush, when the
     // streaming registers are dead); otherwise one at a time (a full list mid-stream: rare)
@@ -1264,17 +1286,35 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const int rp = rowpos[r];
             if (rp <= k) continue;
             if constexpr (decltype(fast)::value) {
-                double xv[P];
+                if constexpr (Gm::deep) {
+                    // x's and y's from memory, four pending updates in flight at a time
 #pragma unroll
-                for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
+                    for (int s0 = 0; s0 < P - 1; s0 += 4) {
+                        double xv[4], yv[4];
 #pragma unroll
-                for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+                        for (int i = 0; i < 4; ++i)
+                            if (s0 + i < P - 1) {
+                                xv[i] = g.X[(int64_t)(s0 + i) * ldx + r];
+                                yv[i] = g.Y[(int64_t)(s0 + i) * ldy + j];
+                            }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (s0 + i < P - 1) v = __dsub_rn(v, __dmul_rn(xv[i], yv[i]));
+                    }
+                } else {
+                    double xv[P];
+#pragma unroll
+                    for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
+#pragma unroll
+                    for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+                }
             } else {
 #pragma unroll 1
                 for (int s = 0; s < P - 1; ++s)
-                    v = __dsub_rn(v, __dmul_rn(g.X[(int64_t)s * ldx + r], L.ys[lc * P + s]));
+                    v = __dsub_rn(v, __dmul_rn(g.X[(int64_t)s * ldx + r],
+                                               Gm::deep ? g.Y[(int64_t)s * ldy + j] : L.ys[lc * P + s]));
             }
-            v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * P + P - 1]));
+            v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * Gm::YS + Gm::YS - 1]));
             const double a2 = __dmul_rn(v, v);
             if (a2 >= best.v) cand_take(best, CandR{a2, v, L.cpos[lc], rp, j, r});
         }
@@ -1340,21 +1380,22 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                     g.Up[k + (int64_t)jst * g.ldu] = yk;
                 }
                 // B fragment: slots (yh_s, yl_s, yh_s) for s < P, zero after
-                _Float16 sl[kMfKS];
+                _Float16 sl[KS];
+                L.ys[lc * Gm::YS + Gm::YS - 1] = yk;
 #pragma unroll
                 for (int s = 0; s < P; ++s) {
-                    L.ys[lc * P + s] = ysv[s];
+                    if constexpr (!Gm::deep) L.ys[lc * P + s] = ysv[s];
                     f16_split(leftorth ? ysv[s] * shs : ysv[s], sl[3 * s], sl[3 * s + 1]);
                     sl[3 * s + 2] = sl[3 * s];
                 }
 #pragma unroll
-                for (int z = 3 * P; z < kMfKS; ++z) sl[z] = (_Float16)0.0f;
+                for (int z = 3 * P; z < KS; ++z) sl[z] = (_Float16)0.0f;
 #pragma unroll
-                for (int z = 0; z < kMfKS / 8; ++z) {
+                for (int z = 0; z < KS / 8; ++z) {
                     h8v w;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) w[e] = sl[8 * z + e];
-                    *reinterpret_cast<h8v*>(&L.yb[lc * kMfKSP + 8 * z]) = w;
+                    *reinterpret_cast<h8v*>(&L.yb[lc * KSP + 8 * z]) = w;
                 }
             }
         }
@@ -1365,7 +1406,9 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
 #pragma unroll
             for (int b = 0; b < kMfBlk; ++b) {
                 const int pr = slice * kMfRows + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
-                af[b] = *reinterpret_cast<const h8v*>(&L.xa[pr * kMfKSP + 8 * gq]);
+#pragma unroll
+                for (int u = 0; u < KSt; ++u)
+                    af[b][u] = *reinterpret_cast<const h8v*>(&L.u.xa[pr * KSP + 32 * u + 8 * gq]);
             }
             PPROF(2);
         }

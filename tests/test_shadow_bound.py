@@ -66,7 +66,7 @@ def test_real_mfma_shadow_bound(seed, decay):
     A = rng.random((m, n)) - 0.3
     if decay:
         A = A * np.exp(-decay * np.arange(n))[None, :]
-    piv, X, Y, blocks = lu_states(A, 14)
+    piv, X, Y, blocks = lu_states(A, 20)
     worst = 0.0
     for t0 in (0, 1, 3):
         stale, rows0, cols0 = blocks[t0]
@@ -74,7 +74,7 @@ def test_real_mfma_shadow_bound(seed, decay):
         B = pv[0] if t0 == 0 else 2.0 * pv[t0 - 1]
         s = sh_scale(B)
         h = f16((stale * s).astype(np.float32)).astype(np.float32)
-        for P in range(1, 11):
+        for P in range(1, 16):  # P <= 10: one MFMA K-step, 11..15: two
             k = t0 + P - 1
             stale_k, rows_k, cols_k = blocks[k + 1] if k + 1 < len(blocks) else (None, None, None)
             if stale_k is None:
