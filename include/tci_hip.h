@@ -84,7 +84,7 @@ int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* l
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
-/* Deferred-update depth of the rrLU (1..16; default 12, env TCI_RRLU_NB): up to nb rank-1
+/* Deferred-update depth of the rrLU (1..16; default 11, env TCI_RRLU_NB): up to nb rank-1
  * updates are applied on the fly by read-only passes and written back every nb-th pivot.
  * Results are bitwise identical for every nb. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);

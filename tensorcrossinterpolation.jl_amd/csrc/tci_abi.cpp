@@ -66,6 +66,8 @@ struct tci_ctx {
     char* zdev = nullptr;  // its device address
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
+    RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
+    hipEvent_t pollev[2] = {nullptr, nullptr};
     unsigned long long* maxbits = nullptr;
     unsigned long long* hmaxbits = nullptr;  // pinned
     void* scratch = nullptr;
@@ -328,6 +330,30 @@ int pick_cb(int64_t m, int64_t n) {
     return 8;
 }
 
+// The stop test of _optimizerrlu! (matrixlu.jl:359-368) runs on the device; passes launched after
+// it fired return at once. The host learns of it without draining the stream: after each chunk
+// of passes the state is copied into one of two pinned slots behind an event, and the host waits
+// only for the previous chunk's copy while the current chunk keeps the GPU busy. A stop is seen
+// at most one chunk late (<= kMaxChunk empty launches), and no chunk boundary leaves the GPU idle.
+struct StopPoll {
+    static constexpr int64_t kMaxChunk = 32;
+    tci_ctx* c;
+    int cur = 0;
+    bool pending = false;
+    explicit StopPoll(tci_ctx* ctx) : c(ctx) {}
+    int after_chunk(bool* stopped) {
+        HIPCHK(c, hipMemcpyAsync(&c->hpoll[cur], c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->pollev[cur], c->stream));
+        if (pending) {
+            HIPCHK(c, hipEventSynchronize(c->pollev[cur ^ 1]));
+            *stopped = c->hpoll[cur ^ 1].done != 0;
+        }
+        pending = true;
+        cur ^= 1;
+        return TCI_OK;
+    }
+};
+
 // The per-pivot loop of _optimizerrlu! (matrixlu.jl:346-369) on a device matrix (clobbered:
 // its trailing values are left stale). Leaves on the device: rowphys/colphys (= rowpermutation /
 // colpermutation, 0-based) in c->rowperm / c->colperm, pivot values in c->pivv, L columns in
@@ -437,8 +463,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
                                       std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
-    bool stopped = false;
-    while (k < mr && !stopped) {
+    StopPoll poll(c);
+    while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
             // pass k: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
@@ -456,13 +482,11 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             if (flush) t0 = kk + 1;
         }
         k = kend;
-        if (k < mr) {
-            HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost,
-                                     c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (c->hst->done) stopped = true;
-            chunk = std::min<int64_t>(chunk * 2, 64);
-        }
+        if (k >= mr) break;
+        bool stopped = false;
+        if ((st = poll.after_chunk(&stopped))) return st;
+        if (stopped) break;
+        chunk = std::min<int64_t>(chunk * 2, StopPoll::kMaxChunk);
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
@@ -691,8 +715,8 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // local argmax of A
     if ((st = select(0))) return st;
     int64_t k = 0, chunk = 2, t0 = 0;
-    bool stopped = false;
-    while (k < mr && !stopped) {
+    StopPoll poll(c);
+    while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
             const int P = (int)(kk - t0) + 1;
@@ -708,12 +732,11 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
             if (flush) t0 = kk + 1;
         }
         k = kend;
-        if (k < mr) {
-            HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (c->hst->done) stopped = true;
-            chunk = std::min<int64_t>(chunk * 2, 64);
-        }
+        if (k >= mr) break;
+        bool stopped = false;
+        if ((st = poll.after_chunk(&stopped))) return st;
+        if (stopped) break;
+        chunk = std::min<int64_t>(chunk * 2, StopPoll::kMaxChunk);
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
@@ -765,6 +788,9 @@ int tci_ctx_create(int device, tci_ctx** out) {
               hipMalloc((void**)&c->fault, sizeof(int)) == hipSuccess &&
               hipMemset(c->ticket, 0, sizeof(unsigned)) == hipSuccess &&
               hipHostMalloc((void**)&c->hflag, sizeof(int), 0) == hipSuccess &&
+              hipHostMalloc((void**)&c->hpoll, 2 * sizeof(RrluState), 0) == hipSuccess &&
+              hipEventCreateWithFlags(&c->pollev[0], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->pollev[1], hipEventDisableTiming) == hipSuccess &&
               hipMalloc((void**)&c->maxbits, sizeof(unsigned long long)) == hipSuccess &&
               hipHostMalloc((void**)&c->hmaxbits, sizeof(unsigned long long), 0) == hipSuccess;
     if (!ok) {
@@ -787,6 +813,9 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->dU); fr(c->cws); fr(c->dRe); fr(c->colposL); fr(c->shsend); fr(c->shrecv); fr(c->lout);
     if (c->hst) hipHostFree(c->hst);
     if (c->hflag) hipHostFree(c->hflag);
+    if (c->hpoll) hipHostFree(c->hpoll);
+    for (auto e : c->pollev)
+        if (e) hipEventDestroy(e);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
     if (c->hin) hipHostFree(c->hin);
     if (c->hout) hipHostFree(c->hout);

@@ -5,11 +5,16 @@ kinds; 1e-12 relative (factors, transcendental integrands) and 1e-10 relative fo
 stated per test.
 """
 import itertools
+import os
 
 import numpy as np
 import pytest
 
 import oracle_lib as O
+
+# the library's deferred-update depth (tci_abi.cpp tci_ctx::flush_every, env TCI_RRLU_NB), restored
+# after tests that change it
+LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "11"))
 
 pytestmark = pytest.mark.gpu
 
@@ -457,4 +462,4 @@ def test_rrlu_deferred_depth_bitwise(ctx, nb):
         for kw in ({"reltol": 1e-7}, {"abstol": 1e-6}):
             assert_lu_bitwise(T.rrlu(B, ctx=ctx, **kw), O.OracleLU(B, **kw))
     finally:
-        ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, 8))
+        ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, LIB_DEFAULT_NB))

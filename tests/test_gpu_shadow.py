@@ -4,10 +4,16 @@ massive ties, exact zeros after the rank, rapidly decaying pivots (the kernel fa
 exact body pass by pass), magnitudes where fp32 would underflow or overflow, NaN and Inf entries,
 odd shapes and every deferred depth. Each case runs with the shadow search on and off.
 """
+import os
+
 import numpy as np
 import pytest
 
 import oracle_lib as O
+
+# the library's deferred-update depth (tci_abi.cpp tci_ctx::flush_every, env TCI_RRLU_NB), restored
+# after tests that change it
+LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "11"))
 
 pytestmark = pytest.mark.gpu
 
@@ -66,7 +72,7 @@ def test_shadow_random(pctx, nb, leftorth):
         kw = dict(maxrank=180, leftorthogonal=leftorth)
         assert_same(outcome_gpu(A, pctx, **kw), outcome_ref(A, **kw))
     finally:
-        pctx.check(pctx.lib.tci_set_rrlu_flush(pctx.h, 10))
+        pctx.check(pctx.lib.tci_set_rrlu_flush(pctx.h, LIB_DEFAULT_NB))
 
 
 @pytest.mark.parametrize("scale", [1e-300, 1e-45, 1e-36, 1e-30, 1e25, 1e31, 1e40, 1e150, 1e300])
