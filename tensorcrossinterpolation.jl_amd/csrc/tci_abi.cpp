@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -335,14 +336,19 @@ int pick_cb(int64_t m, int64_t n) {
 // of passes the state is copied into one of two pinned slots behind an event, and the host waits
 // only for the previous chunk's copy while the current chunk keeps the GPU busy. A stop is seen
 // at most one chunk late (<= kMaxChunk empty launches), and no chunk boundary leaves the GPU idle.
+// Only the leading (np, done) words of the state are copied: RrluState and the ComplexF64 path's
+// CState share that prefix.
+static_assert(offsetof(RrluState, done) == 8 && offsetof(tci::CState, done) == 8, "state prefix");
 struct StopPoll {
     static constexpr int64_t kMaxChunk = 32;
+    static constexpr size_t kPrefix = 16;
     tci_ctx* c;
+    const void* dstate;
     int cur = 0;
     bool pending = false;
-    explicit StopPoll(tci_ctx* ctx) : c(ctx) {}
+    StopPoll(tci_ctx* ctx, const void* state) : c(ctx), dstate(state) {}
     int after_chunk(bool* stopped) {
-        HIPCHK(c, hipMemcpyAsync(&c->hpoll[cur], c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&c->hpoll[cur], dstate, kPrefix, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->pollev[cur], c->stream));
         if (pending) {
             HIPCHK(c, hipEventSynchronize(c->pollev[cur ^ 1]));
@@ -463,7 +469,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
                                       std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
     int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
-    StopPoll poll(c);
+    StopPoll poll(c, c->st);
     while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
@@ -715,7 +721,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // local argmax of A
     if ((st = select(0))) return st;
     int64_t k = 0, chunk = 2, t0 = 0;
-    StopPoll poll(c);
+    StopPoll poll(c, c->st);
     while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
@@ -1126,15 +1132,25 @@ static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t 
         // shadow search, steps with 1..kCShMaxP pending read the fp16 shadow (step 1 is exact and
         // writes the shadow of A's stale values)
         const int nb = std::min(c->c128_nb > 0 ? c->c128_nb : (g.sh ? 11 : 6), tci::kMaxPend - 1);
+        const bool check = getenv("TCI_CSH_CHECK") != nullptr;
         int t0 = 0;
-        for (int t = 0; mr > 0 && t < mr; ++t) {
+        int64_t chunk = 2;
+        StopPoll poll(c, dst);  // the host stops launching soon after the device's stop test fired
+        for (int t = 0, tend = 0; mr > 0 && t < mr; ++t) {
+            if (t == tend && t > 0) {
+                bool stopped = false;
+                if ((st = poll.after_chunk(&stopped))) return st;
+                if (stopped) break;
+                chunk = std::min<int64_t>(chunk * 2, StopPoll::kMaxChunk);
+            }
+            if (t == tend) tend = (int)std::min<int64_t>(t + chunk, mr);
             g.t = t;
             const int P = t - t0;
             const bool flush = P >= nb;
             if (g.sh && !flush && P >= 1 && P <= tci::kCShMaxP) {
                 if (t0 == 0 && t == 1)
                     tci::launch_crrlu_step_stale_sh(c->stream, g);
-                else if (getenv("TCI_CSH_CHECK"))
+                else if (check)
                     tci::debug_crrlu_check_sh(c->stream, g, P);
                 else
                     tci::launch_crrlu_step_sh(c->stream, g, P);
