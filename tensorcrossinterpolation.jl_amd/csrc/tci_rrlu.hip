@@ -50,6 +50,9 @@
 #ifndef TCI_SH_TIGHT
 #define TCI_SH_TIGHT 7  // shadow search only while its error bound is below 2^-TCI_SH_TIGHT |pivot k|
 #endif
+#ifndef TCI_FLUSH_NTL
+#define TCI_FLUSH_NTL 1  // write-back pass: fp64 loads non-temporal (the shadow stays cached for the next pass)
+#endif
 #ifndef TCI_FLUSH_NT
 #define TCI_FLUSH_NT 1  // write-back pass: fp64 stores non-temporal (the next pass reads the shadow, not them)
 #endif
@@ -466,8 +469,16 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
     auto load_chunk = [&](int g0, int h, double2 (&v)[U]) {
         const int j = chunk_col(g0, h);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            v[u] = *reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
+        for (int u = 0; u < U; ++u) {
+            const double2* pa = reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
+            if constexpr (FLUSH && TCI_FLUSH_NTL) {
+                typedef double dv2 __attribute__((ext_vector_type(2)));
+                const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(pa));
+                v[u] = double2{w.x, w.y};
+            } else {
+                v[u] = *pa;
+            }
+        }
     };
     auto stage_col = [&](int g0) -> int {  // the column this thread stages in group g0 (or -1)
         const int gn = min(G, ntc - g0);
