@@ -253,7 +253,7 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_fp16_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_final_pmc_summary.json")
 PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 11, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 
