@@ -33,6 +33,7 @@ extern "C" {
 #define TCI_ERR_NONSQ 3  /* "Pivot matrix at bond $b is not square!" (tensorci2.jl:623)       */
 #define TCI_ERR_DEVICE 4 /* HIP / RCCL failure                                                 */
 #define TCI_ERR_NOMEM 5  /* device allocation failed                                           */
+#define TCI_ERR_HOST 6   /* a host callback (tci_func_create_host) reported failure            */
 
 /* Integrand catalog (DESIGN.md "Integrand catalog"); the reference's `f` is user Julia code,
  * a device kernel needs it as data. */
@@ -46,6 +47,8 @@ extern "C" {
 #define TCI_F_TT 7       /* tensor-train evaluation (test_tensorci2.jl:477-502, TTCache as f)   */
 #define TCI_F_CP 8       /* f(x) = sum_k prod_t g[k][t][x_t]: CP-rank-K synthetic */
 #define TCI_F_MPO 9      /* Contraction(A, B) of two 4-leg tensor trains (contraction.jl:60-575)  */
+#define TCI_F_HOST 10    /* the user's own f / BatchEvaluator, evaluated on the host by a callback
+                            (tci_func_create_host; batcheval.jl:131-214, 247-308)               */
 /* GAUSSMIX, CP and MPO are sums of K separable terms: Pi is assembled as a rank-K fp64 MFMA GEMM
  * (MPO: K = ra*rb at the cut, the factor rows are the left / right environments).
  * MPO params: [N, per site t (ra, d1, d2, ra', rb, d3, rb', offA, offB), cores]: A_t is
@@ -60,11 +63,14 @@ typedef struct tci_func tci_func;
 typedef struct tci_comm tci_comm;
 typedef struct tci_cache tci_cache;
 typedef struct tci_tci2 tci_tci2;
-/* Host-side exchange hook of the column-sharded rrLU: all-gather `count` doubles per rank from
- * d_send into d_recv (rank-major; device pointers of the calling context). Returns 0 on success.
- * Used when no RCCL communicator is passed (e.g. ranks sharing one GPU, or a Julia Distributed
- * transport); called with the context stream synchronised. */
-typedef int (*tci_exchange_fn)(void* user, const double* d_send, double* d_recv, int64_t count);
+/* Host-side exchange hook of the column-sharded rrLU, for when no RCCL communicator is passed
+ * (ranks sharing one GPU, or a Julia Distributed / MPI transport); called with the context stream
+ * synchronised, d_send / d_recv device pointers of the calling context, `count` 8-byte words:
+ *   op 0: all-gather -- d_recv[r * count + i] = rank r's d_send[i];
+ *   op 1: element-wise max over the ranks of d_send[i] as uint64 into d_recv[i].
+ * Returns 0 on success. A failure must be collective (every rank returns nonzero for the same
+ * call), or the other ranks would wait in the next exchange. */
+typedef int (*tci_exchange_fn)(void* user, int op, const void* d_send, void* d_recv, int64_t count);
 
 /* ---------------------------------------------------------------- context */
 int tci_ctx_create(int device, tci_ctx** out);
@@ -122,6 +128,22 @@ int tci_set_dense_mfma(tci_ctx* ctx, int mask);
 int tci_func_create(tci_ctx* ctx, int kind, const double* params, int64_t nparams,
                     const int32_t* localdims, int32_t L, tci_func** out);
 int tci_func_destroy(tci_func* f);
+
+/* The user's own function as an integrand (the route of an arbitrary Julia closure or
+ * BatchEvaluator, batcheval.jl:131-214, onto the device rrLU): the library calls
+ *   fn(user, I, m, nl, J, n, nr, M, out, ldo)
+ * on the calling host thread whenever it needs a batch -- I (m x nl) and J (n x nr) row-major
+ * 1-based host tables, out a column-major (m * D) x n host buffer (ld ldo) to fill with
+ * f([I_i..., c..., J_j...]) at out[i + m*c + ldo*j], exactly the array of
+ * _batchevaluate_dispatch / (f::BatchEvaluator)(Iset, Jset, Val(M)). A nonzero return aborts the
+ * calling entry with TCI_ERR_HOST. The batch is uploaded once into HBM and everything after it
+ * (maxabs, rrLU, MatrixLUCI factors, site-tensor solve, the device memo) runs on the device: any
+ * entry taking a tci_func accepts it (tci_update_pivots_h, tci_sitetensor_h, tci_tci2_sweep2site,
+ * tci_batcheval_*, tci_cache_batcheval_*). */
+typedef int (*tci_host_fn)(void* user, const int32_t* I, int64_t m, int32_t nl, const int32_t* J,
+                           int64_t n, int32_t nr, int32_t M, double* out, int64_t ldo);
+int tci_func_create_host(tci_ctx* ctx, tci_host_fn fn, void* user, const int32_t* localdims,
+                         int32_t L, tci_func** out);
 
 /* ----------------------------------------------------------- batch eval
  * Replaces _batchevaluate_dispatch (batcheval.jl:131-175) plus maxabs (util.jl:34-43) as used by
@@ -310,6 +332,9 @@ int tci_cache_clear(tci_cache* cache);                /* clearcache!(cf), :305-3
 int tci_cache_size(tci_cache* cache, int64_t* n);     /* length of cacheddata(cf) */
 /* cacheddata(cf) (:160-170) as (key, value) pairs: up to capacity written, *n = stored entries */
 int tci_cache_dump_h(tci_cache* cache, int64_t* keys, double* vals, int64_t capacity, int64_t* n);
+/* haskey(cf, x) / cf.cache[key] for npts points X (npts x L row-major, 1-based) without dumping the
+ * table: found[q] = 1 and vals[q] = the memoised value when key(X[q]) is stored, else 0. */
+int tci_cache_lookup_h(tci_cache* cache, const int32_t* X, int64_t npts, int32_t* found, double* vals);
 int tci_cache_batcheval_d(tci_ctx* ctx, tci_cache* cache, const tci_func* f, const int32_t* I, int64_t m,
                           int32_t nl, const int32_t* J, int64_t n, int32_t nr, int32_t M, double* d_out,
                           int64_t ldo, double* maxabs, int64_t* nmiss);
@@ -334,8 +359,9 @@ int tci_comm_allreduce_max_u64_d(tci_comm* comm, void* d_buf, int64_t count);
  * across ranks): rank r holds global columns [c0, c0 + nloc) of the m x n matrix as
  * d_A (ld lda, even) columns 0..nloc-1; column nloc of d_A must exist and is scratch (the pivot
  * column is installed there on every rank). Per pivot every rank runs its pass on its columns, the
- * local winners and their columns are all-gathered (RCCL when comm is given, else exch, else
- * nranks must be 1) and every rank commits the same global winner in the reference's tie order:
+ * local winners (32 B each) are all-gathered, the rank owning the global winner contributes that
+ * column through an element-wise uint64 max (8 (m + 16) B), both over RCCL when comm is given, else
+ * exch, else nranks must be 1; every rank commits the same global winner in the reference's tie order:
  * permutations, npivot, lu.error and pivot errors are bitwise those of tci_rrlu_h on the full
  * matrix, on every rank (rowperm m, colperm n global, 1-based). d_A is clobbered. */
 int tci_rrlu_sharded_d(tci_ctx* ctx, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks,

@@ -48,6 +48,7 @@ struct tci_ctx {
     size_t capS = 0;
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
+    int mid_faulted = 0;   // its grid barrier timed out once on this context: pass pipeline from then on
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
     int c128_nb = -1;            // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1;
                                  // -1: 11 with the shadow search, 6 without -- measured best)
@@ -116,11 +117,14 @@ struct tci_ctx {
     Cand* lout = nullptr;
     size_t capLout = 0;
     int64_t sh_np = 0, sh_nloc = 0, sh_c0 = 0, sh_m = 0, sh_n = 0;
+    int sh_valid = 0;  // the rrLU buffers hold the last tci_rrlu_sharded_d's result (no other rrLU since)
     int sh_leftorth = 1;
     char* cws = nullptr;  // ComplexF64 rrLU: state, candidates, pivot column / row buffers
     size_t capCws = 0;
     double* dRe = nullptr;  // ComplexF64 2-site update: real values of f before the scaling
     size_t capRe = 0;
+    char* hfn = nullptr;    // pinned: the batch a host integrand (TCI_F_HOST) fills
+    size_t capHfn = 0;
     // kernel timing (family 0: rrLU pass with write-back, 1: batch evaluation,
     //                2: rrLU read-only pass)
     bool timing = false;
@@ -176,6 +180,8 @@ struct tci_func {
     int32_t cpK = 0;
     int64_t ntab = 0;
     int32_t mpoEnv = 0, mpoTmp = 0;
+    tci_host_fn hostfn = nullptr;  // TCI_F_HOST: the user's f on the host (tci_func_create_host)
+    void* hostuser = nullptr;
     FuncDev view() const {
         FuncDev f;
         f.cpK = cpK;
@@ -367,6 +373,7 @@ struct StopPoll {
 int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
                 double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out) {
     int st;
+    c->sh_valid = 0;  // the shared rrLU buffers are about to be overwritten
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
@@ -398,7 +405,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         *err_out = (c->hst->np >= std::min(m, n)) ? 0.0 : c->hst->error;  // matrixlu.jl:391-393
         return TCI_OK;
     }
-    if (c->mid_path && c->ncu > 0 && tci::rrlu_mid_fits(m, n, c->ncu)) {
+    if (c->mid_path && !c->mid_faulted && c->ncu > 0 && tci::rrlu_mid_fits(m, n, c->ncu)) {
         // the matrix resident in the LDS of a persistent grid: one launch, one barrier per pivot
         const int64_t G = std::min<int64_t>(std::min(c->ncu, 256), n);
         if ((st = ensure(c, &c->colbuf, &c->capColbuf, (size_t)(G * m)))) return st;
@@ -414,7 +421,9 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             return TCI_OK;
         }
         // the grid barrier timed out (workgroups not co-resident): the input is untouched, so the
-        // pass pipeline below recomputes the same factorisation
+        // pass pipeline below recomputes the same factorisation; this context stops trying the
+        // persistent grid (the device is evidently shared), so the timeout is paid once
+        c->mid_faulted = 1;
     }
     // pending rank-1 updates, slot-major: X[s * ldx + i] (slot s, physical row i), Y[s * ldy + j];
     // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
@@ -570,6 +579,35 @@ int upload_index(tci_ctx* c, int32_t** d, size_t* cap, const int32_t* h, int64_t
     return TCI_OK;
 }
 
+// TCI_F_HOST: the batch is evaluated by the user's callback on this host thread into a pinned
+// buffer (the index tables come back from the device first: every caller has uploaded them), then
+// uploaded once and its max|.| taken on the device, as for the kernels' fused maxabs. The stream is
+// idle while the callback runs, so the pinned buffer is never overwritten under a pending copy.
+int host_batcheval(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
+                   const int32_t* dJ, int64_t n, int32_t nr, int32_t M, int64_t D, double* dout,
+                   int64_t ldo) {
+    if (m <= 0 || n <= 0) return TCI_OK;
+    std::vector<int32_t> hI((size_t)std::max<int64_t>(m * nl, 1)), hJ((size_t)std::max<int64_t>(n * nr, 1));
+    if (m * nl > 0)
+        HIPCHK(c, hipMemcpyAsync(hI.data(), dI, m * nl * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (n * nr > 0)
+        HIPCHK(c, hipMemcpyAsync(hJ.data(), dJ, n * nr * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t mR = m * D;
+    int st;
+    if ((st = ensure_pinned(c, &c->hfn, &c->capHfn, (size_t)(mR * n) * sizeof(double)))) return st;
+    double* hb = reinterpret_cast<double*>(c->hfn);
+    if (f->hostfn(f->hostuser, hI.data(), m, nl, hJ.data(), n, nr, M, hb, mR) != 0)
+        return set_err(c, TCI_ERR_HOST, "host function evaluation failed");
+    ev_begin(c, 1);
+    HIPCHK(c, hipMemcpy2DAsync(dout, ldo * sizeof(double), hb, mR * sizeof(double), mR * sizeof(double), n,
+                               hipMemcpyHostToDevice, c->stream));
+    tci::launch_cache_maxabs(c->stream, dout, mR, n, ldo, c->maxbits);
+    ev_end(c);
+    HIPCHK(c, hipGetLastError());
+    return TCI_OK;
+}
+
 // batch evaluation into a device buffer (column-major, ld ldo). *maxabs = max|out|.
 // batch evaluation launches only (no synchronisation); c->maxbits receives max|out| bits
 int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
@@ -579,6 +617,7 @@ int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
     const int D = M ? f->localdims[nl] : 1;
     if (ldo < m * D) return set_err(c, TCI_ERR_ARG, "ldo < m * prod(centre dims)");
     HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    if (f->kind == TCI_F_HOST) return host_batcheval(c, f, dI, m, nl, dJ, n, nr, M, D, dout, ldo);
     if (m > 0 && n > 0) {
         FuncDev fv = f->view();
         int st;
@@ -613,23 +652,25 @@ int batcheval_device(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
 
 // ------------------------------------------------------------------ column-sharded rrLU driver
 // The loop of rrlu_device with the selection split across ranks: the passes run unchanged on
-// this rank's columns (+ the ghost column) and publish the local winner; then gather -> exchange
-// (RCCL all-gather on the context stream, a host callback, or a copy for one rank) -> commit, all
-// stream-ordered: the host only polls the stop flag in growing chunks, as rrlu_device does.
-int shard_exchange(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* user, int nranks, int64_t rec) {
+// this rank's columns (+ the ghost column) and publish the local winner; then the candidates are
+// exchanged, the rank owning the winning column contributes it, and every rank commits the same
+// pivot (tci_internal.h, column-sharded rrLU) -- all stream-ordered: the host only polls the stop
+// flag in growing chunks, as rrlu_device does. Exchange op 0: all-gather of `words` uint64 per rank
+// (rank-major); op 1: element-wise max of `words` uint64 over the ranks.
+int shard_exchange(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* user, int op, const void* send,
+                   void* recv, int64_t words) {
     if (comm) {
-        if (ncclAllGather(c->shsend, c->shrecv, (size_t)rec, ncclFloat64, comm->nc, c->stream) != ncclSuccess)
-            return set_err(c, TCI_ERR_DEVICE, "rrlu_sharded: ncclAllGather failed");
+        const ncclResult_t r =
+            op == 0 ? ncclAllGather(send, recv, (size_t)words, ncclUint64, comm->nc, c->stream)
+                    : ncclAllReduce(send, recv, (size_t)words, ncclUint64, ncclMax, comm->nc, c->stream);
+        if (r != ncclSuccess)
+            return set_err(c, TCI_ERR_DEVICE, std::string("rrlu_sharded: ") + (op ? "ncclAllReduce" : "ncclAllGather") +
+                                                  " failed: " + ncclGetErrorString(r));
         return TCI_OK;
     }
-    if (exch) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (exch(user, c->shsend, c->shrecv, rec) != 0)
-            return set_err(c, TCI_ERR_DEVICE, "rrlu_sharded: exchange callback failed");
-        return TCI_OK;
-    }
-    if (nranks != 1) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
-    HIPCHK(c, hipMemcpyAsync(c->shrecv, c->shsend, rec * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (exch(user, op, send, recv, words) != 0)
+        return set_err(c, TCI_ERR_DEVICE, "rrlu_sharded: exchange callback failed");
     return TCI_OK;
 }
 
@@ -638,16 +679,21 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
                         int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* np_out,
                         double* err_out) {
     int st;
+    c->sh_valid = 0;
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->colposL, &c->capColposL, (size_t)nloc + 2))) return st;
     if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
-    if ((st = ensure(c, &c->lout, &c->capLout, 1))) return st;
-    const int64_t rec = tci::shard_rec(m);
-    if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)rec))) return st;
-    if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)(rec * nranks)))) return st;
+    const bool multi = nranks > 1 || comm || exch;
+    if (!multi && nranks != 1) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
+    if ((st = ensure(c, &c->lout, &c->capLout, (size_t)nranks + 1))) return st;  // [own, all-gathered ...]
+    const int64_t cw = tci::shard_col(m);
+    if (multi) {
+        if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)cw))) return st;
+        if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)cw))) return st;
+    }
     const int mi = (int)m, nl1 = (int)(nloc + 1);  // local columns + the ghost
     tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, (int)n);
     tci::launch_shard_init(c->stream, c->colposL, (int)nloc, c0);
@@ -699,6 +745,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     g.ticket = c->ticket;
     g.selk = 0;
     g.lout = c->lout;
+    g.pc_off = c0;
     const bool shadow = c->shadow && lda % 4 == 0;
     g.S = nullptr;
     g.lds = 0;
@@ -709,13 +756,20 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
         if ((st = zero_shadow_pad(c, g.lds, m, nl1))) return st;
     }
     const int grid = tci::argmax_grid(mi, nl1, -1, g.cb, std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
+    // candidates: own record at lout[0], the all-gathered ones at lout[1..nranks]
+    tci::Cand* recvC = multi ? c->lout + 1 : c->lout;
+    uint64_t* colsend = reinterpret_cast<uint64_t*>(c->shsend);
+    uint64_t* colrecv = multi ? reinterpret_cast<uint64_t*>(c->shrecv) : nullptr;
     auto select = [&](int selk) -> int {
-        tci::launch_shard_gather(c->stream, c->lout, dA, lda, mi, c->ybuf, ldy, c0, c->shsend);
-        int e = shard_exchange(c, comm, exch, user, nranks, rec);
-        if (e) return e;
-        tci::launch_shard_commit(c->stream, c->shrecv, nranks, rec, mi, selk, c->st, reltol, abstol, c->rowpos,
-                                 c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0, (int)nloc, dA, lda,
-                                 c->ybuf, ldy);
+        if (multi) {
+            int e = shard_exchange(c, comm, exch, user, 0, c->lout, recvC, 4);
+            if (e) return e;
+            tci::launch_shard_pick(c->stream, recvC, nranks, dA, lda, mi, c->ybuf, ldy, c0, (int)nloc, colsend);
+            if ((e = shard_exchange(c, comm, exch, user, 1, colsend, colrecv, cw))) return e;
+        }
+        tci::launch_shard_commit(c->stream, recvC, multi ? nranks : 1, colrecv, mi, selk, c->st, reltol, abstol,
+                                 c->rowpos, c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0, (int)nloc,
+                                 dA, lda, c->ybuf, ldy);
         return TCI_OK;
     };
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // local argmax of A
@@ -826,6 +880,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->hin) hipHostFree(c->hin);
     if (c->hout) hipHostFree(c->hout);
     if (c->zbuf) hipHostFree(c->zbuf);
+    if (c->hfn) hipHostFree(c->hfn);
     for (auto e : c->evpool) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -870,6 +925,7 @@ int tci_set_dense_mfma(tci_ctx* c, int mask) {
 
 int tci_set_rrlu_mid(tci_ctx* c, int enabled) {
     c->mid_path = enabled != 0;
+    c->mid_faulted = 0;
     return TCI_OK;
 }
 
@@ -976,6 +1032,28 @@ int tci_func_create(tci_ctx* c, int kind, const double* params, int64_t nparams,
     return TCI_OK;
 }
 
+int tci_func_create_host(tci_ctx* c, tci_host_fn fn, void* user, const int32_t* localdims, int32_t L,
+                         tci_func** out) {
+    if (!c || !out || !fn || !localdims) return TCI_ERR_ARG;
+    if (L < 1) return set_err(c, TCI_ERR_ARG, "L must be >= 1");
+    for (int t = 0; t < L; ++t)
+        if (localdims[t] < 1) return set_err(c, TCI_ERR_ARG, "localdims must be positive");
+    tci_func* f = new tci_func();
+    f->ctx = c;
+    f->kind = TCI_F_HOST;
+    f->hostfn = fn;
+    f->hostuser = user;
+    f->L = L;
+    f->localdims.assign(localdims, localdims + L);
+    if (hipMalloc((void**)&f->dld, L * sizeof(int32_t)) != hipSuccess) {
+        tci_func_destroy(f);
+        return set_err(c, TCI_ERR_NOMEM, "integrand allocation failed");
+    }
+    hipMemcpy(f->dld, localdims, L * sizeof(int32_t), hipMemcpyHostToDevice);
+    *out = f;
+    return TCI_OK;
+}
+
 int tci_func_destroy(tci_func* f) {
     if (!f) return TCI_OK;
     if (f->dparams) hipFree(f->dparams);
@@ -1064,6 +1142,7 @@ int tci_rrlu_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
 static int crrlu_device(tci_ctx* c, double2* dA, int64_t ld, int64_t m, int64_t n, int64_t mr,
                         double reltol, double abstol, int leftorth, int64_t* np_out,
                         double* err_out, tci::CState** st_out, double2** colbuf_out) {
+    c->sh_valid = 0;
     const int mi = (int)m, ni = (int)n;
     const int G = tci::crrlu_grid(mi, ni, 0);
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -1966,6 +2045,7 @@ int tci_rrlu_sharded_d(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* u
                                  leftorth, &np, &err);
     if (st) return st;
     c->sh_np = np;
+    c->sh_valid = 1;
     c->sh_nloc = nloc;
     c->sh_c0 = c0;
     c->sh_m = m;
@@ -1979,6 +2059,9 @@ int tci_rrlu_sharded_d(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* u
 
 int tci_rrlu_sharded_factors_h(tci_ctx* c, double* L, double* U, int64_t ldu) {
     if (!c) return TCI_ERR_ARG;
+    if (!c->sh_valid)
+        return set_err(c, TCI_ERR_ARG, "rrlu_sharded_factors: no current tci_rrlu_sharded_d result on this "
+                                        "context (another factorisation ran since)");
     const int64_t m = c->sh_m, n = c->sh_n, np = c->sh_np;
     if (np <= 0) return TCI_OK;
     if (U && ldu < np) return set_err(c, TCI_ERR_ARG, "ldu < npivot");
@@ -2054,8 +2137,8 @@ int tci_cache_create(tci_ctx* c, const int32_t* localdims, int32_t L, int64_t ca
     int64_t cap = 1024;
     while (cap < 2 * capacity) cap <<= 1;
     int st;
-    if (hipMalloc((void**)&h->dcoeff, L * 8) != hipSuccess || hipMalloc((void**)&h->counts, 16) != hipSuccess ||
-        hipHostMalloc((void**)&h->hcounts, 16, 0) != hipSuccess) {
+    if (hipMalloc((void**)&h->dcoeff, L * 8) != hipSuccess || hipMalloc((void**)&h->counts, 24) != hipSuccess ||
+        hipHostMalloc((void**)&h->hcounts, 24, 0) != hipSuccess) {
         tci_cache_destroy(h);
         return TCI_ERR_NOMEM;
     }
@@ -2142,7 +2225,7 @@ int tci_cache_batcheval_d(tci_ctx* c, tci_cache* h, const tci_func* f, const int
     if ((st = ensure(c, &h->dup, &h->capDup, (size_t)tot))) return st;
     tci::launch_cache_partial_keys(c->stream, c->dI, (int)m, nl, h->dcoeff, 0, h->kI);
     tci::launch_cache_partial_keys(c->stream, c->dJ, (int)n, nr, h->dcoeff, f->L - nr, h->kJ);
-    HIPCHK(c, hipMemsetAsync(h->counts, 0, 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(h->counts, 0, 24, c->stream));
     tci::CacheProbeArgs a{h->keys, h->vals, h->state, h->cap, h->kI, h->kJ, M ? h->coeffs[nl] : 0, m, mR, n, d_out,
                           ldo, h->miss, h->dup, h->counts};
     if (m == 0 || nl == 0) HIPCHK(c, hipMemsetAsync(h->kI, 0, 8 * std::max<int64_t>(m, 1), c->stream));
@@ -2151,21 +2234,32 @@ int tci_cache_batcheval_d(tci_ctx* c, tci_cache* h, const tci_func* f, const int
     HIPCHK(c, hipMemcpyAsync(h->hcounts, h->counts, 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t nm = (int64_t)h->hcounts[0], nd = (int64_t)h->hcounts[1];
+    // the probe claimed nm empty slots (state 1); until they are filled a failure must give them
+    // back, or later batches would take them for pending values
+    auto rollback = [&](int code) {
+        const std::string msg = c->err;
+        tci::launch_cache_unclaim(c->stream, h->miss, nm, h->keys, h->state);
+        hipStreamSynchronize(c->stream);
+        c->err = msg;
+        return code;
+    };
     if (nm > 0) {
-        if ((st = ensure(c, &h->X, &h->capX, (size_t)(nm * f->L)))) return st;
-        if ((st = ensure(c, &h->mv, &h->capMv, (size_t)nm))) return st;
+        if ((st = ensure(c, &h->X, &h->capX, (size_t)(nm * f->L)))) return rollback(st);
+        if ((st = ensure(c, &h->mv, &h->capMv, (size_t)nm))) return rollback(st);
         tci::launch_cache_gather_points(c->stream, h->miss, nm, c->dI, nl, c->dJ, nr, M, m, mR, h->X);
         // the misses as ONE batch evaluation: no left legs, the points as columns
-        if ((st = batcheval_launch(c, f, c->dI, 1, 0, h->X, nm, f->L, 0, h->mv, 1))) return st;
+        if ((st = batcheval_launch(c, f, c->dI, 1, 0, h->X, nm, f->L, 0, h->mv, 1))) return rollback(st);
         tci::launch_cache_fill(c->stream, h->miss, nm, h->mv, h->vals, h->state, mR, d_out, ldo);
     }
     tci::launch_cache_dups(c->stream, a, nd);
     HIPCHK(c, hipMemsetAsync(c->maxbits, 0, 8, c->stream));
     tci::launch_cache_maxabs(c->stream, d_out, mR, n, ldo, c->maxbits);
     HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(h->hcounts + 2, h->counts + 2, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     h->size += nm;
+    if (h->hcounts[2]) return set_err(c, TCI_ERR_DEVICE, "cache: a repeated point found no ready value");
     if (nmiss) *nmiss = nm;
     if (maxabs) {
         double v;
@@ -2173,6 +2267,25 @@ int tci_cache_batcheval_d(tci_ctx* c, tci_cache* h, const tci_func* f, const int
         memcpy(&v, &b, sizeof v);
         *maxabs = v;
     }
+    return TCI_OK;
+}
+
+int tci_cache_lookup_h(tci_cache* h, const int32_t* X, int64_t npts, int32_t* found, double* vals) {
+    if (!h || npts < 0 || (npts > 0 && (!X || !found || !vals))) return TCI_ERR_ARG;
+    if (npts == 0) return TCI_OK;
+    tci_ctx* c = h->ctx;
+    int st;
+    const size_t bx = (size_t)(npts * h->L) * 4;
+    if ((st = ensure(c, &h->X, &h->capX, (size_t)(npts * h->L)))) return st;
+    if ((st = ensure(c, &h->mv, &h->capMv, (size_t)(2 * npts)))) return st;
+    HIPCHK(c, hipMemcpyAsync(h->X, X, bx, hipMemcpyHostToDevice, c->stream));
+    int32_t* dfound = reinterpret_cast<int32_t*>(h->mv + npts);
+    tci::launch_cache_lookup(c->stream, h->X, npts, h->L, h->dcoeff, h->keys, h->vals, h->state, h->cap, dfound,
+                             h->mv);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(vals, h->mv, npts * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(found, dfound, npts * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }
 

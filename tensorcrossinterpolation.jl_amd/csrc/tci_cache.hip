@@ -49,7 +49,7 @@ struct CacheProbe {
     int64_t ldo;
     int64_t* miss;      // element index, slot (pairs)
     int64_t* dup;       // element index
-    unsigned long long* counts;  // [0] misses, [1] duplicates
+    unsigned long long* counts;  // [0] misses, [1] duplicates, [2] a duplicate found no ready value
 };
 
 __global__ void k_cache_probe(CacheProbe g) {
@@ -120,10 +120,57 @@ __global__ void k_cache_dups(CacheProbe g, int64_t ndup) {
         int64_t s = (int64_t)(cache_hash(key) & (unsigned long long)(g.cap - 1));
         for (int64_t probe = 0; probe < g.cap; ++probe, s = (s + 1) & (g.cap - 1)) {
             if (g.keys[s] == key) {
-                g.out[R + g.ldo * j] = g.vals[s];
+                if (g.state[s] == 2) {
+                    g.out[R + g.ldo * j] = g.vals[s];
+                } else {  // never served as a value: the batch reports an error
+                    g.out[R + g.ldo * j] = __longlong_as_double(0x7ff8000000000badll);
+                    atomicOr(&g.counts[2], 1ull);
+                }
                 break;
             }
         }
+    }
+}
+
+// roll back the slots a failed batch claimed (state 1: value never written): EMPTY again. Safe
+// under linear probing -- the slots were empty before this batch, so no older key's probe chain
+// runs through them, and every key of this batch that probed past one is itself a claim undone here
+__global__ void k_cache_unclaim(const int64_t* __restrict__ miss, int64_t nmiss, unsigned long long* keys,
+                                unsigned* state) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nmiss; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = miss[2 * q + 1];
+        if (state[s] == 1) {
+            state[s] = 0;
+            keys[s] = kCacheEmpty;
+        }
+    }
+}
+
+// haskey / lookup of npts points (row-major, width L, 1-based): found[q] = 1 and vals[q] when the
+// key is in the table with a ready value (cachedfunction.jl:197-240)
+__global__ void k_cache_lookup(const int32_t* __restrict__ X, int64_t npts, int L, const int64_t* __restrict__ coeff,
+                               const unsigned long long* __restrict__ keys, const double* __restrict__ vals,
+                               const unsigned* __restrict__ state, int64_t cap, int32_t* found, double* out) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npts; q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t k = 0;
+        for (int t = 0; t < L; ++t) k += (int64_t)(X[q * L + t] - 1) * coeff[t];
+        const unsigned long long key = (unsigned long long)k;
+        int64_t s = (int64_t)(cache_hash(key) & (unsigned long long)(cap - 1));
+        int32_t f = 0;
+        double v = 0.0;
+        for (int64_t probe = 0; probe < cap; ++probe, s = (s + 1) & (cap - 1)) {
+            const unsigned long long kk = keys[s];
+            if (kk == kCacheEmpty) break;
+            if (kk == key) {
+                if (state[s] == 2) {
+                    f = 1;
+                    v = vals[s];
+                }
+                break;
+            }
+        }
+        found[q] = f;
+        out[q] = v;
     }
 }
 
@@ -192,6 +239,20 @@ void launch_cache_dups(hipStream_t s, const CacheProbeArgs& a, int64_t ndup) {
     CacheProbe g{a.keys, a.vals, a.state, a.cap, a.kI, a.kJ, a.ccoef, a.m, a.mR, a.n, a.out, a.ldo, a.miss, a.dup,
                  a.counts};
     hipLaunchKernelGGL(k_cache_dups, dim3(grid_of(ndup)), dim3(256), 0, s, g, ndup);
+}
+
+void launch_cache_unclaim(hipStream_t s, const int64_t* miss, int64_t nmiss, unsigned long long* keys,
+                          unsigned* state) {
+    if (nmiss <= 0) return;
+    hipLaunchKernelGGL(k_cache_unclaim, dim3(grid_of(nmiss)), dim3(256), 0, s, miss, nmiss, keys, state);
+}
+
+void launch_cache_lookup(hipStream_t s, const int32_t* X, int64_t npts, int L, const int64_t* coeff,
+                         const unsigned long long* keys, const double* vals, const unsigned* state, int64_t cap,
+                         int32_t* found, double* out) {
+    if (npts <= 0) return;
+    hipLaunchKernelGGL(k_cache_lookup, dim3(grid_of(npts)), dim3(256), 0, s, X, npts, L, coeff, keys, vals, state,
+                       cap, found, out);
 }
 
 void launch_cache_maxabs(hipStream_t s, const double* out, int64_t mR, int64_t n, int64_t ldo,

@@ -68,8 +68,10 @@ struct PassArgs {
     float* S;
     int64_t lds;
     // column-sharded rrLU (tci_rrlu_sharded_d): the pass tail writes its rank-local winner here
-    // instead of committing pivot selk (null: commit as usual)
+    // instead of committing pivot selk (null: commit as usual), its physical column made global by
+    // adding pc_off (the rank's first global column; -1 when the rank has no candidate)
     Cand* lout = nullptr;
+    int64_t pc_off = 0;
 };
 
 // Selection fields of PassArgs as seen by the device.
@@ -84,6 +86,7 @@ struct SelArgs {
     double reltol, abstol;
     int selk;
     Cand* lout;  // non-null: local winner only, no commit (column-sharded rrLU)
+    int64_t pc_off;
 };
 
 // MPO-MPO contraction integrand (TCI_F_MPO): LDS limits of the environment kernel, in doubles
@@ -219,18 +222,23 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
 
 // ---- column-sharded rrLU (tci_rrlu.hip). Rank r holds the global columns [c0, c0 + nloc) as its
 // local physical columns 0..nloc-1 plus a ghost column nloc: the column of the last committed
-// pivot, installed on every rank so that the unchanged passes derive x_k from it. Per pivot each
-// rank's pass publishes its local winner (lout); k_shard_gather packs it, the pending y's of its
-// column and that column's stale values into a record of kShardRec(m) doubles; the records of all
-// ranks are all-gathered (RCCL); k_shard_commit reduces them in rank order (every rank reaches the
-// same winner: abs2, then column position, then row position -- submatrixargmax's order), commits
-// it to the replicated row / global column maps and installs the ghost.
-constexpr int kShardHdr = 4 + kMaxPend;
-inline int64_t shard_rec(int64_t m) { return (kShardHdr + m + 1) / 2 * 2; }
+// pivot, installed on every rank so that the unchanged passes derive x_k from it. Per pivot, the
+// candidate first: each rank's pass publishes its local winner (lout: a 32-B Cand
+// with the GLOBAL physical column); the N records are all-gathered (exchange op 0); k_shard_pick
+// reduces them in rank order to the same winner everywhere (abs2, then column position, then row
+// position -- submatrixargmax's order) and the ONE rank owning the winning column writes its pending
+// y's and stale values into a kShardCol(m)-word buffer, the others zeros; an element-wise max of
+// those words as uint64 over the ranks (exchange op 1) leaves the winner's bits everywhere (every
+// bit pattern, -0.0 and NaN payloads included, is >= 0 as uint64); k_shard_commit commits the pivot
+// to the replicated row / global column maps and installs the ghost. Per pivot 32 B x N + 8 (m +
+// kMaxPend) B cross the ranks, not N x 8 m. One rank: no exchange, the commit reads the column in
+// place.
+inline int64_t shard_col(int64_t m) { return m + kMaxPend; }
 void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0);
-void launch_shard_gather(hipStream_t s, const Cand* lout, const double* A, int64_t lda, int m,
-                         const double* Y, int64_t ldy, int64_t c0, double* send);
-void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t rec, int m, int k,
+void launch_shard_pick(hipStream_t s, const Cand* recv, int nranks, const double* A, int64_t lda, int m,
+                       const double* Y, int64_t ldy, int64_t c0, int nloc, uint64_t* colsend);
+// colrecv null (one rank): the winner's column and pending y's are read from this rank's A / Y
+void launch_shard_commit(hipStream_t s, const Cand* recv, int nranks, const uint64_t* colrecv, int m, int k,
                          RrluState* st, double reltol, double abstol, int32_t* rowpos,
                          int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
                          int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
@@ -265,6 +273,11 @@ void launch_cache_gather_points(hipStream_t s, const int64_t* miss, int64_t nmis
 void launch_cache_fill(hipStream_t s, const int64_t* miss, int64_t nmiss, const double* v, double* vals,
                        unsigned* state, int64_t mR, double* out, int64_t ldo);
 void launch_cache_dups(hipStream_t s, const CacheProbeArgs& a, int64_t ndup);
+void launch_cache_unclaim(hipStream_t s, const int64_t* miss, int64_t nmiss, unsigned long long* keys,
+                          unsigned* state);
+void launch_cache_lookup(hipStream_t s, const int32_t* X, int64_t npts, int L, const int64_t* coeff,
+                         const unsigned long long* keys, const double* vals, const unsigned* state, int64_t cap,
+                         int32_t* found, double* out);
 void launch_cache_maxabs(hipStream_t s, const double* out, int64_t mR, int64_t n, int64_t ldo,
                          unsigned long long* maxbits);
 void launch_cache_rehash(hipStream_t s, const unsigned long long* ok, const double* ov, int64_t ocap,

@@ -312,7 +312,7 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     if (threadIdx.x == 0) {
         __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (sel.lout) {  // column-sharded: this rank's winner, committed after the exchange
-            *sel.lout = Cand{w.v, w.val, w.cpos, w.rpos, w.pc, w.pr};
+            *sel.lout = Cand{w.v, w.val, w.cpos, w.rpos, w.v >= 0.0 ? (int32_t)(w.pc + sel.pc_off) : -1, w.pr};
             return;
         }
         commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
@@ -1539,7 +1539,7 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 template <int P>
 static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs& g, int grid) {
     const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
-                      g.ticket, g.reltol, g.abstol,  g.selk,    g.lout};
+                      g.ticket, g.reltol, g.abstol,  g.selk,    g.lout, g.pc_off};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
                   g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
     if (shadow && kShHalf) {
@@ -2066,10 +2066,12 @@ __device__ __forceinline__ bool mid_grid_sync(unsigned* count, unsigned& epoch, 
         const unsigned old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int bad = 0;
         if (old + 1 < target) {
-            unsigned spins = 0;
+            // bounded by wall time (100 MHz counter): 4 ms is ~300x a pivot's barrier wait, so only
+            // workgroups that are not co-resident (another stream or process holding CUs) reach it
+            const unsigned long long t0 = wall_clock64();
             while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24) ||
+                if (wall_clock64() - t0 > 400000ull ||
                     __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                     bad = 1;  // a peer is missing or has failed: give up instead of hanging
                     __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2345,64 +2347,66 @@ void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0)
 __device__ __forceinline__ double bits_dbl(uint64_t u) { return __longlong_as_double((long long)u); }
 __device__ __forceinline__ uint64_t dbl_bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
-// Record: [0] abs2, [1] value, [2] column | row position (int32 pair), [3] global physical column |
-// physical row, [4, 4 + kMaxPend) the pending y's of that column, then its m stale values.
-__global__ __launch_bounds__(256) void k_shard_gather(const Cand* __restrict__ lout, const double* __restrict__ A,
-                                                      int64_t lda, int m, const double* __restrict__ Y,
-                                                      int64_t ldy, int64_t c0, double* __restrict__ send) {
-    const Cand c = *lout;
-    const bool has = c.v >= 0.0;
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0) {
-        if (tid == 0) {
-            send[0] = c.v;
-            send[1] = c.val;
-            send[2] = bits_dbl((uint64_t)(uint32_t)c.cpos | ((uint64_t)(uint32_t)c.rpos << 32));
-            const int32_t pcg = has ? (int32_t)(c0 + c.pcol) : -1;
-            send[3] = bits_dbl((uint64_t)(uint32_t)pcg | ((uint64_t)(uint32_t)c.prow << 32));
+// every block reduces the N published candidates in rank order (the reference's tie order) to the
+// same winner; -1: no rank has a candidate
+__device__ __forceinline__ int shard_winner(const Cand* __restrict__ recv, int nranks, CandR& w) {
+    w = cand_none();
+    int wr = -1;
+    for (int r = 0; r < nranks; ++r) {
+        const Cand h = recv[r];
+        if (h.v >= 0.0 && cand_better(h.v, h.cpos, h.rpos, w.v, w.cpos, w.rpos)) {
+            w = CandR{h.v, h.val, h.cpos, h.rpos, h.pcol, h.prow};
+            wr = r;
         }
-        if (tid < kMaxPend) send[4 + tid] = has ? Y[(int64_t)tid * ldy + c.pcol] : 0.0;
     }
-    // the column: every block a 1024-row slice, 4 independent loads per thread
-    const double* col = A + (int64_t)(has ? c.pcol : 0) * lda;
-    const int i0 = blockIdx.x * 1024 + tid;
+    return wr;
+}
+
+// the rank owning the winning column writes [pending y's | stale column] as bits, the others zeros
+__global__ __launch_bounds__(256) void k_shard_pick(const Cand* __restrict__ recv, int nranks,
+                                                    const double* __restrict__ A, int64_t lda, int m,
+                                                    const double* __restrict__ Y, int64_t ldy, int64_t c0, int nloc,
+                                                    uint64_t* __restrict__ colsend) {
+    __shared__ int own_s;
+    if (threadIdx.x == 0) {
+        CandR w;
+        const int wr = shard_winner(recv, nranks, w);
+        own_s = (wr >= 0 && w.pc >= c0 && w.pc < c0 + nloc) ? (int)(w.pc - c0) : -1;
+    }
+    __syncthreads();
+    const int own = own_s;
+    const double* col = A + (int64_t)(own >= 0 ? own : 0) * lda;
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPend)
+        colsend[threadIdx.x] = own >= 0 ? dbl_bits(Y[(int64_t)threadIdx.x * ldy + own]) : 0ull;
+    const int i0 = blockIdx.x * 1024 + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = i0 + u * 256;
-        if (i < m) send[kShardHdr + i] = has ? col[i] : 0.0;
+        if (i < m) colsend[kMaxPend + i] = own >= 0 ? dbl_bits(col[i]) : 0ull;
     }
 }
 
-void launch_shard_gather(hipStream_t s, const Cand* lout, const double* A, int64_t lda, int m,
-                         const double* Y, int64_t ldy, int64_t c0, double* send) {
-    hipLaunchKernelGGL(k_shard_gather, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, lout, A,
-                       lda, m, Y, ldy, c0, send);
+void launch_shard_pick(hipStream_t s, const Cand* recv, int nranks, const double* A, int64_t lda, int m,
+                       const double* Y, int64_t ldy, int64_t c0, int nloc, uint64_t* colsend) {
+    hipLaunchKernelGGL(k_shard_pick, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, recv,
+                       nranks, A, lda, m, Y, ldy, c0, nloc, colsend);
 }
 
-// Every block reduces the N records (rank order, the reference's tie order) to the same winner and
-// installs its slice of the ghost column; block 0 alone commits (stop test, maps, st). A ghost
-// installed after a stop is never read (the passes return at once).
-__global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__ recv, int nranks, int64_t rec,
-                                                      int m, int k, RrluState* st, double reltol, double abstol,
-                                                      int32_t* rowpos, int32_t* colpos_g, int64_t* rowphys,
-                                                      int64_t* colphys_g, double* pivvals, int32_t* colpos_loc,
-                                                      int64_t c0, int nloc, double* A, int64_t lda, double* Y,
-                                                      int64_t ldy) {
-    __shared__ int win;
+// Every block reduces the N candidates to the same winner and installs its slice of the ghost
+// column; block 0 alone commits (stop test, maps, st). A ghost installed after a stop is never read
+// (the passes return at once). colrecv null: one rank, the winning column is this rank's own.
+__global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ recv, int nranks,
+                                                      const uint64_t* __restrict__ colrecv, int m, int k,
+                                                      RrluState* st, double reltol, double abstol, int32_t* rowpos,
+                                                      int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g,
+                                                      double* pivvals, int32_t* colpos_loc, int64_t c0, int nloc,
+                                                      double* A, int64_t lda, double* Y, int64_t ldy) {
+    __shared__ int win_s, own_s;
     if (threadIdx.x == 0) {
-        CandR w = cand_none();
-        int wr = -1;
-        for (int r = 0; r < nranks; ++r) {
-            const double* h = recv + (int64_t)r * rec;
-            const uint64_t b2 = dbl_bits(h[2]), b3 = dbl_bits(h[3]);
-            const CandR c{h[0], h[1], (int)(uint32_t)b2, (int)(uint32_t)(b2 >> 32), (int)(uint32_t)b3,
-                          (int)(uint32_t)(b3 >> 32)};
-            if (c.v >= 0.0 && cand_better(c.v, c.cpos, c.rpos, w.v, w.cpos, w.rpos)) {
-                w = c;
-                wr = r;
-            }
-        }
-        win = wr;
+        CandR w;
+        const int wr = shard_winner(recv, nranks, w);
+        win_s = wr;
+        own_s = (wr >= 0 && w.pc >= c0 && w.pc < c0 + nloc) ? (int)(w.pc - c0) : -1;
         if (blockIdx.x == 0 && !st->done) {
             const int64_t rk = rowphys[k], ck = colphys_g[k];
             commit_pivot(k, w, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals, rk, ck);
@@ -2416,30 +2420,40 @@ __global__ __launch_bounds__(256) void k_shard_commit(const double* __restrict__
         }
     }
     __syncthreads();
-    // the ghost: the winner's stale column and its pending y's (every trailing value NaN: no winner,
-    // pivot NaN, the column is NaN as the reference's would be after the division)
-    const int wr = win;
-    const double* src = wr >= 0 ? recv + (int64_t)wr * rec : nullptr;
+    // the ghost: the winner's stale column and its pending y's (no winner: every trailing value
+    // NaN, as the reference's column would be after the division by a NaN pivot)
+    const int wr = win_s, own = own_s;
     double* gcol = A + (int64_t)nloc * lda;
     const double qnan = __longlong_as_double(0x7ff8000000000000LL);
+    const double* lcol = A + (int64_t)(own >= 0 ? own : 0) * lda;
     const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // all reads before any write: own may alias nothing, but be safe
+        const int i = i0 + u * 256;
+        v[u] = qnan;
+        if (i < m && wr >= 0) v[u] = colrecv ? bits_dbl(colrecv[kMaxPend + i]) : lcol[i];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = i0 + u * 256;
-        if (i < m) gcol[i] = src ? src[kShardHdr + i] : qnan;
+        if (i < m) gcol[i] = v[u];
     }
-    if (blockIdx.x == 0 && threadIdx.x < kMaxPend)
-        Y[(int64_t)threadIdx.x * ldy + nloc] = src ? src[4 + threadIdx.x] : 0.0;
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPend) {
+        const int t = threadIdx.x;
+        const double y = wr < 0 ? 0.0 : colrecv ? bits_dbl(colrecv[t]) : Y[(int64_t)t * ldy + own];
+        Y[(int64_t)t * ldy + nloc] = y;
+    }
 }
 
-void launch_shard_commit(hipStream_t s, const double* recv, int nranks, int64_t rec, int m, int k,
+void launch_shard_commit(hipStream_t s, const Cand* recv, int nranks, const uint64_t* colrecv, int m, int k,
                          RrluState* st, double reltol, double abstol, int32_t* rowpos,
                          int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
                          int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
                          int64_t ldy) {
     hipLaunchKernelGGL(k_shard_commit, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, recv,
-                       nranks, rec, m, k, st, reltol, abstol,
-                       rowpos, colpos_g, rowphys, colphys_g, pivvals, colpos_loc, c0, nloc, A, lda, Y, ldy);
+                       nranks, colrecv, m, k, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals,
+                       colpos_loc, c0, nloc, A, lda, Y, ldy);
 }
 
 }  // namespace tci

@@ -11,6 +11,7 @@ from .cachedfunction import CachedFunction
 from .contraction import Contraction, contract, contract_naive, contract_TCI
 from .distributed import (Comm, DeviceComm, HostExchange, ShardedBatchEvaluator, column_blocks, rrlu_sharded,
                           rrlu_sharded_factors)
+from .hostfunction import HostFunctionEvaluator
 from .globalpivotfinder import AbstractGlobalPivotFinder, DefaultGlobalPivotFinder, FixedGlobalPivotFinder
 from .matrixlu import (DeviceMatrix, colindices, dgemm_device, diag, lastpivoterror, ldiv, left, npivots,
                        pivoterrors, right, rowindices, rrLU, rrlu, rrlu_inplace_device, schur_update_device,

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TCI_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libtci_hip.so"))
 
-TCI_OK, TCI_ERR_ARG, TCI_ERR_NAN, TCI_ERR_NONSQ, TCI_ERR_DEVICE, TCI_ERR_NOMEM = range(6)
+TCI_OK, TCI_ERR_ARG, TCI_ERR_NAN, TCI_ERR_NONSQ, TCI_ERR_DEVICE, TCI_ERR_NOMEM, TCI_ERR_HOST = range(7)
 
 i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
@@ -61,6 +61,7 @@ SIGNATURES = {
     "tci_set_dense_mfma": ([vp, C.c_int], C.c_int),
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),
+    "tci_func_create_host": ([vp, vp, vp, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_batcheval_d": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_rrlu_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, i64, pi64, pdbl],
@@ -105,6 +106,7 @@ SIGNATURES = {
     "tci_cache_clear": ([vp], C.c_int),
     "tci_cache_size": ([vp, pi64], C.c_int),
     "tci_cache_dump_h": ([vp, vp, vp, i64, pi64], C.c_int),
+    "tci_cache_lookup_h": ([vp, vp, i64, vp, vp], C.c_int),
     "tci_cache_batcheval_d": ([vp, vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl, pi64], C.c_int),
     "tci_cache_batcheval_h": ([vp, vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl, pi64], C.c_int),
     "tci_comm_unique_id": ([vp, pi64], C.c_int),
@@ -122,8 +124,9 @@ SIGNATURES = {
     "tci_memcpy_d2d": ([vp, vp, vp, i64], C.c_int),
 }
 
-# tci_exchange_fn (include/tci_hip.h): int (*)(void* user, const double* d_send, double* d_recv, int64 count)
-EXCHANGE_FN = C.CFUNCTYPE(C.c_int, vp, vp, vp, i64)
+# tci_exchange_fn (include/tci_hip.h): int (*)(void* user, int op, const void* d_send, void* d_recv,
+# int64 count) -- op 0 all-gather, op 1 element-wise uint64 max, count 8-byte words
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, vp, C.c_int, vp, vp, i64)
 
 _lib = None
 _lock = threading.Lock()
@@ -146,6 +149,16 @@ def load():
                 fn.restype = res
             _lib = lib
     return _lib
+
+
+_host_exc = threading.local()
+
+
+def set_host_exception(e):
+    """Records the exception a host callback (tci_func_create_host) raised; Context.check re-raises
+    it when the library returns TCI_ERR_HOST, so an error inside the user's f propagates as it
+    would from f in the reference."""
+    _host_exc.e = e
 
 
 def ptr(a):
@@ -231,6 +244,11 @@ class Context:
         if st == TCI_OK:
             return
         msg = self.lib.tci_last_error(self.h).decode(errors="replace")
+        if st == TCI_ERR_HOST:
+            e = getattr(_host_exc, "e", None)
+            _host_exc.e = None
+            if e is not None:
+                raise e
         if st == TCI_ERR_ARG:
             raise TCIArgumentError(st, msg)
         if st == TCI_ERR_DEVICE or st == TCI_ERR_NOMEM:

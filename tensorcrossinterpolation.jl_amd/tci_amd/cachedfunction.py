@@ -56,6 +56,15 @@ class _DeviceMemo:
                                                      C.byref(n)))
         return keys[: n.value], vals[: n.value]
 
+    def lookup(self, X):
+        """(found, values) of the points X (npts x L) -- one device probe, no table dump."""
+        X = np.ascontiguousarray(X, np.int32)
+        found = np.zeros(max(len(X), 1), np.int32)
+        vals = np.zeros(max(len(X), 1))
+        self.ctx.check(self.ctx.lib.tci_cache_lookup_h(self.h, self._lib.ptr(X), len(X), self._lib.ptr(found),
+                                                       self._lib.ptr(vals)))
+        return found[: len(X)].astype(bool), vals[: len(X)]
+
     def pi(self, f, I, J, M):
         """(Pi as a Fortran (|I| D) x |J| array, max|Pi|, number of misses evaluated)."""
         ctx, _lib = self.ctx, self._lib
@@ -108,7 +117,8 @@ class CachedFunction:
 
     def haskey(self, x):
         if self._memo is not None:
-            return self.key(x) in set(int(k) for k in self._memo.dump()[0])
+            self.key(x)  # argument check
+            return bool(self._memo.lookup(np.asarray([x], np.int32).reshape(1, self.L))[0][0])
         return self.key(x) in self.cache
 
     def cacheddata(self):

@@ -92,6 +92,12 @@ class Comm:
         self.dist.all_gather_into_tensor(out, t, group=self.group)
         return out.cpu().numpy()
 
+    def allreduce_max_u64(self, words):
+        """element-wise max over the ranks of uint64 vectors (bit patterns; equal lengths)."""
+        w = np.ascontiguousarray(words, np.uint64)
+        allb = self.allgather_flat(w.view(np.float64)).reshape(self.world, -1)
+        return np.ascontiguousarray(allb).view(np.uint64).max(axis=0)
+
     def allreduce_sum(self, a):
         torch = self.torch
         a = np.asarray(a, np.float64)
@@ -285,9 +291,13 @@ class DeviceComm:
 
 
 class HostExchange:
-    """The tci_exchange_fn hook over a host `Comm` (gloo): device -> host, all-gather, host ->
+    """The tci_exchange_fn hook over a host `Comm` (gloo): device -> host, collective, host ->
     device. For ranks that cannot form an RCCL communicator (several ranks on one GPU, CPU-side
-    transports); correct everywhere, slower than DeviceComm."""
+    transports); correct everywhere, slower than DeviceComm.
+
+    Failures are collective: every rank always enters the host collective, with an ok flag next to
+    its data, and every rank reports failure when any rank's flag is down -- so a copy that fails
+    on one rank cannot leave the others waiting in the next exchange."""
 
     def __init__(self, ctx, comm):
         from . import _lib
@@ -295,14 +305,30 @@ class HostExchange:
         self.ctx, self.comm = ctx, comm
         self._lib = _lib
 
-        def fn(user, d_send, d_recv, count):
+        def fn(user, op, d_send, d_recv, count):
+            count = int(count)
+            ok = 1.0
+            buf = np.zeros(count, np.uint64)
             try:
-                buf = np.empty(int(count))
                 ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, _lib.ptr(buf), d_send, buf.nbytes))
-                allb = comm.allgather_flat(buf)
-                ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, d_recv, _lib.ptr(allb), allb.nbytes))
+            except Exception:
+                ok = 0.0
+            try:
+                if op == 0:  # all-gather of the words, with the flag as one extra word per rank
+                    allb = comm.allgather_flat(np.concatenate([buf.view(np.float64), [ok]]))
+                    allb = allb.reshape(comm.world, count + 1)
+                    if not np.all(allb[:, count] == 1.0):
+                        return 1
+                    out = np.ascontiguousarray(allb[:, :count]).ravel()
+                else:  # element-wise uint64 max: all-gather and reduce (bit patterns, no float compare)
+                    allb = comm.allgather_flat(np.concatenate([buf.view(np.float64), [ok]]))
+                    allb = allb.reshape(comm.world, count + 1)
+                    if not np.all(allb[:, count] == 1.0):
+                        return 1
+                    out = np.ascontiguousarray(allb[:, :count]).view(np.uint64).max(axis=0)
+                ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, d_recv, _lib.ptr(np.ascontiguousarray(out)), out.nbytes))
                 return 0
-            except Exception:  # reported to the library as a failed exchange
+            except Exception:
                 return 1
 
         self.fn = _lib.EXCHANGE_FN(fn)  # keep a reference for the library's lifetime of the call
@@ -345,8 +371,22 @@ def rrlu_sharded_factors(ctx, m, n, npivot, host_comm=None):
     U = np.zeros((npivot, n), order="F")
     if npivot == 0:
         return L, U
-    ctx.check(ctx.lib.tci_rrlu_sharded_factors_h(ctx.h, L.ctypes.data_as(C.c_void_p),
-                                                 U.ctypes.data_as(C.c_void_p), npivot))
+    st = ctx.lib.tci_rrlu_sharded_factors_h(ctx.h, L.ctypes.data_as(C.c_void_p), U.ctypes.data_as(C.c_void_p),
+                                            npivot)
     if host_comm is not None and host_comm.world > 1:
+        # the NaN checks (matrixlu.jl:376-381) see only this rank's columns of U: agree on the
+        # status first, so that every rank raises together instead of one rank raising while the
+        # others wait in the sum below
+        codes = host_comm.allgather_flat(np.array([float(st)]))
+        bad = [int(c) for c in codes if c != 0]
+        if bad:
+            if st == 0:
+                st = bad[0]
+                from . import _lib
+                raise _lib.TCIError(st, "lu.U contains NaNs" if st == _lib.TCI_ERR_NAN else
+                                    f"rrlu_sharded_factors failed on another rank (code {st})")
+            ctx.check(st)
         U = host_comm.allreduce_sum(U)
+    else:
+        ctx.check(st)
     return L, U

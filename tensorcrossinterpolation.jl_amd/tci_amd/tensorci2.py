@@ -402,7 +402,7 @@ class TensorCI2:
                  checkbatchevaluatable=False, checkconvglobalpivot=True, rng=None):
         """optimize! (tensorci2.jl:1018-1172). Returns (ranks, errors ./ errornormalization)."""
         errors, ranks, nglobalpivots = [], [], []
-        if checkbatchevaluatable and not isinstance(f, GPUBatchEvaluator):
+        if checkbatchevaluatable and not (isinstance(f, GPUBatchEvaluator) or getattr(f, "is_batch", False)):
             raise RuntimeError("Function `f` is not batch evaluatable")
         if 0 < nsearchglobalpivot < maxnglobalpivot:
             raise RuntimeError("nsearchglobalpivot < maxnglobalpivot!")
@@ -513,7 +513,8 @@ def reconstractglobalpivotsfromijset(localdims, Isets, Jsets):
 def _native_ok(f):
     """The native sweep driver takes a real device integrand (a GPUBatchEvaluator's tci_func)."""
     return (hasattr(f, "h") and getattr(f, "ctx", None) is not None and not getattr(f, "is_complex", False)
-            and not getattr(f, "shard_rrlu", False) and type(f).__name__ == "GPUBatchEvaluator")
+            and not getattr(f, "shard_rrlu", False)
+            and type(f).__name__ in ("GPUBatchEvaluator", "HostFunctionEvaluator"))
 
 
 class _NativeTCI2:

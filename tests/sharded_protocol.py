@@ -3,9 +3,12 @@ tci_rrlu_sharded_d (include/tci_hip.h), for the CPU (gloo) 
 
 Each rank holds the columns [c0, c0 + nloc) of the matrix. Per pivot k it finds the argmax of
 abs2 over ITS part of the trailing block in the reference's scan order (submatrixargmax,
-/root/reference/src/matrixlu.jl:46-87: column position, then row position, strict '>'), sends
-(abs2, value, column position, row position, global column, row) and that column's current values
-to every rank (all-gather), and every rank commits the same winner: stop test of _optimizerrlu!
+/root/reference/src/matrixlu.jl:46-87: column position, then row position, strict '>'), sends the
+candidate (abs2, value, column position, row position, global column, row) to every rank
+(all-gather); every rank reduces the candidates to the same winner, the rank owning the winning
+column contributes that column's current values and the others zeros, and an element-wise max of
+the contributions as uint64 bit patterns gives every rank the column (candidate first: 8 m bytes
+per pivot, not N x 8 m); then every rank commits the same winner: stop test of _optimizerrlu!
 (matrixlu.jl:359-368), swaprow!/swapcol! as position maps, normalisation and the rank-1 update of
 addpivot! (matrixlu.jl:295-322, separate multiply and subtract) on its own columns, with the pivot
 column taken from the winner's record. The result must equal the unsharded oracle bit for bit --
@@ -15,10 +18,12 @@ device kernels (those are checked against the same oracle in tests/test_gpu_shar
 import numpy as np
 
 
-def sharded_rrlu(A_loc, m, n, c0, allgather, maxrank=None, reltol=1e-14, abstol=0.0, leftorth=True):
+def sharded_rrlu(A_loc, m, n, c0, allgather, allreduce_max_u64, maxrank=None, reltol=1e-14, abstol=0.0,
+                 leftorth=True):
     """A_loc: this rank's m x nloc block (physical = original indices). allgather(vec) returns the
-    rank-major concatenation of every rank's equal-length float64 vector. Returns npivot, error,
-    rowperm, colperm (0-based), L (m x np), this rank's U columns (np x n, zeros elsewhere)."""
+    rank-major concatenation of every rank's equal-length float64 vector; allreduce_max_u64(words)
+    the element-wise max over the ranks of uint64 vectors. Returns npivot, error, rowperm, colperm
+    (0-based), L (m x np), this rank's U columns (np x n, zeros elsewhere)."""
     A = np.array(A_loc, dtype=np.float64, order="F")
     nloc = A.shape[1]
     mr = min(m, n) if maxrank is None else min(int(maxrank), m, n)
@@ -43,16 +48,18 @@ def sharded_rrlu(A_loc, m, n, c0, allgather, maxrank=None, reltol=1e-14, abstol=
             _, _, i, j = min(key)
             best = (float(mx), float(sub[i, j]), int(colpos[c0 + Cc[j]]), int(rowpos[R[i]]), int(c0 + Cc[j]),
                     int(R[i]))
-        jl = best[4] - c0 if best[4] >= 0 else 0
-        rec = np.concatenate([np.array(best, np.float64), A[:, jl] if best[4] >= 0 else np.zeros(m)])
-        allr = allgather(rec).reshape(-1, 6 + m)
+        allr = allgather(np.array(best, np.float64)).reshape(-1, 6)
         win = None
         for r in range(allr.shape[0]):
             c = tuple(allr[r, :6])
             c = (c[0], c[1], int(c[2]), int(c[3]), int(c[4]), int(c[5]))
-            if c[4] >= 0 and (win is None or _better(c, win[0])):
-                win = (c, allr[r, 6:])
-        (a2, val, cp, rp, pc, pr), col = win
+            if c[4] >= 0 and (win is None or _better(c, win)):
+                win = c
+        a2, val, cp, rp, pc, pr = win
+        # the owner of the winning column contributes it (as bits), the others zeros
+        mine = c0 <= pc < c0 + nloc
+        contrib = A[:, pc - c0].copy().view(np.uint64) if mine else np.zeros(m, np.uint64)
+        col = np.ascontiguousarray(allreduce_max_u64(contrib), np.uint64).view(np.float64)
         err = abs(val)
         error = err
         if (err < reltol * maxerror or err < abstol) and k > 0:

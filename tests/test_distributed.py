@@ -194,7 +194,8 @@ def _shard_worker(rank, world, port, outdir):
         for name, (A, kw) in cases.items():
             m, n = A.shape
             j0, j1 = column_blocks(n, world)[rank]
-            npv, err, rp, cp, L, U = sharded_rrlu(A[:, j0:j1], m, n, j0, comm.allgather_flat, **kw)
+            npv, err, rp, cp, L, U = sharded_rrlu(A[:, j0:j1], m, n, j0, comm.allgather_flat,
+                                                  comm.allreduce_max_u64, **kw)
             U = comm.allreduce_sum(U)
             ref = O.OracleLU(A, maxrank=kw.get("maxrank", min(m, n)), reltol=kw.get("reltol", 1e-14),
                              leftorthogonal=kw.get("leftorth", True))
@@ -209,8 +210,9 @@ def _shard_worker(rank, world, port, outdir):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_rrlu_protocol_gloo(tmp_path, world):
-    """The column-sharded rrLU protocol (local argmax, all-gather of candidates + columns, the same
-    commit on every rank) reproduces the unsharded oracle bit for bit (tests/sharded_protocol.py)."""
+    """The column-sharded rrLU protocol (local argmax, all-gather of the candidates, the winning
+    column from its owner through a uint64 max, the same commit on every rank) reproduces the
+    unsharded oracle bit for bit (tests/sharded_protocol.py)."""
     import torch.multiprocessing as mp
 
     mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)

@@ -97,3 +97,40 @@ def test_no_gpu_raises_loudly():
         pytest.skip("GPU present")
     with pytest.raises(tci_amd.TCIError):
         tci_amd.Context(0)
+
+
+@pytest.mark.parametrize("mode", ["pointwise", "threads", "vectorized", "batch"])
+@pytest.mark.parametrize("M", [0, 1])
+def test_host_function_batch_layout_vs_oracle(mode, M):
+    """HostFunctionEvaluator's host batch (the array its callback hands the library) has the
+    layout of _batchevaluate_dispatch (batcheval.jl:154-174): element (i, c, j) at i + m c + m D j,
+    bitwise the oracle's batch evaluation of the same integer-exact f (f = sum(x), kind 0)."""
+    from tci_amd.hostfunction import HostFunctionEvaluator
+    ld = [3, 4, 5, 2, 3]
+    ev = object.__new__(HostFunctionEvaluator)  # host side only: no device context
+    ev.localdims, ev.L, ev._pool = ld, len(ld), None
+    ev.threads, ev.vectorized, ev.is_batch = (4 if mode == "threads" else 1), mode == "vectorized", mode == "batch"
+    if mode == "vectorized":
+        ev.f = lambda X: X.sum(axis=1).astype(float)
+    elif mode == "batch":
+        def fb(I, J, MM):
+            s = I.sum(1)[:, None] + J.sum(1)[None, :]
+            if MM == 0:
+                return s.astype(float)
+            d = ld[I.shape[1]]
+            return (s[:, None, :] + np.arange(1, d + 1)[None, :, None]).astype(float)
+        ev.f = fb
+    else:
+        ev.f = lambda x: float(sum(x))
+    rng = np.random.default_rng(M)
+    nl = 2
+    I = np.stack([rng.integers(1, d + 1, 23) for d in ld[:nl]], 1).astype(np.int32)
+    J = np.stack([rng.integers(1, d + 1, 17) for d in ld[nl + M:]], 1).astype(np.int32)
+    got = ev._batch_host(I, J, M)
+    ref, mx = O.batcheval(0, [0.0], ld, I, J, M)
+    D = ld[nl] if M else 1
+    assert np.array_equal(got, ref.reshape((23 * D, 17), order="F"))
+    out, gmx = ev.pi(I, J, M)
+    assert gmx == mx
+    if ev._pool is not None:
+        ev._pool.shutdown()
