@@ -29,34 +29,53 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2):
+def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1):
     """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-1 with k % stride == 0
-    (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block. Exact passes: a
-    read-only pass reads 8 B/element, every nb-th pass (pending count reaches nb; never the last)
-    also writes 8 B/element back. With the certified shadow search (sh_bytes = 2
-    for the fp16 shadow, 4 for fp32) a read-only pass streams the shadow instead, and a
-    write-back pass also writes it (8 + 8 + sh_bytes B/element); with the fp16 shadow pass 0 is
-    exact and writes the shadow of A (8 + 2). The exact re-reads of candidate elements are
-    data-dependent and not counted. Returns (read_only, write_back) as (bytes, launches)."""
+    (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block, following the host
+    schedule of tci_abi.cpp rrlu_device. Exact passes: a read-only pass reads 8 B/element, every
+    nb-th pass also writes 8 B/element back. With the certified shadow search (DESIGN.md K2;
+    sh_bytes = 2 for the fp16 shadow, 4 for fp32) a read-only pass streams the shadow instead; with
+    the fp16 shadow pass 0 is exact and writes the shadow of A (8 + 2), and the two-level epoch
+    ends every shadow epoch of nb pivots with a refresh (the shadow read and rewritten: 2 + 2) and
+    every epochs-th with a write-back (8 read + 8 + 2 written). The exact re-reads of candidate
+    elements and the pending x / y vectors are data-dependent / small and not counted.
+    Returns (read_only, write_back, refresh) as (bytes, launches)."""
+    if not (shadow and sh_bytes == 2 and 2 <= nb <= 15):
+        epochs = 1
+    epochs = max(1, min(epochs, 32 // nb))
+    nbx = nb * epochs
     ro_per, wb_per = (float(sh_bytes), 16.0 + sh_bytes) if shadow else (8.0, 16.0)
-    ro_b = wb_b = 0.0
-    ro_n = wb_n = 0
-    pend = 0
+    ro_b = wb_b = rf_b = 0.0
+    ro_n = wb_n = rf_n = 0
+    te = ts = 0
     for k in range(r):
-        pend += 1
+        PE, PS = k - te + 1, k - ts + 1
+        last = k + 1 >= r
+        flush = PE >= nbx and not last
+        refresh = not flush and epochs > 1 and PS >= nb and not last
         elems = float(m - k - 1) * float(n - k - 1)
-        flush = pend >= nb and k + 1 < r
         if flush:
-            pend = 0
+            te = ts = k + 1
+        elif refresh:
+            ts = k + 1
         if k % stride:
             continue
         if flush:
             wb_b += wb_per * elems
             wb_n += 1
+        elif refresh:
+            rf_b += 2.0 * sh_bytes * elems
+            rf_n += 1
         else:
             ro_b += (8.0 + sh_bytes if (shadow and sh_bytes == 2 and k == 0) else ro_per) * elems
             ro_n += 1
-    return (ro_b, ro_n), (wb_b, wb_n)
+    return (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n)
+
+
+def len_sched(m, n, r, nb, epochs, shadow, sh_bytes):
+    """(read-only, write-back, refresh) launch counts of one factorisation."""
+    (_, a), (_, b), (_, c) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes, epochs)
+    return a, b, c
 
 
 def main():
@@ -74,10 +93,13 @@ def main():
                     help="diagnostic: no HIP events in the timed region (no roofline line)")
     ap.add_argument("--timing-stride", type=int, default=5,
                     help="time the rrLU pass of every s-th pivot with HIP events")
-    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "11")),
-                    help="deferred-update depth of the rrLU (results are identical for every nb)")
+    ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "10")),
+                    help="shadow epoch of the rrLU: pending updates before the shadow is rewritten "
+                         "(results are identical for every nb)")
+    ap.add_argument("--epochs", type=int, default=int(os.environ.get("TCI_RRLU_EPOCHS", "3")),
+                    help="shadow epochs per fp64 write-back (two-level epoch; identical results)")
     ap.add_argument("--no-shadow", action="store_true",
-                    help="exact fp64 read-only passes instead of the certified fp32 shadow search")
+                    help="exact fp64 read-only passes instead of the certified fp16 shadow search")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,6 +116,7 @@ def main():
     # rehearse the multi-rank control flow on a one-GPU machine
     ctx = T.context(int(os.environ.get("TCI_BENCH_DEVICE", local_rank)))
     ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, args.nb))
+    ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, args.epochs))
     shadow = not args.no_shadow and os.environ.get("TCI_RRLU_SHADOW", "1") != "0"
     ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, int(shadow)))
     m, n, r = args.m, args.n, args.r
@@ -131,6 +154,7 @@ def main():
     assert np_ == min(r, m, n), np_
     wb_ms, wb_launches = ctx.kernel_stats(0)
     ro_ms, ro_launches = ctx.kernel_stats(2)
+    rf_ms, rf_launches = ctx.kernel_stats(23)
     by_pending = {}  # read-only pass time by pending depth P (sub-families 3 + P)
     for P in range(1, args.nb):
         pm, pn = ctx.kernel_stats(3 + P)
@@ -153,7 +177,7 @@ def main():
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
     sh_bytes = int(ctx.lib.tci_rrlu_shadow_bytes())
-    (ro_b, ro_n), (wb_b, wb_n) = pass_bytes(m, n, r, nb, stride, shadow, sh_bytes)
+    (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n) = pass_bytes(m, n, r, nb, stride, shadow, sh_bytes, args.epochs)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
@@ -172,8 +196,8 @@ def main():
                                                        wb_b, wb_n)
     # whole-step context: every pass's algorithmic bytes (stride 1), the initial argmax pass (8 B)
     # and the copy rrlu makes (16 B per element), over the measured step time
-    (ro_all, _), (wb_all, _) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes)
-    step_bytes = ro_all + wb_all + 24.0 * m * n
+    (ro_all, _), (wb_all, _), (rf_all, _) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes, args.epochs)
+    step_bytes = ro_all + wb_all + rf_all + 24.0 * m * n
     avg_launch_ms = dom_ms / max(dom_launches, 1)
     bytes_per_launch = dom_bytes / max(dom_n, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -183,7 +207,12 @@ def main():
              "read_only_pass": {"launches": ro_launches, "avg_ms": round(ro_ms / max(ro_launches, 1), 5),
                                 "GBps": round(ro_b / max(ro_n, 1) / (ro_ms / max(ro_launches, 1) * 1e-3) / 1e9, 1)
                                 if ro_launches else None,
-                                "avg_ms_by_pending_depth": by_pending}}
+                                "avg_ms_by_pending_depth": by_pending},
+             "refresh_pass": {"launches": rf_launches, "avg_ms": round(rf_ms / max(rf_launches, 1), 5),
+                              "GBps": round(rf_b / max(rf_n, 1) / (rf_ms / max(rf_launches, 1) * 1e-3) / 1e9, 1)
+                              if rf_launches else None},
+             "step_share": {"write_back": round(wb_ms / max(wb_launches, 1) * len_sched(m, n, r, nb, args.epochs, shadow, sh_bytes)[1]
+                                                / (ms_per_step), 4) if wb_launches else None}}
     out = {
         "metric": "rrLU GFLOP/s at (m,n,r)=(8192,8192,256)" if (m, n, r) == (8192, 8192, 256)
         else f"rrLU GFLOP/s at (m,n,r)=({m},{n},{r})",
@@ -204,7 +233,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
-                     "deferred_depth_nb": nb, "shadow_search": shadow, "shadow_bytes": sh_bytes,
+                     "deferred_depth_nb": nb, "epochs": args.epochs, "shadow_search": shadow, "shadow_bytes": sh_bytes,
                      "step_algorithmic_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                      "step_note": "all passes' algorithmic bytes + initial pass + copy, per measured step; "
                                   "frac above is the dominant (read-only) kernel alone, half of whose "
@@ -238,6 +267,20 @@ def main():
             out["extras"] = extras(T, ctx)
             out["extras"]["pi_lorentz_sharded"] = sh
             out["extras"].update(shr)
+            # the paths that shard, as strong-scaling lines next to the replica
+            # headline: fixed total work over N ranks, max-over-ranks time
+            lines = {"n_gpus": world, "scaling": "strong"}
+            for rec in shr.get("rrlu_sharded", []):
+                lines[f"rrlu_sharded_{rec['m']}x{rec['n']}_r{rec['r']}"] = {
+                    "value": rec["GFLOPs"], "unit": "GFLOP/s", "ms": rec["ms"],
+                    "pivots_equal_unsharded": rec.get("pivots_equal_unsharded")}
+            lines["pi_lorentz_sharded_8192x8192"] = {"value": sh["pi_rows_per_s"], "unit": "Pi-rows/s",
+                                                     "ms": sh["ms_per_pi"]}
+            if "pi_sharded_with_gather" in shr:
+                g = shr["pi_sharded_with_gather"]
+                lines["pi_lorentz_gathered_8192x8192"] = {"value": g["pi_rows_per_s"], "unit": "Pi-rows/s",
+                                                          "ms": g["ms"]}
+            out["scaling_lines"] = lines
     parity_ok = True
     if rank == 0 and not args.no_cpu and world == 1:
         base, cpu_res = cpu_baseline(m, n, r, args.cpu_pivots)
@@ -324,14 +367,25 @@ def sharded_extras(T, ctx, dist, world, rank, full_res):
         dt = tmax(min(times))
         rec = {"m": m, "n": n, "r": r, "ranks": world, "npivot": out[0], "ms": round(dt * 1e3, 3),
                "GFLOPs": round(rrlu_flops(m, n, out[0]) / dt / 1e9, 1),
-               "exchange_bytes_per_pivot": 8 * world * (4 + 16 + m)}
-        if full_res is not None and (m, n, r) == (8192, 8192, 256):
-            npd, rpd, cpd, ped = full_res
+               "exchange": "candidate first: all-gather of 32-B candidates, then the winning column from "
+                           "its owner by an element-wise uint64 max (DESIGN.md 7)",
+               "exchange_bytes_per_pivot": {"allgather_candidates": 32 * world, "allreduce_column": 8 * (m + 32)}}
+        A0.free()
+        W.free()
+        if rank == 0:
+            # the same matrix factorised unsharded on this GPU: pivots, permutations and pivot
+            # errors must be bitwise equal (at 8192^2 the headline step ran it already)
+            if (m, n, r) == (8192, 8192, 256) and full_res is not None:
+                npd, rpd, cpd, ped = full_res
+            else:
+                Af = T.DeviceMatrix(m, n, ctx=ctx)
+                Af.fill_uniform(seed=0)
+                npd, _, rpd, cpd, ped = T.rrlu_inplace_device(Af, maxrank=r, want_perms=True)
+                rpd, cpd = rpd[:m].copy(), cpd[:n].copy()
+                Af.free()
             rec["pivots_equal_unsharded"] = bool(out[0] == npd and np.array_equal(out[2], rpd)
                                                  and np.array_equal(out[3], cpd) and np.array_equal(out[4], ped))
         recs.append(rec)
-        A0.free()
-        W.free()
     res["rrlu_sharded"] = recs
     # Pi assembly + device all-gather of the column blocks (n divisible by world: equal blocks)
     m = n = 8192
@@ -664,7 +718,14 @@ def dense_extras(T, ctx, only_k3=False):
 
 
 def _host_info():
-    info = {"nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        share = len(os.sched_getaffinity(0))
+    except Exception:
+        share = None
+    info = {"nproc_machine": os.cpu_count(), "cpus_allowed": share,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "note": "nproc_machine counts the whole host; the lease's share is OMP_NUM_THREADS "
+                    "(the box sets it to 16) -- cores below is the thread count actually used"}
     try:
         with open("/proc/cpuinfo") as fh:
             for line in fh:
@@ -759,16 +820,29 @@ def cpu_baseline(m, n, r, pivots):
     pe_one = np.concatenate([np.abs(a[np.arange(npv) * (m + 1)]), [err]])
     del a
     fl = rrlu_flops(m, n, npv)
+    # Pi half of the metric: the oracle's _batchevaluate_dispatch restatement (one thread, the
+    # reference's loop) on the bench's 8192^2 L = 20 Lorentzian tables, bounded to 1024 rows
+    rng = np.random.default_rng(1)
+    I = rng.integers(1, 11, (8192, 10)).astype(np.int32)
+    J = rng.integers(1, 11, (8192, 10)).astype(np.int32)
+    rows = 1024
+    t0 = time.perf_counter()
+    O.batcheval(1, [1.0], [10] * 20, I[:rows], J, 0)
+    dtp = time.perf_counter() - t0
+    pi_base = {"value": round(rows / dtp, 1), "unit": "Pi-rows/s", "cores": 1, "kind": "port",
+               "sample": f"first {rows} of 8192 rows x 8192 columns of the L = 20 Lorentzian Pi (bench extras "
+                         f"pi_lorentz inputs), oracle batch evaluation (batcheval.jl:131-175 loop), {dtp:.2f} s"}
     base = {"value": round(rrlu_flops(m, n, npo) / dto / 1e9, 4), "unit": "GFLOP/s", "cores": threads,
             "kind": "port",
             "sample": f"all {npo} of {r} pivots of rrlu on the same {m}x{n} seed-0 matrix, "
-                      f"{dto:.2f} s: oracle/cpu_rrlu_omp.c (OpenMP over {threads} threads, rank-1 update fused "
-                      f"with the next argmax, bitwise the oracle's results)",
+                      f"{dto:.2f} s: oracle/cpu_rrlu_omp.c (OpenMP over {threads} threads = the lease's CPU "
+                      f"share, rank-1 update fused with the next argmax, bitwise the oracle's results)",
             "build": build,
             "host": _host_info(),
             "single_thread": {"value": round(fl / dt / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
                               "sample": f"oracle rrLU (tci_oracle.c, loop-for-loop, 1 thread) first {npv} of {r} "
-                                        f"pivots on the same {m}x{n} matrix, {dt:.1f} s"}}
+                                        f"pivots on the same {m}x{n} matrix, {dt:.1f} s"},
+            "pi_rows": pi_base}
     return base, {"omp": (npo, rpo, cpo, pe_omp), "one": (npv, rp, cp, pe_one)}
 
 

@@ -85,15 +85,20 @@ int tci_ctx_synchronize(tci_ctx* ctx);
  * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
  * 1 = batch evaluation; 3 + P (P = 1..16) = the read-only passes that applied P pending updates
  * (a breakdown of family 2); 20 = site-tensor solve (getrf + getrs of P^T), 21 = MatrixLUCI
- * factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d. */
+ * factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d, 23 = rrLU refresh
+ * passes (read-only passes that also rewrite the fp16 shadow, two-level epoch). */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
-/* Deferred-update depth of the rrLU (1..16; default 11, env TCI_RRLU_NB): up to nb rank-1
- * updates are applied on the fly by read-only passes and written back every nb-th pivot.
- * Results are bitwise identical for every nb. */
+/* Deferred-update depth of the rrLU (1..16; default 10, env TCI_RRLU_NB): up to nb rank-1
+ * updates are applied on the fly by read-only passes, after which the shadow of the values is
+ * rewritten -- by the search itself (a refresh) or, every `epochs`-th time, by a write-back of the
+ * fp64 values. Results are bitwise identical for every nb and epochs. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
+/* Shadow epochs per fp64 write-back (two-level epoch; 1..32 with nb * epochs <= 32;
+ * default 3, env TCI_RRLU_EPOCHS; 1 = write back every nb pivots). */
+int tci_set_rrlu_epochs(tci_ctx* ctx, int epochs);
 /* Matrices with m*n <= 16384 and m + n <= 4096 are factorised by one workgroup holding the whole
  * matrix in LDS (one launch instead of one per pivot); enabled = 0 forces the pass pipeline.
  * Both paths give bitwise identical results. Default on (env TCI_RRLU_SMALL=0: off). */
@@ -207,6 +212,13 @@ int tci_rrlu_c128_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int
 int tci_luci_h(tci_ctx* ctx, const double* A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
                double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
                double* pivoterrors, double* left, double* right, int64_t* npivot);
+
+/* MatrixLUCI on a device matrix (e.g. a Pi all-gathered over RCCL by the sharded evaluation):
+ * d_A (ld lda, even; 16-B aligned) is clobbered as rrlu!'s work matrix; outputs as tci_luci_h, on
+ * the host. */
+int tci_luci_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+                       double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
+                       double* pivoterrors, double* left, double* right, int64_t* npivot);
 
 /* MatrixLUCI{ComplexF64} (matrixluci.jl:55-57, 161-311) on top of the ComplexF64 rrLU:
  * left m x np, right np x n, interleaved (re, im) column-major; otherwise as tci_luci_h. */
@@ -404,6 +416,9 @@ int tci_free_d(tci_ctx* ctx, void* p);
 int tci_memcpy_h2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int tci_memcpy_d2h(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int tci_memcpy_d2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+/* strided copy of `height` rows of `width` bytes (e.g. matrix columns between leading dimensions) */
+int tci_memcpy2d_d2d(tci_ctx* ctx, void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                     int64_t height);
 
 #ifdef __cplusplus
 }

@@ -40,7 +40,8 @@ struct tci_ctx {
     size_t capX = 0;
     double* ybuf = nullptr;
     size_t capY = 0;
-    int flush_every = 11;  // deferred-update depth nb (1 = write back every pivot; 10-12 measured equal with the shadow search)
+    int flush_every = 10;  // deferred-update depth nb: the shadow epoch (1 = write back every pivot)
+    int epochs = 3;        // shadow epochs per fp64 write-back (two-level epoch; env TCI_RRLU_EPOCHS)
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
     int pass_gridx = 1;    // rrLU pass workgroups per CU (env TCI_PASS_GRIDX; 1 = all resident at once)
@@ -138,7 +139,7 @@ struct tci_ctx {
         size_t idx;
     };
     std::vector<EvPair> evpairs;
-    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 3;  // + 20 solve, 21 LUCI factors, 22 K3
+    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 4;  // + 20 solve, 21 LUCI factors, 22 K3, 23 refresh
     double fam_ms[kFams] = {};
     int64_t fam_n[kFams] = {};
 };
@@ -429,8 +430,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     // ldx >= m + 2 so the 16-B loads of a tile's last odd row stay in bounds
     const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
     const int64_t ldx = round_up(m + 2, 16), ldy = round_up(n + 2, 16);
-    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPend * ldx)))) return st;
-    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPend * ldy)))) return st;
+    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPendR * ldx)))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPendR * ldy)))) return st;
     if ((m + tci::kRowsPerTile - 1) / tci::kRowsPerTile > kMaxGrid)
         return set_err(c, TCI_ERR_ARG, "rrlu: more than " +
                                            std::to_string((long long)tci::kRowsPerTile * kMaxGrid) +
@@ -476,8 +477,19 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
                                       std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
+    // two-level epoch: shadow epochs of nb pivots end with a refresh of the fp16
+    // shadow by the MFMA search itself, and only every `epochs`-th of them with a write-back of the
+    // fp64 values (exact pending updates up to nb * epochs <= kMaxPendR). epochs = 1: every shadow
+    // epoch ends with a write-back (round 2's scheme); the exact passes (shadow off) always do.
+    // (the refresh is the MFMA search's: shadow epochs of 2 .. 15 pivots -- pass 0 writes the
+    // shadow of A and cannot refresh, and the search has at most two K-steps)
+    const int epochs = (shadow && tci::shadow_elem_bytes() == 2 && nb >= 2 && nb <= 15)
+                           ? std::max(1, std::min(c->epochs, tci::kMaxPendR / nb)) : 1;
+    const int nbx = nb * epochs;
+    g.nbs = nb;
+    g.pe = g.ps = 0;
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
-    int64_t k = 0, chunk = 2, t0 = 0;  // t0: first pivot whose update is still pending
+    int64_t k = 0, chunk = 2, te = 0, ts = 0;  // te / ts: first pivot whose update is pending in fp64 / the shadow
     StopPoll poll(c, c->st);
     while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
@@ -485,16 +497,21 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             // pass k: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
             // selects pivot k+1 from the updated block. After the last pivot only x_k / y_k are
             // needed: no selection.
-            const int P = (int)(kk - t0) + 1;
-            const bool flush = (P >= nb) && (kk + 1 < mr);
+            const int PE = (int)(kk - te) + 1, PS = (int)(kk - ts) + 1;
+            const bool last = kk + 1 >= mr;
+            const bool flush = PE >= nbx && !last;
+            const bool refresh = !flush && epochs > 1 && PS >= nb && !last;
             g.k = (int)kk;
-            g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
+            g.pe = PE;
+            g.ps = PS;
+            g.selk = !last ? (int)(kk + 1) : -1;
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
-            ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
-            tci::launch_pass(c->stream, P, flush, shadow, g, grid);
+            ev_begin(c, flush ? 0 : refresh ? 23 : 2, sampled, flush || refresh ? -1 : 3 + PS);
+            tci::launch_pass(c->stream, PE, flush, shadow, g, grid, flush ? 1 : refresh ? 2 : 0);
             ev_end(c, sampled);
-            if (flush) t0 = kk + 1;
+            if (flush) te = ts = kk + 1;
+            if (refresh) ts = kk + 1;
         }
         k = kend;
         if (k >= mr) break;
@@ -712,8 +729,8 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * nl1)))) return st;
     const int nb = std::max(1, std::min(c->flush_every, tci::kMaxPend));
     const int64_t ldx = round_up(m + 2, 16), ldy = round_up(nl1 + 2, 16);
-    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPend * ldx)))) return st;
-    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPend * ldy)))) return st;
+    if ((st = ensure(c, &c->xbuf, &c->capX, (size_t)(tci::kMaxPendR * ldx)))) return st;
+    if ((st = ensure(c, &c->ybuf, &c->capY, (size_t)(tci::kMaxPendR * ldy)))) return st;
     if ((m + tci::kRowsPerTile - 1) / tci::kRowsPerTile > kMaxGrid)
         return set_err(c, TCI_ERR_ARG, "rrlu: too many rows");
     tci::PassArgs g;
@@ -824,6 +841,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     c->device = device;
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_EPOCHS")) c->epochs = std::max(1, std::min(atoi(e), tci::kMaxPendR));
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
@@ -897,6 +915,13 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
     if (nb < 1 || nb > tci::kMaxPend)
         return set_err(c, TCI_ERR_ARG, "flush interval must be in 1.." + std::to_string(tci::kMaxPend));
     c->flush_every = nb;
+    return TCI_OK;
+}
+
+int tci_set_rrlu_epochs(tci_ctx* c, int epochs) {
+    if (!c || epochs < 1 || epochs > tci::kMaxPendR)
+        return set_err(c, TCI_ERR_ARG, "epochs must be in 1.." + std::to_string(tci::kMaxPendR));
+    c->epochs = epochs;
     return TCI_OK;
 }
 
@@ -1525,6 +1550,21 @@ int tci_luci_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t lda, i
     return luci_outputs(c, m, n, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
 }
 
+int tci_luci_inplace_d(tci_ctx* c, double* d_A, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
+                       double reltol, double abstol, int leftorth, int64_t* rowidx, int64_t* colidx,
+                       double* pivoterrs, double* left, double* right, int64_t* npivot) {
+    if (!c || !npivot) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || lda < m || (lda & 1) || ((uintptr_t)d_A & 15))
+        return set_err(c, TCI_ERR_ARG, "luci: need lda >= m, lda even and a 16-byte aligned matrix");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    int64_t np;
+    double err;
+    int st;
+    if ((st = rrlu_device(c, d_A, m, n, lda, maxrank, reltol, abstol, leftorth, &np, &err))) return st;
+    *npivot = np;
+    return luci_outputs(c, m, n, leftorth, np, err, rowidx, colidx, pivoterrs, left, right);
+}
+
 // The 2-site update of a small Pi (rrlu_small_fits) with one host synchronisation and no
 // device-to-host copies: index tables up by one copy from mapped host memory, Pi + maxabs, then
 // one workgroup doing rrLU, NaN checks and the MatrixLUCI factors from LDS and writing every
@@ -1968,6 +2008,16 @@ int tci_memcpy_d2h(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
 }
 int tci_memcpy_d2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+
+int tci_memcpy2d_d2d(tci_ctx* c, void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                     int64_t height) {
+    if (!c || width < 0 || height < 0 || dpitch < width || spitch < width) return TCI_ERR_ARG;
+    if (width == 0 || height == 0) return TCI_OK;
+    HIPCHK(c, hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)height,
+                               hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }

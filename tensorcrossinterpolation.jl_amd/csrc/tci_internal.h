@@ -6,7 +6,10 @@
 
 namespace tci {
 
-constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at most
+constexpr int kMaxPend = 16;       // deferred rank-1 updates kept pending at most (ComplexF64 rrLU; the
+                                   // register-resident x's of the real rrLU's k_pass2)
+constexpr int kMaxPendR = 32;      // real rrLU: exact pending updates of a two-level epoch (X / Y slots;
+                                   // beyond kMaxPend the x's live in LDS, k_pass_x)
 constexpr int kRowsPerTile = 512;  // 256 lanes x double2
 constexpr int kMaxCB = 16;         // rrLU pass: at most this many columns per tile (measured best)
 constexpr int kMaxPassGrid = 2048; // rrLU pass: at most this many workgroups (8 per CU)
@@ -72,6 +75,11 @@ struct PassArgs {
     // adding pc_off (the rank's first global column; -1 when the rank has no candidate)
     Cand* lout = nullptr;
     int64_t pc_off = 0;
+    // two-level epoch: the pass applies pe exact pending updates (the fp64 stale
+    // values were last written back after pivot k - pe) and ps of them through the shadow (it was
+    // last written -- by a write-back or a refresh -- after pivot k - ps); shadow epochs since the
+    // last write-back are nbs pivots long. pe == ps: no refresh since the write-back.
+    int pe = 0, ps = 0, nbs = 0;
 };
 
 // Selection fields of PassArgs as seen by the device.
@@ -186,7 +194,9 @@ void launch_ctt_eval(hipStream_t s, const double2* cores, const int64_t* off, co
 void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int m, int n, int np,
                           int leftorth, const int64_t* rowperm, const int64_t* colperm,
                           double2* left, double2* right);
-void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid);
+// kind: 0 read-only, 1 write-back (fp64 + shadow), 2 refresh (shadow only, from the MFMA search's
+// values or, when its bound is not tight, from the exact ones); P = g.pe
+void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid, int kind = -1);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:
@@ -231,9 +241,9 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
 // those words as uint64 over the ranks (exchange op 1) leaves the winner's bits everywhere (every
 // bit pattern, -0.0 and NaN payloads included, is >= 0 as uint64); k_shard_commit commits the pivot
 // to the replicated row / global column maps and installs the ghost. Per pivot 32 B x N + 8 (m +
-// kMaxPend) B cross the ranks, not N x 8 m. One rank: no exchange, the commit reads the column in
+// kMaxPendR) B cross the ranks, not N x 8 m. One rank: no exchange, the commit reads the column in
 // place.
-inline int64_t shard_col(int64_t m) { return m + kMaxPend; }
+inline int64_t shard_col(int64_t m) { return m + kMaxPendR; }
 void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0);
 void launch_shard_pick(hipStream_t s, const Cand* recv, int nranks, const double* A, int64_t lda, int m,
                        const double* Y, int64_t ldy, int64_t c0, int nloc, uint64_t* colsend);

@@ -412,6 +412,7 @@ struct PassK {
     int rev;
     float* S;  // fp32 shadow of the stale values (ld lds), or null
     int64_t lds;
+    int pe, ps, nbs;  // two-level epoch: exact / shadow pending counts, shadow epoch length
 };
 
 // LDS of a one-workgroup-per-CU pass: the staged columns' y's [local column][slot] in fp64 (and
@@ -1092,17 +1093,40 @@ constexpr int kMfMaxP = 15;
 constexpr int kMfExCap = 128;                         // deferred examinations per wave
 static_assert(3 * kMfMaxP <= 64 && kMfMaxP < kMaxPend, "two MFMA K-steps per tile");
 
-template <int P>
+template <int P, bool EXT = false>
 struct MfGeom {
     static constexpr bool deep = P > 10;
     static constexpr int KS = deep ? 64 : 32;         // split slots per row / column
     static constexpr int KSP = KS + 8;                // LDS stride in halves (spreads banks)
-    static constexpr int YS = deep ? 1 : P;           // exact y's kept per staged column
+    // exact y's kept per staged column: all P, or (deep search, or an exact epoch longer than the
+    // shadow epoch: EXT) only y_k -- the examinations then read the pending y's from Y
+    static constexpr bool ymem = deep || EXT;
+    static constexpr int YS = ymem ? 1 : P;
 };
 
-template <int P>
+// v - x_0 y_0 - x_1 y_1 - ... (cnt terms, in order; separate multiply and subtract, the
+// reference's arithmetic) with strided x / y loads, kB of each in flight at a time
+template <int kB>
+__device__ __forceinline__ double pend_apply(double v, const double* __restrict__ xp, int64_t xst,
+                                             const double* __restrict__ yp, int64_t yst, int cnt) {
+    for (int s0 = 0; s0 < cnt; s0 += kB) {
+        double xv[kB], yv[kB];
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+            if (s0 + i < cnt) {
+                xv[i] = xp[(int64_t)(s0 + i) * xst];
+                yv[i] = yp[(int64_t)(s0 + i) * yst];
+            }
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+            if (s0 + i < cnt) v = __dsub_rn(v, __dmul_rn(xv[i], yv[i]));
+    }
+    return v;
+}
+
+template <int P, bool EXT = false>
 struct P2MfLds {
-    using Gm = MfGeom<P>;
+    using Gm = MfGeom<P, EXT>;
     double ys[kP2StageCols * Gm::YS];                 // exact y's of the staged columns (examinations)
     _Float16 yb[kP2StageCols * Gm::KSP];              // their B fragments (y splits)
     int cpos[kP2StageCols];
@@ -1128,12 +1152,20 @@ __device__ __forceinline__ void f16_split(double v, _Float16& hi, _Float16& lo) 
     lo = (_Float16)(float)(v - (double)hi);
 }
 
-template <int P>
-__device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P>& L,
+// Two-level epoch: EXT -- the exact epoch is longer than the shadow epoch: the pass
+// applies the P shadow-pending updates on the matrix cores, but x_k, y_k and the exact
+// examinations apply all PE = g.pe exact-pending ones (the shadow epoch's slots are the last P of
+// them). RF -- a refresh: the pass also writes the shadow of the values it computes (W, updated
+// through pivot k, scaled for the epoch that starts at k + 1; rows outside the trailing block 0),
+// so the next shadow epoch starts without a write-back of the fp64 values.
+template <int P, bool EXT = false, bool RF = false>
+__device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P, EXT>& L,
                                              CandR& best, float eps, double shs,
                                              unsigned long long (&pt)[6]) {
     static_assert(P >= 1 && P <= kMfMaxP, "at most two MFMA K-steps per tile");
-    using Gm = MfGeom<P>;
+    using Gm = MfGeom<P, EXT>;
+    const int PE = EXT ? g.pe : P;  // exact pending updates; the shadow's are slots off .. PE - 1
+    const int off = PE - P;
     constexpr int KS = Gm::KS, KSP = Gm::KSP, KSt = KS / 32;
     RrluState* st = sel.st;
     const int32_t* colpos = sel.colpos;
@@ -1190,6 +1222,14 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         const int r = sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
         act |= (r < m && rowpos[r] > k);
     }
+    // refresh: which of the lane's 16 loaded rows are trailing (the others get shadow 0)
+    [[maybe_unused]] unsigned tmask = 0;
+    if constexpr (RF) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmask |= (rl + i < m && rowpos[rl + i] > k ? 1u : 0u) << i;
+    }
+    [[maybe_unused]] const float rscale =
+        RF ? (float)(sh_scale(sh_bound(pv, k + 1)) / shs) : 1.0f;  // a power of two: exact
     int jst = ntc > 0 ? stage_col(0) : -1;
     int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
     const int prow = threadIdx.x - kP2StageCols;  // this thread's tile row (row threads)
@@ -1209,14 +1249,18 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         const int rr = rrow < m ? rrow : 0;
         double xs[P];
 #pragma unroll
-        for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)s * ldx + rr];
+        for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
         double xk = g.A[rr + (int64_t)bq * lda];
+        if constexpr (EXT) {  // all PE - 1 exact pending updates, 16 loads in flight at a time
+            xk = pend_apply<16>(xk, g.X + rr, ldx, g.Y + bq, ldy, PE - 1);
+        } else {
 #pragma unroll
-        for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
+            for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
+        }
         if (leftorth) xk = xk / piv;
         L.xk[prow] = xk;
         if (q == 0 && rpos > k) {
-            g.X[(int64_t)(P - 1) * ldx + rrow] = xk;
+            g.X[(int64_t)(PE - 1) * ldx + rrow] = xk;
             g.Lp[rrow + (int64_t)k * g.ldl] = xk;
         }
         xs[P - 1] = xk;
@@ -1243,12 +1287,13 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         }
     }
     PPROF(1);
-    const bool wact = __any(act);
+    const bool wact = RF || __any(act);  // a refresh rewrites every row's shadow (non-trailing: 0)
     const float margin = 0x1p-20f;
     float tau = 0.0f;
     h8v af[kMfBlk][KSt];  // A fragments (registers for the whole pass)
     // chunk h: the lane's column's maximum |w| over its 16 rows and per 4-row block (-1: not a
     // trailing column)
+    int g0r = 0;  // the staged group approx() works on (its columns, for the refresh stores)
     auto approx = [&](int h, int gcols, const h8v (&v)[2], float (&mbs)[kMfBlk]) -> float {
         const int lc = h * 16 + lcol;
         const int cp = lc < gcols ? L.cpos[lc] : -1;
@@ -1257,6 +1302,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         for (int u = 0; u < KSt; ++u)
             bf[u] = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * KSP + 32 * u + 8 * gq]);
         float c = 0.0f;
+        [[maybe_unused]] h8v wout[2];
 #pragma unroll
         for (int b = 0; b < kMfBlk; ++b) {
             const h8v& hv = v[b >> 1];
@@ -1267,6 +1313,19 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             mbs[b] = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
                                      __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
             c = __builtin_fmaxf(c, mbs[b]);
+            if constexpr (RF) {  // rows rl + 4 b + t: the new epoch's shadow, 0 off the trailing block
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    wout[b >> 1][o + t] = (tmask >> (4 * b + t)) & 1u ? (_Float16)(acc[t] * rscale) : (_Float16)0.0f;
+            }
+        }
+        if constexpr (RF) {
+            const int j = lc < gcols ? col_of(g0r, lc) : n;
+            if (rload && j < n && cp > k) {
+                h8v* p = reinterpret_cast<h8v*>(const_cast<_Float16*>(sbase) + (int64_t)j * lds);
+                p[0] = wout[0];
+                p[1] = wout[1];
+            }
         }
         if (cp <= k) {
 #pragma unroll
@@ -1297,20 +1356,19 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const int rp = rowpos[r];
             if (rp <= k) continue;
             if constexpr (decltype(fast)::value) {
-                if constexpr (Gm::deep) {
+                if constexpr (Gm::ymem) {
                     // x's and y's from memory, four pending updates in flight at a time
-#pragma unroll
-                    for (int s0 = 0; s0 < P - 1; s0 += 4) {
+                    for (int s0 = 0; s0 < PE - 1; s0 += 4) {
                         double xv[4], yv[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            if (s0 + i < P - 1) {
+                            if (s0 + i < PE - 1) {
                                 xv[i] = g.X[(int64_t)(s0 + i) * ldx + r];
                                 yv[i] = g.Y[(int64_t)(s0 + i) * ldy + j];
                             }
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            if (s0 + i < P - 1) v = __dsub_rn(v, __dmul_rn(xv[i], yv[i]));
+                            if (s0 + i < PE - 1) v = __dsub_rn(v, __dmul_rn(xv[i], yv[i]));
                     }
                 } else {
                     double xv[P];
@@ -1321,9 +1379,9 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                 }
             } else {
 #pragma unroll 1
-                for (int s = 0; s < P - 1; ++s)
+                for (int s = 0; s < PE - 1; ++s)
                     v = __dsub_rn(v, __dmul_rn(g.X[(int64_t)s * ldx + r],
-                                               Gm::deep ? g.Y[(int64_t)s * ldy + j] : L.ys[lc * P + s]));
+                                               Gm::ymem ? g.Y[(int64_t)s * ldy + j] : L.ys[lc * P + s]));
             }
             v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * Gm::YS + Gm::YS - 1]));
             const double a2 = __dmul_rn(v, v);
@@ -1364,6 +1422,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         const int gn = min(G, ntc - g0);
         const int gcols = gn * cb;
         const int nch = (gcols + 15) / 16;
+        g0r = g0;
         if (g0 > 0) {
             jst = stage_col(g0);
             cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
@@ -1380,14 +1439,18 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             if (cpst > k) {
                 double ysv[P];
 #pragma unroll
-                for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)s * ldy + jst];
+                for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)(off + s) * ldy + jst];
                 double yk = g.A[a + (int64_t)jst * lda];
+                if constexpr (EXT) {
+                    yk = pend_apply<16>(yk, g.X + a, ldx, g.Y + jst, ldy, PE - 1);
+                } else {
 #pragma unroll
-                for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
+                    for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
+                }
                 if (!leftorth) yk = yk / piv;
                 ysv[P - 1] = yk;
                 if (tr == 0) {
-                    g.Y[(int64_t)(P - 1) * ldy + jst] = yk;
+                    g.Y[(int64_t)(PE - 1) * ldy + jst] = yk;
                     g.Up[k + (int64_t)jst * g.ldu] = yk;
                 }
                 // B fragment: slots (yh_s, yl_s, yh_s) for s < P, zero after
@@ -1395,7 +1458,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                 L.ys[lc * Gm::YS + Gm::YS - 1] = yk;
 #pragma unroll
                 for (int s = 0; s < P; ++s) {
-                    if constexpr (!Gm::deep) L.ys[lc * P + s] = ysv[s];
+                    if constexpr (!Gm::ymem) L.ys[lc * P + s] = ysv[s];
                     f16_split(leftorth ? ysv[s] * shs : ysv[s], sl[3 * s], sl[3 * s + 1]);
                     sl[3 * s + 2] = sl[3 * s];
                 }
@@ -1487,39 +1550,297 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     return true;
 }
 
-template <int P>
+// ------------------------------------------------------------------ deep exact pass (two-level epoch)
+// The exact body for up to kMaxPendR pending updates: P (= g.pe, runtime) x's per row do not fit
+// the registers of k_pass2 (which spills from P = 13), so the tile's x's live in LDS, [s][row], and
+// the tile is processed in two 256-row halves (64 KiB of x's each); the staged columns' y's are in
+// LDS too, [s][column], 128 columns per group. Per element the reference's arithmetic in its order,
+// v = v - x_s[i] * y_s[j] for s = 0 .. P-1 (separate multiply and subtract): bitwise k_pass2's
+// values. MODE 0: read only (the exact fallback of a read pass whose shadow bound is not tight);
+// 1: write-back of the fp64 values and the fp16 shadow of the new epoch (as k_pass2<P,true,true>);
+// 2: the shadow only (a refresh whose MFMA bound is not tight: the new epoch's shadow is then exact
+// again, which the bound recursion of k_pass_mf knows -- it re-derives every past decision). Same
+// grid, tiles, candidates and tail as k_pass2, so it also serves as k_pass_mf's fallback body.
+constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
+constexpr int kXStage = 128;  // staged columns per group
+constexpr int kXU = 4;        // columns per chunk (two chunks in flight per lane)
+constexpr int kXSlices = kXHalf / 128;
+constexpr int kXReps = kP2Threads / 64 / kXSlices;
+struct PxLds {
+    double xs[kMaxPendR * kXHalf];   // x_s of the half-tile's rows
+    double ys[kMaxPendR * kXStage];  // y_s of the staged columns
+    double xa[kMaxPendR];            // X[s][a] (pivot row a)
+    double yb[kMaxPendR];            // Y[s][b] (pivot column b)
+    int cpos[kXStage];
+    int cnt[kXSlices];
+};
+
+template <int MODE>
+__device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, PxLds& L, CandR& best,
+                                           unsigned long long (&pt)[6]) {
+    RrluState* st = sel.st;
+    const int32_t* rowpos = sel.rowpos;
+    const int32_t* colpos = sel.colpos;
+    double* __restrict__ A = g.A;
+    const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy;
+    const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
+    const int P = g.pe;  // 1 .. kMaxPendR
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slice = wave % kXSlices, rep = wave / kXSlices;
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+    const int tiles_c = (n + cb - 1) / cb;
+    const int nq = gridDim.x / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int tr = wid % tiles_r;
+    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    const int G = kXStage / cb;
+    const int cbs = __builtin_ctz(cb);
+    auto col_of = [&](int g0, int lc) -> int {
+        const int it = g0 + (lc >> cbs);
+        return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
+    };
+    if (st->done) return false;
+    const int a = (int)st->p, b = (int)st->q;
+    const double piv = st->pval;
+    // the pivot row's pending x's and the pivot column's pending y's (same for every thread)
+    if (threadIdx.x < P - 1) {
+        L.xa[threadIdx.x] = g.X[(int64_t)threadIdx.x * ldx + a];
+        L.yb[threadIdx.x] = g.Y[(int64_t)threadIdx.x * ldy + b];
+    }
+    [[maybe_unused]] const double shs = MODE ? sh_scale(sh_bound(sel.pivvals, k + 1)) : 1.0;
+    PPROF(1);
+    for (int half = 0; half < kRowsPerTile / kXHalf; ++half) {
+        const int hb = tr * kRowsPerTile + half * kXHalf;  // first row of the half
+        if (hb >= m) break;
+        __syncthreads();  // the previous half's readers are done with xs / ys
+        for (int e = threadIdx.x; e < (P - 1) * kXHalf; e += kP2Threads) {
+            const int s = e / kXHalf, rr = e - s * kXHalf;
+            L.xs[e] = hb + rr < m ? g.X[(int64_t)s * ldx + hb + rr] : 0.0;
+        }
+        __syncthreads();
+        if (threadIdx.x < kXHalf) {  // x_k of the half's rows (pivot k's column, updates applied)
+            const int rr = threadIdx.x, r = hb + rr;
+            double xk = 0.0;
+            if (r < m) {
+                xk = A[r + (int64_t)b * lda];
+                for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(L.xs[s * kXHalf + rr], L.yb[s]));
+                if (leftorth) xk = xk / piv;
+                if (q == 0 && rowpos[r] > k) {
+                    g.X[(int64_t)(P - 1) * ldx + r] = xk;
+                    g.Lp[r + (int64_t)k * g.ldl] = xk;
+                }
+            }
+            L.xs[(P - 1) * kXHalf + rr] = xk;
+        }
+        const int lr = slice * 128 + 2 * lane;  // the lane's first row within the half
+        const int r0 = hb + lr;
+        const bool rowok = r0 < m, pair = r0 + 1 < m;
+        const int rp0 = rowok ? rowpos[r0] : -1, rp1 = pair ? rowpos[r0 + 1] : -1;
+        const bool in0 = rp0 > k, in1 = rp1 > k;
+        const bool wact = MODE != 0 || __any(in0 || in1);
+        double* const base = A + (rowok ? r0 : 0);
+        for (int g0 = 0; g0 < ntc; g0 += G) {
+            const int gcols = min(G, ntc - g0) * cb;
+            const int nch = gcols / kXU;
+            if (g0 > 0) __syncthreads();  // the previous group's readers are done with ys / cpos
+            if (threadIdx.x < gcols) {
+                const int lc = threadIdx.x, j = col_of(g0, lc);
+                const int cp = j < n ? colpos[j] : -1;
+                L.cpos[lc] = cp;
+                if (cp > k) {
+                    double yk = A[a + (int64_t)j * lda];
+                    for (int s = 0; s < P - 1; ++s) {
+                        const double yv = g.Y[(int64_t)s * ldy + j];
+                        L.ys[s * kXStage + lc] = yv;
+                        yk = __dsub_rn(yk, __dmul_rn(L.xa[s], yv));
+                    }
+                    if (!leftorth) yk = yk / piv;
+                    L.ys[(P - 1) * kXStage + lc] = yk;
+                    if (tr == 0 && half == 0) {
+                        g.Y[(int64_t)(P - 1) * ldy + j] = yk;
+                        g.Up[k + (int64_t)j * g.ldu] = yk;
+                    }
+                }
+            }
+            if (threadIdx.x < kXSlices) L.cnt[threadIdx.x] = 2 * kXReps;
+            __syncthreads();
+            if (g0 == 0 && half == 0) PPROF(2);
+            if (!wact) continue;
+            auto load_chunk = [&](int h, double2 (&v)[kXU]) {
+#pragma unroll
+                for (int u = 0; u < kXU; ++u) {
+                    const int j = min(col_of(g0, h * kXU + u), n - 1);
+                    const double2* pa = reinterpret_cast<const double2*>(base + (int64_t)j * lda);
+                    if constexpr (MODE == 1 && TCI_FLUSH_NTL) {
+                        typedef double dv2 __attribute__((ext_vector_type(2)));
+                        const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(pa));
+                        v[u] = double2{w.x, w.y};
+                    } else {
+                        v[u] = *pa;
+                    }
+                }
+            };
+            auto process = [&](int h, double2 (&v)[kXU]) {
+                int cp[kXU];
+                bool any = false;
+#pragma unroll
+                for (int u = 0; u < kXU; ++u) {
+                    cp[u] = L.cpos[h * kXU + u];
+                    any |= cp[u] > k;
+                }
+                if (!any) return;
+                for (int s = 0; s < P; ++s) {
+                    const double2 x = *reinterpret_cast<const double2*>(&L.xs[s * kXHalf + lr]);
+                    const double2 y01 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU]);
+                    const double2 y23 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU + 2]);
+                    const double y[kXU] = {y01.x, y01.y, y23.x, y23.y};
+#pragma unroll
+                    for (int u = 0; u < kXU; ++u) {
+                        v[u].x = __dsub_rn(v[u].x, __dmul_rn(x.x, y[u]));
+                        v[u].y = __dsub_rn(v[u].y, __dmul_rn(x.y, y[u]));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kXU; ++u) {
+                    if (cp[u] <= k) continue;
+                    const int j = col_of(g0, h * kXU + u);
+                    if constexpr (MODE == 1) {  // trailing rows only (see k_pass2's write-back)
+                        if (in0 || in1) {
+                            double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
+                            if (!in1) {
+                                pa->x = v[u].x;
+                            } else if (!in0) {
+                                pa->y = v[u].y;
+                            } else {
+                                typedef double dv2 __attribute__((ext_vector_type(2)));
+                                dv2 w = {v[u].x, v[u].y};
+                                __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(pa));
+                            }
+                        }
+                    }
+                    if constexpr (MODE != 0 && kShHalf) {
+                        if (rowok) {
+                            _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
+                            const _Float16 h0 = in0 ? (_Float16)(float)(v[u].x * shs) : (_Float16)0.0f;
+                            if (pair) {
+                                typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                                *reinterpret_cast<h2v*>(ps) = h2v{h0, in1 ? (_Float16)(float)(v[u].y * shs) : (_Float16)0.0f};
+                            } else {
+                                ps[0] = h0;
+                            }
+                        }
+                    }
+                    const double a0 = __dmul_rn(v[u].x, v[u].x), a1 = __dmul_rn(v[u].y, v[u].y);
+                    if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                        if (in0) cand_take(best, CandR{a0, v[u].x, cp[u], rp0, j, r0});
+                        if (in1) cand_take(best, CandR{a1, v[u].y, cp[u], rp1, j, r0 + 1});
+                    }
+                }
+            };
+            auto grab = [&]() -> int {
+                int h = 0;
+                if (lane == 0) h = atomicAdd(&L.cnt[slice], 1);
+                return __shfl(h, 0);
+            };
+            double2 va[kXU], vb[kXU];
+            int h0 = rep, h1 = rep + kXReps;
+            if (h0 < nch) load_chunk(h0, va);
+            if (h1 < nch) load_chunk(h1, vb);
+            while (h0 < nch) {
+                process(h0, va);
+                h0 = grab();
+                if (h0 < nch) load_chunk(h0, va);
+                if (h1 >= nch) break;
+                process(h1, vb);
+                h1 = grab();
+                if (h1 < nch) load_chunk(h1, vb);
+            }
+        }
+    }
+    return true;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kP2Threads) void k_pass_x(PassK g, SelArgs sel) {
+    __shared__ PxLds L;
+    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    PPROF(0);
+    CandR best = cand_none();
+    if (!passx_body<MODE>(g, sel, L, best, pt)) return;
+    PPROF(3);
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, g.pe, MODE);
+}
+
+// The certificate of a shadow-search pass after pivot k (two-level epoch): the
+// current shadow epoch started at t0 = k - PS + 1, the exact epoch at te = k - PE + 1, and every
+// shadow epoch in [te, t0) (nbs pivots each) ended with a refresh. In absolute units, with
+// |v| <= Mf the epoch's stale bound, d the error of its shadow against the exact stale values
+// (0 after a write-back or an exact refresh, else the bound of the refresh pass's W) and
+// sumM = sum |pivot_s| over its pending updates:
+//   d + 2^-11 (1 + 2^-9) (Mf + d) + 2^-25 / s     fp16 storage (s the epoch's scale)
+//     + 2^-19 sumM + P 2^-24 / s                   f16 splits, dropped xl yl
+//     + (3P + 4) 2^-23 (Mf + d + 2 sumM)           fp32 accumulation
+// The search runs while that is below 2^-TCI_SH_TIGHT |pivot k| (else the exact body, uniform).
+// Each pass re-derives the decisions of the refreshes before it from the pivot values with this
+// same function, so every pass agrees with what they did.
+struct ShCert {
+    double eps;  // scaled units of the current epoch
+    double shs;  // the current epoch's scale
+    bool ok;
+};
+__device__ __forceinline__ ShCert sh_cert(const double* pv, int k, int PS, int PE, int nbs) {
+    const int te = k - PE + 1, t0 = k - PS + 1;
+    double d = 0.0;
+    ShCert c{0.0, 0.0, false};
+    for (int e = te;; e += nbs) {
+        const bool cur = e >= t0;
+        const int ke = cur ? k : e + nbs - 1;  // the pass whose certificate this is
+        const int P = ke - e + 1;
+        double sumM = 0.0, maxM = 0.0;
+        for (int t = e; t <= ke; ++t) {
+            sumM += fabs(pv[t]);
+            maxM = fmax(maxM, fabs(pv[t]));
+        }
+        const double s = sh_scale(sh_bound(pv, e));
+        const double Mfd = fabs(pv[e]) + d;
+        const double mag = Mfd + 2.0 * sumM;
+        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 / s + 0x1p-19 * sumM +
+                                        (double)P * 0x1p-24 / s + (double)(3 * P + 4) * 0x1p-23 * mag
+                                  : 0.0;
+        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(pv[ke]) * s, -TCI_SH_TIGHT);
+        if (cur) {
+            c.eps = ea * s;
+            c.shs = s;
+            return c;
+        }
+        d = c.ok ? ea : 0.0;  // a refresh that could not certify its bound wrote exact values
+    }
+}
+
+template <int P, bool EXT, bool RF>
 __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     __shared__ union {
         P2Lds<P> x;
-        P2MfLds<P> f;
+        P2MfLds<P, EXT> f;
+        typename std::conditional<(EXT || RF), PxLds, char>::type px;
     } L;
     [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
     PPROF(0);
-    const double* pv = sel.pivvals;
-    const int t0 = g.k - P + 1;
-    const double Mf = fabs(pv[t0]);
-    double sumM = 0.0, maxM = 0.0;
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-        sumM += fabs(pv[t0 + s]);
-        maxM = fmax(maxM, fabs(pv[t0 + s]));
-    }
-    const double mag = Mf + 2.0 * sumM;
-    const double shs = sh_scale(sh_bound(pv, t0));
-    const double epsd = 0x1p-11 * (1.0 + 0x1p-9) * Mf * shs + 0x1p-25 + 0x1p-19 * sumM * shs +
-                        (double)P * 0x1p-24 + (double)(3 * P + 4) * 0x1p-23 * mag * shs;
-    // the f16 operands (the scaled factor <= s |pivot_s|) must stay below 2^15
-    const bool shok = shs > 0.0 && mag < 0x1p100 && maxM * shs <= 0x1p15 &&
-                      epsd < ldexp(fabs(pv[g.k]) * shs, -TCI_SH_TIGHT);
+    const ShCert c = sh_cert(sel.pivvals, g.k, P, EXT ? g.pe : P, g.nbs > 0 ? g.nbs : P);
     CandR best = cand_none();
     bool go;
-    if (shok)
-        go = pass_mf_body<P>(g, sel, L.f, best, (float)(epsd * (1.0 + 0x1p-20)), shs, pt);
+    if (c.ok)
+        go = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, (float)(c.eps * (1.0 + 0x1p-20)), c.shs, pt);
+    else if constexpr (RF)
+        go = passx_body<2>(g, sel, L.px, best, pt);
+    else if constexpr (EXT)
+        go = passx_body<0>(g, sel, L.px, best, pt);
     else
         go = pass2_body<P, false, false>(g, sel, L.x, best, pt);
     if (!go) return;
     PPROF(3);
-    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, 0);
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, RF ? 2 : 0);
 }
 
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
@@ -1537,11 +1858,12 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid) {
 }
 
 template <int P>
-static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs& g, int grid) {
+static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs& g, int grid, int kind) {
     const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
                       g.ticket, g.reltol, g.abstol,  g.selk,    g.lout, g.pc_off};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
-                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds};
+                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
+                  g.pe, g.ps, g.nbs};
     if (shadow && kShHalf) {
         // fp16: the shadow's scale needs |pivot 0|, so the initial pass only selects, and pass 0
         // (exact) writes the shadow of A; write-backs write the shadow of the new stale values
@@ -1552,10 +1874,20 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
         else if (P == 1 && g.k == 0)
             hipLaunchKernelGGL((k_pass2<1, false, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
         else if constexpr (P > 0) {
-            if constexpr (TCI_SH_MFMA && P <= kMfMaxP)
-                hipLaunchKernelGGL((k_pass_mf<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-            else
+            // P here is the shadow-pending count g.ps; EXT when the exact epoch is longer
+            const bool ext = g.pe > g.ps, rf = kind == 2;
+            if constexpr (TCI_SH_MFMA && P <= kMfMaxP) {
+                if (ext && rf)
+                    hipLaunchKernelGGL((k_pass_mf<P, true, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+                else if (ext)
+                    hipLaunchKernelGGL((k_pass_mf<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+                else if (rf)
+                    hipLaunchKernelGGL((k_pass_mf<P, false, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+                else
+                    hipLaunchKernelGGL((k_pass_mf<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            } else {
                 hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            }
         }
     } else if (shadow) {
         if (flush || P == 0)
@@ -1569,10 +1901,29 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
     }
 }
 
-void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid) {
-    switch (P) {
+#ifndef TCI_PASSX_MIN
+#define TCI_PASSX_MIN 12  // write-backs with at least this many pending updates: k_pass_x (x's in LDS)
+#endif
+
+// kind: -1 legacy (P pending, write-back iff flush); 0 read-only, 1 write-back, 2 refresh, with
+// g.pe / g.ps the exact / shadow pending counts (two-level epoch)
+void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid, int kind) {
+    if (kind < 0) kind = flush ? 1 : 0;
+    PassArgs h = g;
+    if (h.pe <= 0) h.pe = h.ps = P;  // legacy callers (column-sharded driver): one epoch level
+    if (kind == 1 && shadow && kShHalf && h.pe >= TCI_PASSX_MIN) {
+        const SelArgs sel{h.rowpos, h.colpos, h.rowphys, h.colphys, h.pivvals, h.st,
+                          h.ticket, h.reltol, h.abstol,  h.selk,    h.lout, h.pc_off};
+        const PassK a{h.A,  h.lda, h.m,  h.n,   h.k,        h.X,    h.ldx, h.Y,   h.ldy,
+                      h.Lp, h.ldl, h.Up, h.ldu, h.leftorth, h.cand, h.cb,  h.rev, h.S, h.lds,
+                      h.pe, h.ps, h.nbs};
+        hipLaunchKernelGGL((k_pass_x<1>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        return;
+    }
+    const int PP = kind == 1 || !(shadow && kShHalf) ? h.pe : h.ps;
+    switch (PP) {
 #define TCI_PASS_CASE(p) \
-    case p: launch_pass_p<p>(s, flush, shadow, g, grid); break;
+    case p: launch_pass_p<p>(s, kind == 1, shadow, h, grid, kind); break;
         TCI_PASS_CASE(0) TCI_PASS_CASE(1) TCI_PASS_CASE(2) TCI_PASS_CASE(3) TCI_PASS_CASE(4)
         TCI_PASS_CASE(5) TCI_PASS_CASE(6) TCI_PASS_CASE(7) TCI_PASS_CASE(8) TCI_PASS_CASE(9)
         TCI_PASS_CASE(10) TCI_PASS_CASE(11) TCI_PASS_CASE(12) TCI_PASS_CASE(13) TCI_PASS_CASE(14)
@@ -2376,13 +2727,13 @@ __global__ __launch_bounds__(256) void k_shard_pick(const Cand* __restrict__ rec
     __syncthreads();
     const int own = own_s;
     const double* col = A + (int64_t)(own >= 0 ? own : 0) * lda;
-    if (blockIdx.x == 0 && threadIdx.x < kMaxPend)
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPendR)
         colsend[threadIdx.x] = own >= 0 ? dbl_bits(Y[(int64_t)threadIdx.x * ldy + own]) : 0ull;
     const int i0 = blockIdx.x * 1024 + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = i0 + u * 256;
-        if (i < m) colsend[kMaxPend + i] = own >= 0 ? dbl_bits(col[i]) : 0ull;
+        if (i < m) colsend[kMaxPendR + i] = own >= 0 ? dbl_bits(col[i]) : 0ull;
     }
 }
 
@@ -2432,14 +2783,14 @@ __global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ r
     for (int u = 0; u < 4; ++u) {  // all reads before any write: own may alias nothing, but be safe
         const int i = i0 + u * 256;
         v[u] = qnan;
-        if (i < m && wr >= 0) v[u] = colrecv ? bits_dbl(colrecv[kMaxPend + i]) : lcol[i];
+        if (i < m && wr >= 0) v[u] = colrecv ? bits_dbl(colrecv[kMaxPendR + i]) : lcol[i];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = i0 + u * 256;
         if (i < m) gcol[i] = v[u];
     }
-    if (blockIdx.x == 0 && threadIdx.x < kMaxPend) {
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPendR) {
         const int t = threadIdx.x;
         const double y = wr < 0 ? 0.0 : colrecv ? bits_dbl(colrecv[t]) : Y[(int64_t)t * ldy + own];
         Y[(int64_t)t * ldy + nloc] = y;

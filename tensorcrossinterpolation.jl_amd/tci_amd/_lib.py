@@ -53,6 +53,7 @@ SIGNATURES = {
     "tci_last_kernel_stats": ([vp, C.c_int, pdbl, pi64], C.c_int),
     "tci_set_timing": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
+    "tci_set_rrlu_epochs": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_small": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_mid": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_shadow": ([vp, C.c_int], C.c_int),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "tci_rrlu_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, pi64, pdbl, vp],
                            C.c_int),
     "tci_luci_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),
+    "tci_luci_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),
     "tci_update_pivots_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i64, dbl, dbl, C.c_int, C.c_int, vp,
                              vp, vp, pi64, pdbl, vp, vp], C.c_int),
     "tci_sitetensor_h": ([vp, vp, vp, i64, i32, vp, i64, i32, vp, i64, vp, pdbl], C.c_int),
@@ -122,6 +124,7 @@ SIGNATURES = {
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy_d2h": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy_d2d": ([vp, vp, vp, i64], C.c_int),
+    "tci_memcpy2d_d2d": ([vp, vp, i64, vp, i64, i64, i64], C.c_int),
 }
 
 # tci_exchange_fn (include/tci_hip.h): int (*)(void* user, int op, const void* d_send, void* d_recv,

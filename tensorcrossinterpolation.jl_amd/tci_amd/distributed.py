@@ -167,6 +167,111 @@ class ShardedBatchEvaluator:
             mx = m_.value
         return view, (j0, j1), self.comm.allreduce_maxabs(mx)
 
+    @property
+    def device_gather(self):
+        """A replicated Pi can be assembled in HBM by RCCL (no host staging)."""
+        return self.device_comm is not None
+
+    def pi_device(self, I, J, M=0, slot=0):
+        """Full (|I| * D) x |J| Pi replicated in HBM on every rank, with no host staging (SURVEY 8(e)
+        C1): each rank evaluates its block of w = ceil(|J| / N) columns into its slot of a padded
+        ld x (N w) buffer and ONE ncclAllGather (in place, on the context stream) fills the other
+        slots; the first |J| columns are Pi. Returns (view, max|Pi| over the ranks). slot selects
+        one of two buffers (Pi1 and P of a site tensor)."""
+        from . import _lib
+
+        ctx = self.local.ctx
+        I = np.ascontiguousarray(np.asarray(I, np.int32))
+        J = np.ascontiguousarray(np.asarray(J, np.int32))
+        m, nl = I.shape
+        n, nr = J.shape
+        D = self.localdims[nl] if M == 1 else 1
+        rows = m * D
+        N, r = self.comm.world, self.comm.rank
+        w = max(1, -(-n // N))
+        ld = max(16, (rows + 15) // 16 * 16)
+        need = ld * w * N
+        bufs = self.__dict__.setdefault("_gbufs", [None, None])
+        if bufs[slot] is None or bufs[slot].size < need:
+            if bufs[slot] is not None:
+                bufs[slot].free()
+            bufs[slot] = _DevBuf(ctx, int(need * 1.25) + 1024)
+        base = bufs[slot].ptr.value
+        j0, j1 = min(r * w, n), min((r + 1) * w, n)
+        mx = 0.0
+        if j1 > j0 and rows > 0:
+            Jl = np.ascontiguousarray(J[j0:j1])
+            m_ = C.c_double()
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), j1 - j0, nr, M,
+                                              C.c_void_p(base + 8 * ld * w * r), ld, C.byref(m_)))
+            mx = m_.value
+        if rows > 0:
+            self.device_comm.allgather(C.c_void_p(base + 8 * ld * w * r), C.c_void_p(base), 8 * ld * w)
+        return _DevView(ctx, C.c_void_p(base), rows, n, ld), self.comm.allreduce_maxabs(mx)
+
+    def update_pivots_gathered(self, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                               want_left=True, want_right=True):
+        """updatepivots! with the factors (first half-sweep, sweep1site!): Pi all-gathered in HBM
+        over RCCL, MatrixLUCI on this rank's GPU (tci_luci_inplace_d); every rank computes the same
+        bits. Same result dict as tensorci2.update_pivots_device."""
+        from . import _lib
+
+        ctx = self.local.ctx
+        view, gmx = self.pi_device(rows, cols, 0)
+        m, n = view.m, view.n
+        mr = int(max(min(int(maxrank), m, n), 0))
+        rowidx = np.zeros(max(mr, 1), np.int64)
+        colidx = np.zeros(max(mr, 1), np.int64)
+        pe = np.zeros(mr + 1)
+        npv = C.c_int64()
+        left = np.zeros(max(m * mr, 1)) if (want_factors and want_left) else None
+        right = np.zeros(max(mr * n, 1)) if (want_factors and want_right) else None
+        ctx.check(ctx.lib.tci_luci_inplace_d(ctx.h, view.ptr, m, n, view.ld, int(min(maxrank, 2 ** 62)),
+                                             float(reltol), float(abstol), int(bool(leftorth)), _lib.ptr(rowidx),
+                                             _lib.ptr(colidx), _lib.ptr(pe), _lib.ptr(left), _lib.ptr(right),
+                                             C.byref(npv)))
+        k = npv.value
+        res = {"rowidx": rowidx[:k].copy(), "colidx": colidx[:k].copy(), "pivoterrors": pe[: k + 1].copy(),
+               "maxabs": gmx, "npivot": k}
+        if left is not None:
+            res["left"] = left[: m * k].reshape((m, k), order="F")
+        if right is not None:
+            res["right"] = right[: k * n].reshape((k, n), order="F")
+        return res
+
+    def sitetensor_gathered(self, Ib, Jb, Inext, solve=True):
+        """setsitetensor!'s T = Pi1 P^-1 (tensorci2.jl:599-629) with Pi1 and P all-gathered in HBM
+        and the solve on this rank's GPU (tci_sitetensor_solve_d); only T comes to the host."""
+        ctx = self.local.ctx
+        if not solve:
+            _, _, gmx = self.pi_local(Ib, Jb, 1)
+            return None, gmx
+        v1, gmx = self.pi_device(Ib, Jb, 1, slot=0)
+        R, r = v1.m, v1.n
+        if Inext is None:  # the last site: T = Pi1
+            if R * r == 0:
+                return np.zeros((R, r), order="F"), gmx
+            buf = np.empty(v1.ld * r)
+            ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, C.c_void_p(buf.ctypes.data), v1.ptr, buf.nbytes))
+            return np.asfortranarray(buf.reshape((v1.ld, r), order="F")[:R, :]), gmx
+        vp_, _ = self.pi_device(Inext, Jb, 0, slot=1)
+        if vp_.m != vp_.n:
+            raise RuntimeError("Pivot matrix is not square!")
+        if R == 0 or r == 0:
+            return np.zeros((R, r), order="F"), gmx
+        from .matrixlu import DeviceMatrix
+        P = DeviceMatrix(r, r, ctx=ctx, ld=r)
+        Pi1 = DeviceMatrix(R, r, ctx=ctx, ld=R)
+        Tm = DeviceMatrix(R, r, ctx=ctx, ld=R)
+        try:
+            ctx.check(ctx.lib.tci_memcpy2d_d2d(ctx.h, P.ptr, 8 * r, vp_.ptr, 8 * vp_.ld, 8 * r, r))
+            ctx.check(ctx.lib.tci_memcpy2d_d2d(ctx.h, Pi1.ptr, 8 * R, v1.ptr, 8 * v1.ld, 8 * R, r))
+            ctx.check(ctx.lib.tci_sitetensor_solve_d(ctx.h, P.ptr, r, Pi1.ptr, R, Tm.ptr))
+            return Tm.to_host().copy(order="F"), gmx
+        finally:
+            for x in (P, Pi1, Tm):
+                x.free()
+
     def update_pivots_sharded(self, rows, cols, maxrank, reltol, abstol, leftorth):
         """updatepivots!'s :full search with Pi sharded on the devices: returns the dict of
         tensorci2.update_pivots_device (pivot positions, pivot errors, max|Pi|; no factors)."""

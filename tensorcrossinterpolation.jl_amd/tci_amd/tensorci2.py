@@ -550,6 +550,9 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
                                    want_left, want_right)
     if getattr(f, "shard_rrlu", False) and not want_factors:
         return f.update_pivots_sharded(rows, cols, maxrank, reltol, abstol, leftorth)
+    if getattr(f, "device_gather", False):  # sharded evaluation, Pi gathered in HBM over RCCL
+        return f.update_pivots_gathered(rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                                        want_left, want_right)
     if not hasattr(f, "h"):
         return _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                       want_left, want_right)
@@ -682,6 +685,8 @@ def sitetensor_device(f, Ib, Jb, Inext, solve=True):
         ctx.check(ctx.lib.tci_sitetensor_solve_c128_h(ctx.h, _lib.ptr(np.asfortranarray(P)), r,
                                                       _lib.ptr(np.asfortranarray(Pi1)), R, _lib.ptr(T)))
         return T[: R * r].reshape((R, r), order="F"), mx
+    if getattr(f, "device_gather", False):
+        return f.sitetensor_gathered(Ib, Jb, Inext, solve)
     if not hasattr(f, "h"):
         return _sitetensor_generic(f, Ib, Jb, Inext, solve)
     ctx = f.ctx

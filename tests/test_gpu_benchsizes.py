@@ -1,7 +1,7 @@
 """Parity at the benchmarked sizes: the rrLU of BASELINE config 2
 (4096 x 4096, r = 256) and of the metric matrix (8192 x 8192, r = 256) -- the very seed-0 U[0,1)
 matrices bench.py factorises -- bitwise against the CPU oracle (permutations, L, U, npivot,
-error), leftorthogonal true and false, with the certified fp32 shadow search on (the default) and
+error), leftorthogonal true and false, with the certified fp16 shadow search on (the default) and
 off. Reference: src/matrixlu.jl:346-396 (_optimizerrlu!), benchmark/rrlu.jl:13-18.
 
 The oracle takes ~3 s (4096^2) and ~11 s (8192^2) per factorisation on one core; each oracle

@@ -14,7 +14,8 @@ import oracle_lib as O
 
 # the library's deferred-update depth (tci_abi.cpp tci_ctx::flush_every, env TCI_RRLU_NB), restored
 # after tests that change it
-LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "11"))
+LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "10"))
+LIB_DEFAULT_EPOCHS = int(os.environ.get("TCI_RRLU_EPOCHS", "3"))
 
 pytestmark = pytest.mark.gpu
 
@@ -26,7 +27,7 @@ def ctx(request):
     """Every test runs four times: with the default size-based choice of rrLU path (one-workgroup
     LDS kernel for small Pi, persistent grid for mid-size Pi, the pass pipeline above), with the
     mid-size path for everything it fits, and with the pass pipeline forced for every size, with
-    the certified fp32 shadow search (default) and without it (every pass reads fp64)."""
+    the certified fp16 shadow search (default) and without it (every pass reads fp64)."""
     c = T.Context(0)
     c.check(c.lib.tci_set_rrlu_small(c.h, int(request.param == "default")))
     c.check(c.lib.tci_set_rrlu_mid(c.h, int(request.param not in ("pipeline", "pipeline_exact"))))

@@ -1,4 +1,5 @@
-"""GPU parity of the certified fp32 shadow search (k_pass_sh): the pass pipeline with
+"""GPU parity of the certified fp16 shadow search (k_pass_mf, DESIGN.md K2, with its two-level epoch of
+refreshes and deep exact passes k_pass_x): the pass pipeline with
 the shadow on must give the reference's bits (oracle) on inputs chosen to stress the certificate:
 massive ties, exact zeros after the rank, rapidly decaying pivots (the kernel falls back to the
 exact body pass by pass), magnitudes where fp32 would underflow or overflow, NaN and Inf entries,
@@ -13,7 +14,8 @@ import oracle_lib as O
 
 # the library's deferred-update depth (tci_abi.cpp tci_ctx::flush_every, env TCI_RRLU_NB), restored
 # after tests that change it
-LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "11"))
+LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "10"))
+LIB_DEFAULT_EPOCHS = int(os.environ.get("TCI_RRLU_EPOCHS", "3"))
 
 pytestmark = pytest.mark.gpu
 
@@ -63,16 +65,41 @@ def rand(m, n, seed):
     return O.fill_uniform(m * n, seed=seed).reshape((m, n), order="F")
 
 
-@pytest.mark.parametrize("nb", [2, 10, 16])
+@pytest.mark.parametrize("nb,epochs", [(2, 1), (10, 1), (16, 1), (2, 4), (3, 10), (5, 6), (8, 4), (10, 3),
+                                       (15, 2)])
 @pytest.mark.parametrize("leftorth", [True, False])
-def test_shadow_random(pctx, nb, leftorth):
+def test_shadow_random(pctx, nb, epochs, leftorth):
+    """Every schedule of the two-level epoch: shadow epochs of nb pivots, a refresh
+    of the shadow by the MFMA search after each, an fp64 write-back after every epochs-th (exact
+    pending updates up to nb * epochs, x's in LDS from 12 on) -- the reference's bits each time."""
     pctx.check(pctx.lib.tci_set_rrlu_flush(pctx.h, nb))
+    pctx.check(pctx.lib.tci_set_rrlu_epochs(pctx.h, epochs))
     try:
-        A = rand(1100, 900, 11 + nb)
+        A = rand(1100, 900, 11 + nb + 100 * epochs)
         kw = dict(maxrank=180, leftorthogonal=leftorth)
         assert_same(outcome_gpu(A, pctx, **kw), outcome_ref(A, **kw))
     finally:
         pctx.check(pctx.lib.tci_set_rrlu_flush(pctx.h, LIB_DEFAULT_NB))
+        pctx.check(pctx.lib.tci_set_rrlu_epochs(pctx.h, LIB_DEFAULT_EPOCHS))
+
+
+@pytest.mark.parametrize("epochs", [2, 3])
+def test_shadow_refresh_fallbacks(pctx, epochs):
+    """Decays at which the refresh's accumulated bound stops certifying part of the way through an
+    exact epoch: refreshes then rewrite the shadow from exact values (k_pass_x mode 2), later read
+    passes of the same epoch run k_pass_x's exact body with up to nb * epochs pending updates."""
+    rng = np.random.default_rng(epochs)
+    pctx.check(pctx.lib.tci_set_rrlu_epochs(pctx.h, epochs))
+    try:
+        for base in (1.05, 1.2, 1.6):
+            Q1 = rng.standard_normal((900, 200))
+            Q2 = rng.standard_normal((200, 800))
+            A = (Q1 * base ** -np.arange(200.0)) @ Q2
+            for lo in (True, False):
+                kw = dict(maxrank=150, reltol=0.0, leftorthogonal=lo)
+                assert_same(outcome_gpu(A, pctx, **kw), outcome_ref(A, **kw))
+    finally:
+        pctx.check(pctx.lib.tci_set_rrlu_epochs(pctx.h, LIB_DEFAULT_EPOCHS))
 
 
 @pytest.mark.parametrize("scale", [1e-300, 1e-45, 1e-36, 1e-30, 1e25, 1e31, 1e40, 1e150, 1e300])

@@ -151,3 +151,77 @@ def test_complex_mfma_shadow_bound():
             worst = max(worst, err / epsd)
     assert worst < 1.0, worst
     assert worst > 1e-3
+
+
+def sh_cert(pv, k, PS, PE, nbs, tight=7):
+    """Python restatement of tci_rrlu.hip sh_cert (two-level epoch): (eps in absolute units,
+    certified) of the shadow-search pass after pivot k."""
+    te, t0 = k - PE + 1, k - PS + 1
+    d = 0.0
+    e = te
+    while True:
+        cur = e >= t0
+        ke = k if cur else e + nbs - 1
+        P = ke - e + 1
+        sumM = float(np.sum(pv[e:ke + 1]))
+        maxM = float(np.max(pv[e:ke + 1]))
+        s = sh_scale(pv[0] if e == 0 else 2.0 * pv[e - 1])
+        Mfd = pv[e] + d
+        mag = Mfd + 2.0 * sumM
+        ea = (d + 2.0 ** -11 * (1 + 2.0 ** -9) * Mfd + 2.0 ** -25 / s + 2.0 ** -19 * sumM + P * 2.0 ** -24 / s
+              + (3 * P + 4) * 2.0 ** -23 * mag) if s > 0 else 0.0
+        ok = s > 0 and mag < 2.0 ** 100 and maxM * s <= 2.0 ** 15 and ea * s < math.ldexp(pv[ke] * s, -tight)
+        if cur:
+            return ea, ok
+        d = ea if ok else 0.0
+        e += nbs
+
+
+@pytest.mark.parametrize("seed,decay,nb", [(0, 0.0, 5), (1, 0.0, 10), (2, 0.02, 4), (3, 0.0, 3)])
+def test_real_two_level_epoch_accumulated_bound(seed, decay, nb):
+    """The two-level epoch: each shadow epoch of nb pivots ends with a refresh that
+    stores fl16(s_new / s_old W) -- W the MFMA search's fp32 value, not the exact one -- so the next
+    epochs start from a shadow whose error against the exact stale values is the previous pass's
+    whole bound. Emulated over 3 epochs (up to 3 nb exact pending updates) on genuine
+    full-pivoting states: every W stays within the recursive bound sh_cert uses."""
+    rng = np.random.default_rng(seed)
+    m, n = 150, 130
+    A = rng.random((m, n)) - 0.3
+    if decay:
+        A = A * np.exp(-decay * np.arange(n))[None, :]
+    epochs = 3
+    steps = nb * epochs + 1
+    piv, X, Y, blocks = lu_states(A, steps + 1)
+    pv = np.abs(np.array(piv))
+    worst = 0.0
+    stale0, rows_s, cols_s = blocks[0]
+    s_cur = sh_scale(pv[0])
+    h = f16((stale0 * s_cur).astype(np.float32)).astype(np.float32)  # pass 0 writes the shadow of A
+    t0 = 0
+    for k in range(1, steps):
+        PS = k - t0 + 1
+        PE = k + 1  # no write-back inside the emulated exact epoch
+        stale_k, rows_k, cols_k = blocks[k + 1]
+        ri = [int(np.where(rows_s == q)[0][0]) for q in rows_k]
+        ci = [int(np.where(cols_s == q)[0][0]) for q in cols_k]
+        W = h[np.ix_(ri, ci)].astype(np.float32).copy()
+        for q in range(t0, k + 1):
+            xs = restrict(X[q], rows_k)
+            ys = restrict(Y[q], cols_k) * s_cur
+            xh, xl = split(-xs)
+            yh, yl = split(ys)
+            for a, b in ((xh, yh), (xh, yl), (xl, yh)):
+                W = (W + np.outer(a, b).astype(np.float32)).astype(np.float32)
+        ea, ok = sh_cert(pv, k, PS, PE, nb)
+        err = np.abs(W.astype(np.float64) / s_cur - stale_k).max()
+        if ok:
+            worst = max(worst, err / ea)
+        if PS == nb and k + 1 < steps:  # refresh: the new epoch's shadow from W (trailing block after k)
+            s_new = sh_scale(2.0 * pv[k])
+            if ok:
+                h = f16((W * np.float32(s_new / s_cur)).astype(np.float32)).astype(np.float32)
+            else:  # a refresh that cannot certify writes the exact values
+                h = f16((stale_k * s_new).astype(np.float32)).astype(np.float32)
+            rows_s, cols_s, s_cur, t0 = rows_k, cols_k, s_new, k + 1
+    assert worst < 1.0, worst
+    assert worst > 1e-3
