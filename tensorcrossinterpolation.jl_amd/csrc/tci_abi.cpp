@@ -60,7 +60,7 @@ struct tci_ctx {
     unsigned* bar = nullptr;   // mid path: grid-barrier counter
     int* fault = nullptr;      // mid path: barrier timeout flag
     int* flag = nullptr;
-    unsigned* ticket = nullptr;  // rrLU pass tail hand-off counter (zero between passes)
+    unsigned* ticket = nullptr;  // rrLU pass tail hand-off counters: [0] top, [16 (1 + c)] XCD class c (zero between passes)
     char* hin = nullptr;         // pinned staging for uploads / downloads of the small path
     size_t capHin = 0;
     char* hout = nullptr;
@@ -379,7 +379,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
-    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
+    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid + 8))) return st;  // + the XCD-class candidates
     const int mi = (int)m, ni = (int)n;
     tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, ni);
     int64_t mr = std::min<int64_t>(maxrank, std::min<int64_t>(m, n));
@@ -702,7 +702,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->colposL, &c->capColposL, (size_t)nloc + 2))) return st;
-    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid))) return st;
+    if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid + 8))) return st;  // + the XCD-class candidates
     const bool multi = nranks > 1 || comm || exch;
     if (!multi && nranks != 1) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
     if ((st = ensure(c, &c->lout, &c->capLout, (size_t)nranks + 1))) return st;  // [own, all-gathered ...]
@@ -861,10 +861,10 @@ int tci_ctx_create(int device, tci_ctx** out) {
     bool ok = hipMalloc((void**)&c->st, sizeof(RrluState)) == hipSuccess &&
               hipHostMalloc((void**)&c->hst, sizeof(RrluState), 0) == hipSuccess &&
               hipMalloc((void**)&c->flag, sizeof(int)) == hipSuccess &&
-              hipMalloc((void**)&c->ticket, sizeof(unsigned)) == hipSuccess &&
+              hipMalloc((void**)&c->ticket, 256 * sizeof(unsigned)) == hipSuccess &&
               hipMalloc((void**)&c->bar, sizeof(unsigned)) == hipSuccess &&
               hipMalloc((void**)&c->fault, sizeof(int)) == hipSuccess &&
-              hipMemset(c->ticket, 0, sizeof(unsigned)) == hipSuccess &&
+              hipMemset(c->ticket, 0, 256 * sizeof(unsigned)) == hipSuccess &&
               hipHostMalloc((void**)&c->hflag, sizeof(int), 0) == hipSuccess &&
               hipHostMalloc((void**)&c->hpoll, 2 * sizeof(RrluState), 0) == hipSuccess &&
               hipEventCreateWithFlags(&c->pollev[0], hipEventDisableTiming) == hipSuccess &&

@@ -262,6 +262,10 @@ __device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
 #define PPROF(i) ((void)pt)
 #endif
 
+#ifndef TCI_TICKET_XCD
+#define TCI_TICKET_XCD 0  // pass tail: 1 = per-XCD-class counters + a top counter (measured 2.7 us slower per pass than one counter)
+#endif
+
 // Pass tail: block reduction of the workgroups' candidates, then the hand-off to the last one
 // (sc1 stores + agent-scope ticket), which reduces all of them and commits pivot sel.selk.
 template <int NT>
@@ -274,6 +278,63 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     block_reduce_cand<NT>(best);
     if (sel.selk < 0) return;
     __shared__ int last_s;
+#if TCI_TICKET_XCD
+    // Two-level hand-off (MI355X_MICROARCH.md price list, fanin: shard the counter per XCD): the
+    // workgroups of one blockIdx % 8 class (one XCD under the round-robin dispatch; speed only)
+    // count on their own line, the last of each class reduces the class's candidates and publishes
+    // one, and the last of the <= 8 class leaders reduces those and commits. Each level is the
+    // hand-off table's first row (sc1 stores, vmcnt(0), one agent-scope counter, the last adder
+    // reads). The reduction order does not matter: cand_better is a strict total order.
+    const int ncls = min((int)gridDim.x, 8);
+    const int cls = (int)blockIdx.x & 7;
+    const int csize = ((int)gridDim.x - cls + 7) >> 3;  // blocks b < grid with b % 8 == cls
+    unsigned* ctick = sel.ticket + 16 * (1 + cls);      // own 64-B line
+    if (threadIdx.x == 0) {
+#if TCI_PASS_PROF
+        for (int i = 0; i < 4; ++i)
+            __hip_atomic_store(&g_pprof[blockIdx.x * 8 + i], pt[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        store_cand_sc1(cand + blockIdx.x, best);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(ctick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = (old == (unsigned)csize - 1);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    {
+        constexpr int CPC = kMaxPassGrid / 8 / NT > 0 ? kMaxPassGrid / 8 / NT : 1;
+        CandR cs[CPC];
+#pragma unroll
+        for (int u = 0; u < CPC; ++u) {
+            const int i = threadIdx.x + u * NT;
+            cs[u] = i < csize ? load_cand_sc1(cand + cls + 8 * i) : cand_none();
+        }
+        CandR wc = cs[0];
+#pragma unroll
+        for (int u = 1; u < CPC; ++u) cand_take(wc, cs[u]);
+        __syncthreads();  // block_reduce_cand's LDS slots are reused
+        block_reduce_cand<NT>(wc);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(ctick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            store_cand_sc1(cand + kMaxPassGrid + cls, wc);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned old = __hip_atomic_fetch_add(sel.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_s = (old == (unsigned)ncls - 1);
+            PPROF(4);
+        }
+        __syncthreads();
+        if (!last_s) return;
+    }
+    int64_t rk = -1, ck = -1;
+    if (threadIdx.x == 0) {
+        rk = sel.rowphys[sel.selk];
+        ck = sel.colphys[sel.selk];
+    }
+    CandR w = threadIdx.x < ncls ? load_cand_sc1(cand + kMaxPassGrid + threadIdx.x) : cand_none();
+    __syncthreads();
+    block_reduce_cand<NT>(w);
+#else
     if (threadIdx.x == 0) {
 #if TCI_PASS_PROF
         for (int i = 0; i < 4; ++i)
@@ -309,6 +370,7 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
     __syncthreads();  // block_reduce_cand's LDS slots are reused
     block_reduce_cand<NT>(w);
+#endif
     if (threadIdx.x == 0) {
         __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (sel.lout) {  // column-sharded: this rank's winner, committed after the exchange
@@ -1104,6 +1166,9 @@ struct MfGeom {
     static constexpr int YS = ymem ? 1 : P;
 };
 
+#ifndef TCI_EXT_B
+#define TCI_EXT_B 16 // two-level epoch: pending loads in flight per thread in the x_k / y_k chains
+#endif
 // v - x_0 y_0 - x_1 y_1 - ... (cnt terms, in order; separate multiply and subtract, the
 // reference's arithmetic) with strided x / y loads, kB of each in flight at a time
 template <int kB>
@@ -1124,9 +1189,29 @@ __device__ __forceinline__ double pend_apply(double v, const double* __restrict_
     return v;
 }
 
+// the same with one side a uniform vector already in LDS (stride 1), kB loads of the other side
+// in flight at a time
+template <int kB>
+__device__ __forceinline__ double pend_apply_l(double v, const double* __restrict__ xp, int64_t xst,
+                                               const double* yl, int cnt, bool x_first) {
+    for (int s0 = 0; s0 < cnt; s0 += kB) {
+        double xv[kB];
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+            if (s0 + i < cnt) xv[i] = xp[(int64_t)(s0 + i) * xst];
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+            if (s0 + i < cnt)
+                v = __dsub_rn(v, x_first ? __dmul_rn(xv[i], yl[s0 + i]) : __dmul_rn(yl[s0 + i], xv[i]));
+    }
+    return v;
+}
+
 template <int P, bool EXT = false>
 struct P2MfLds {
     using Gm = MfGeom<P, EXT>;
+    double pxa[EXT ? kMaxPendR : 1];  // EXT: X[s][a] and Y[s][b] of the pivot (uniform), s < PE - 1
+    double pyb[EXT ? kMaxPendR : 1];
     double ys[kP2StageCols * Gm::YS];                 // exact y's of the staged columns (examinations)
     _Float16 yb[kP2StageCols * Gm::KSP];              // their B fragments (y splits)
     int cpos[kP2StageCols];
@@ -1243,6 +1328,13 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     if (st->done) return false;
     const int a = (int)st->p, bq = (int)st->q;
     const double piv = st->pval;
+    if constexpr (EXT) {  // the pivot row's pending x's / column's pending y's, once per workgroup
+        if ((int)threadIdx.x < PE - 1) {
+            L.pxa[threadIdx.x] = g.X[(int64_t)threadIdx.x * ldx + a];
+            L.pyb[threadIdx.x] = g.Y[(int64_t)threadIdx.x * ldy + bq];
+        }
+        __syncthreads();
+    }
     if (!stager) {
         // row thread: x_k of its row (the reference's operation order), the split A fragment row
         // -(x_0 .. x_{P-1}) with the data masking of rows outside the trailing block
@@ -1251,8 +1343,8 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
 #pragma unroll
         for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
         double xk = g.A[rr + (int64_t)bq * lda];
-        if constexpr (EXT) {  // all PE - 1 exact pending updates, 16 loads in flight at a time
-            xk = pend_apply<16>(xk, g.X + rr, ldx, g.Y + bq, ldy, PE - 1);
+        if constexpr (EXT) {  // all PE - 1 exact pending updates, 8 loads in flight at a time
+            xk = pend_apply_l<TCI_EXT_B>(xk, g.X + rr, ldx, L.pyb, PE - 1, true);
         } else {
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
@@ -1442,7 +1534,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                 for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)(off + s) * ldy + jst];
                 double yk = g.A[a + (int64_t)jst * lda];
                 if constexpr (EXT) {
-                    yk = pend_apply<16>(yk, g.X + a, ldx, g.Y + jst, ldy, PE - 1);
+                    yk = pend_apply_l<TCI_EXT_B>(yk, g.Y + jst, ldy, L.pxa, PE - 1, false);
                 } else {
 #pragma unroll
                     for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
@@ -1614,9 +1706,19 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
         const int hb = tr * kRowsPerTile + half * kXHalf;  // first row of the half
         if (hb >= m) break;
         __syncthreads();  // the previous half's readers are done with xs / ys
-        for (int e = threadIdx.x; e < (P - 1) * kXHalf; e += kP2Threads) {
-            const int s = e / kXHalf, rr = e - s * kXHalf;
-            L.xs[e] = hb + rr < m ? g.X[(int64_t)s * ldx + hb + rr] : 0.0;
+        {  // the half's pending x's, all of a thread's loads in flight at once
+            constexpr int kPer = kMaxPendR * kXHalf / kP2Threads;  // 8
+            double v[kPer];
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int e = threadIdx.x + u * kP2Threads, s = e / kXHalf, rr = e - s * kXHalf;
+                v[u] = (s < P - 1 && hb + rr < m) ? g.X[(int64_t)s * ldx + hb + rr] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int e = threadIdx.x + u * kP2Threads;
+                if (e < (P - 1) * kXHalf) L.xs[e] = v[u];
+            }
         }
         __syncthreads();
         if (threadIdx.x < kXHalf) {  // x_k of the half's rows (pivot k's column, updates applied)
@@ -1644,22 +1746,39 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
             const int gcols = min(G, ntc - g0) * cb;
             const int nch = gcols / kXU;
             if (g0 > 0) __syncthreads();  // the previous group's readers are done with ys / cpos
-            if (threadIdx.x < gcols) {
-                const int lc = threadIdx.x, j = col_of(g0, lc);
-                const int cp = j < n ? colpos[j] : -1;
-                L.cpos[lc] = cp;
-                if (cp > k) {
-                    double yk = A[a + (int64_t)j * lda];
-                    for (int s = 0; s < P - 1; ++s) {
-                        const double yv = g.Y[(int64_t)s * ldy + j];
-                        L.ys[s * kXStage + lc] = yv;
-                        yk = __dsub_rn(yk, __dmul_rn(L.xa[s], yv));
-                    }
+            // staging in two steps: every thread loads a share of the group's pending y's into LDS
+            // (all in flight at once), then one thread per column runs y_k's sequential chain from
+            // LDS (the reference's order)
+            {
+                constexpr int kPer = kMaxPendR * kXStage / kP2Threads;  // 4
+                const int lc = threadIdx.x & (kXStage - 1), s0 = threadIdx.x / kXStage;
+                const int j = lc < gcols ? col_of(g0, lc) : 0;
+                double v[kPer];
+#pragma unroll
+                for (int u = 0; u < kPer; ++u) {
+                    const int s = s0 + u * (kP2Threads / kXStage);
+                    v[u] = (s < P - 1 && lc < gcols) ? g.Y[(int64_t)s * ldy + j] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kPer; ++u) {
+                    const int s = s0 + u * (kP2Threads / kXStage);
+                    if (s < P - 1) L.ys[s * kXStage + lc] = v[u];
+                }
+            }
+            const int lcs = threadIdx.x, js = lcs < gcols ? col_of(g0, lcs) : 0;
+            const int cps = (lcs < gcols && js < n) ? colpos[js] : -1;
+            const double ypr = (lcs < gcols && cps > k) ? A[a + (int64_t)js * lda] : 0.0;
+            __syncthreads();
+            if (lcs < gcols) {
+                L.cpos[lcs] = cps;
+                if (cps > k) {
+                    double yk = ypr;
+                    for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(L.xa[s], L.ys[s * kXStage + lcs]));
                     if (!leftorth) yk = yk / piv;
-                    L.ys[(P - 1) * kXStage + lc] = yk;
+                    L.ys[(P - 1) * kXStage + lcs] = yk;
                     if (tr == 0 && half == 0) {
-                        g.Y[(int64_t)(P - 1) * ldy + j] = yk;
-                        g.Up[k + (int64_t)j * g.ldu] = yk;
+                        g.Y[(int64_t)(P - 1) * ldy + js] = yk;
+                        g.Up[k + (int64_t)js * g.ldu] = yk;
                     }
                 }
             }
