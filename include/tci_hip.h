@@ -280,6 +280,27 @@ int tci_tci2_errors(tci_tci2* tci, double* maxsample, double* bonderrors, double
 int tci_tci2_sweep2site(tci_tci2* tci, const tci_func* f, int32_t niter, int32_t iter1,
                         double abstol, int64_t maxbonddim, int32_t sweepstrategy,
                         int32_t strictlynested);
+/* tci_tci2_sweep2site followed by fillsitetensors!'s maxsample update (see tci_tci2_fill_maxsample)
+ * in the same device launch when the device-resident path runs; *filled = 0: the caller runs
+ * its own fill loop. */
+int tci_tci2_sweep2site_fill(tci_tci2* tci, const tci_func* f, int32_t niter, int32_t iter1,
+                             double abstol, int64_t maxbonddim, int32_t sweepstrategy,
+                             int32_t strictlynested, int* filled);
+/* All sites of one bank in one call: counts[p] entries of set p, the sets concatenated in site
+ * order (a width-0 set contributes no ints). get: packed may be NULL (counts only); capacity in
+ * ints. */
+int tci_tci2_set_sets(tci_tci2* tci, int which, const int64_t* counts, const int32_t* packed);
+int tci_tci2_get_sets(tci_tci2* tci, int which, int64_t* counts, int32_t* packed, int64_t capacity);
+/* fillsitetensors! with the solve unobservable (globalsearch.jl:202-208; tensorci2.jl:599-611):
+ * updatemaxsample!(tci, Pi1) over every site, on the device in one launch for the staged catalog
+ * kinds. *handled = 0: not done here (other kinds, a non-square pivot matrix, a site too large);
+ * the caller runs its own loop (tci_sitetensor_h / a batch maxabs per site). */
+int tci_tci2_fill_maxsample(tci_tci2* tci, const tci_func* f, int* handled);
+/* Device-resident sweeps (tci_sweep_small.hip): while every bond's Pi fits the one-workgroup rrLU,
+ * tci_tci2_sweep2site runs whole iterations in one kernel launch for the staged catalog kinds
+ * (SUM, LORENTZ, TABLE, GAUSS, QOSC, QEXP), bitwise the per-bond loop; on by default (env
+ * TCI_SWEEP_SMALL=0 disables). */
+int tci_set_sweep_small(tci_ctx* ctx, int enabled);
 
 /* ---------------------------------------------------- site-tensor solve
  * Replaces setsitetensor!(tci, f, b) (tensorci2.jl:599-629): Pi1 = f(Iset_b x d x Jset_b),

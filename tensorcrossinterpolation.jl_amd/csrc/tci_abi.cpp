@@ -67,6 +67,17 @@ struct tci_ctx {
     size_t capHout = 0;
     char* zbuf = nullptr;  // mapped pinned host memory the small path's kernels write into
     char* zdev = nullptr;  // its device address
+    int small_sweep = 1;   // device-resident small sweeps (tci_sweep_small.hip; env TCI_SWEEP_SMALL=0)
+    int32_t* sw_ws = nullptr;   // their six banks of index sets
+    size_t capSwWs = 0;
+    char* sw_inbuf = nullptr;   // device copy of the input image
+    size_t capSwInbuf = 0;
+    char* sw_in = nullptr;      // mapped host I/O images (SwIO)
+    char* sw_in_d = nullptr;
+    size_t capSwIn = 0;
+    char* sw_out = nullptr;
+    char* sw_out_d = nullptr;
+    size_t capSwOut = 0;
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
@@ -266,6 +277,25 @@ int ensure_mapped(tci_ctx* c, size_t bytes) {
 }
 
 // pinned host staging buffer (grown on demand; the stream is idle whenever it is reallocated)
+int ensure_mapped_pair(tci_ctx* c, char** h, char** d, size_t* cap, size_t bytes) {
+    if (bytes <= *cap && *h) return TCI_OK;
+    const size_t want = std::max<size_t>(bytes, 1 << 16);
+    if (*h) {
+        hipStreamSynchronize(c->stream);
+        hipHostFree(*h);
+        *h = *d = nullptr;
+        *cap = 0;
+    }
+    if (hipHostMalloc((void**)h, want, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)d, *h, 0) != hipSuccess) {
+        *h = *d = nullptr;
+        return set_err(c, TCI_ERR_NOMEM, "mapped host allocation of " + std::to_string(want) +
+                                             " bytes failed");
+    }
+    *cap = want;
+    return TCI_OK;
+}
+
 int ensure_pinned(tci_ctx* c, char** p, size_t* cap, size_t bytes) {
     if (bytes <= *cap && *p) return TCI_OK;
     size_t want = std::max<size_t>(bytes, 1 << 16);
@@ -845,6 +875,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
+    if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
     if (const char* e = getenv("TCI_C128_SH")) c->c128_sh = atoi(e) != 0;
@@ -898,6 +929,9 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->hin) hipHostFree(c->hin);
     if (c->hout) hipHostFree(c->hout);
     if (c->zbuf) hipHostFree(c->zbuf);
+    fr(c->sw_ws); fr(c->sw_inbuf);
+    if (c->sw_in) hipHostFree(c->sw_in);
+    if (c->sw_out) hipHostFree(c->sw_out);
     if (c->hfn) hipHostFree(c->hfn);
     for (auto e : c->evpool) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -927,6 +961,12 @@ int tci_set_rrlu_epochs(tci_ctx* c, int epochs) {
 
 int tci_set_rrlu_small(tci_ctx* c, int enabled) {
     c->small_path = enabled != 0;
+    return TCI_OK;
+}
+
+int tci_set_sweep_small(tci_ctx* c, int enabled) {
+    if (!c) return TCI_ERR_ARG;
+    c->small_sweep = enabled != 0;
     return TCI_OK;
 }
 
@@ -2357,3 +2397,60 @@ int tci_cache_batcheval_h(tci_ctx* c, tci_cache* h, const tci_func* f, const int
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- device-resident small sweeps
+// Called by tci_sweep.cpp (C++ linkage): whether f / L can take the path, one launch of
+// k_sweep_small on the SwIO images (tci_internal.h), and the reference's message for a status.
+bool tci_sweep_small_ok(tci_ctx* c, const tci_func* f, int L) {
+    return c && f && c->small_path && c->small_sweep && L >= 2 && L <= tci::kSwMaxL && !f->hostfn &&
+           tci::sweep_small_kind(f->kind);
+}
+
+int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
+                        int mode, int fill, int niter, int iter1, int strategy, int strictlynested, double abstol,
+                        int64_t maxbonddim, std::vector<char>& out) {
+    auto width = [&](int bank, int p) { return (bank & 1) ? L - 1 - p : p; };
+    const int64_t tot = 6 * cap * ((int64_t)L * (L - 1) / 2);  // six banks (tci_sweep_small.hip)
+    const tci::SwIO io = tci::sw_io(L);
+    const size_t outcap = io.sets + (size_t)tot * 4;
+    int st;
+    if ((st = ensure(c, &c->sw_ws, &c->capSwWs, (size_t)std::max<int64_t>(tot, 1)))) return st;
+    if ((st = ensure(c, &c->sw_inbuf, &c->capSwInbuf, inbytes))) return st;
+    if ((st = ensure_mapped_pair(c, &c->sw_in, &c->sw_in_d, &c->capSwIn, inbytes))) return st;
+    if ((st = ensure_mapped_pair(c, &c->sw_out, &c->sw_out_d, &c->capSwOut, outcap))) return st;
+    memcpy(c->sw_in, in, inbytes);
+    HIPCHK(c, hipMemcpyAsync(c->sw_inbuf, c->sw_in, inbytes, hipMemcpyHostToDevice, c->stream));
+    tci::SweepSmallArgs a;
+    a.f = f->view();
+    a.L = L;
+    a.ws = c->sw_ws;
+    a.cap = cap;
+    a.inbuf = c->sw_inbuf;
+    a.out = c->sw_out_d;
+    a.niter = niter;
+    a.iter1 = iter1;
+    a.strategy = strategy;
+    a.strictlynested = strictlynested;
+    a.abstol = abstol;
+    a.maxbonddim = maxbonddim;
+    a.mode = mode;
+    a.fill = fill;
+    HIPCHK(c, tci::launch_sweep_small(c->stream, a));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t* hdr = reinterpret_cast<const int64_t*>(c->sw_out);
+    const int64_t* cn = reinterpret_cast<const int64_t*>(c->sw_out + io.counts);
+    size_t bytes = io.sets;
+    const int nb = (hdr[0] == 1 && hdr[4]) ? 6 : 4;
+    for (int b = 0; b < nb; ++b)
+        for (int p = 0; p < L; ++p) bytes += (size_t)cn[(size_t)b * L + p] * width(b, p) * 4;
+    if (bytes > outcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: output image overflow");
+    out.assign(c->sw_out, c->sw_out + bytes);
+    return TCI_OK;
+}
+
+int tci_sweep_small_error(tci_ctx* c, int status, int64_t bond) {
+    if (status == 2) return set_err(c, TCI_ERR_NAN, "lu.L contains NaNs");
+    if (status == 3) return set_err(c, TCI_ERR_NAN, "lu.U contains NaNs");
+    if (status == 4) return set_err(c, TCI_ERR_NONSQ, "Pivot matrix at bond " + std::to_string(bond) + " is not square!");
+    return set_err(c, TCI_ERR_DEVICE, "device sweep: status " + std::to_string(status));
+}

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 
+#include "tci_funcdev.h"
 #include "tci_internal.h"
 
 namespace tci {
@@ -309,26 +310,7 @@ void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t
 // sum, an integer bit index, a table offset, a partial sum of squares) run in two stages:
 // per-row and per-column "state" (O((m+n)L)), then one pass that combines and writes
 // Pi[R + ldo*j] -- an HBM-write-bound stream. Other kinds evaluate directly per element.
-enum { F_SUM = 0, F_LORENTZ = 1, F_TABLE = 2, F_GAUSS = 3, F_GAUSSMIX = 4, F_QOSC = 5, F_QEXP = 6,
-       F_TT = 7, F_CP = 8, F_MPO = 9 };
-
-// Kinds that are a sum of K separable terms, f = sum_k rowfactor_k(I, c) * colfactor_k(J): Pi is
-// a rank-K product EL * ER^T, assembled by an fp64 MFMA GEMM (k_gemm_cp).
-__host__ __device__ __forceinline__ bool cp_kind(int kind) {
-    return kind == F_GAUSSMIX || kind == F_CP || kind == F_MPO;
-}
-
-__host__ __device__ __forceinline__ bool staged_kind(int kind) {
-    return kind == F_SUM || kind == F_LORENTZ || kind == F_TABLE || kind == F_GAUSS ||
-           kind == F_QOSC || kind == F_QEXP;
-}
-
-// state of a leg value v (1-based) at global position t; combined by integer/double addition or
-// bit concatenation.
-union St {
-    int64_t i;
-    double d;
-};
+// the kinds, St, leg_state() and combine<KIND>(): tci_funcdev.h
 
 // Row states: R in [0, m*D); i = R % m, c = R / m (centre index, only for M == 1).
 __global__ void k_state_rows(FuncDev f, const int32_t* __restrict__ I, int m, int nl, int M,
@@ -337,43 +319,7 @@ __global__ void k_state_rows(FuncDev f, const int32_t* __restrict__ I, int m, in
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t R = gid; R < (int64_t)m * D; R += stride) {
         const int i = (int)(R % m), c = (int)(R / m);
-        const int32_t* e = I + (int64_t)i * nl;
-        St s;
-        s.i = 0;
-        switch (f.kind) {
-        case F_SUM:
-            for (int t = 0; t < nl; ++t) s.i += e[t];
-            if (M) s.i += c + 1;
-            break;
-        case F_LORENTZ:
-            for (int t = 0; t < nl; ++t) s.i += (int64_t)e[t] * e[t];
-            if (M) s.i += (int64_t)(c + 1) * (c + 1);
-            break;
-        case F_TABLE:
-            for (int t = 0; t < nl; ++t) s.i += (int64_t)(e[t] - 1) * f.strides[t];
-            if (M) s.i += (int64_t)c * f.strides[nl];
-            break;
-        case F_GAUSS: {
-            double a = 0.0;
-            for (int t = 0; t < nl; ++t) {
-                const double u = (double)e[t] - f.params[1];
-                a = __dadd_rn(a, __dmul_rn(u, u));
-            }
-            if (M) {
-                const double u = (double)(c + 1) - f.params[1];
-                a = __dadd_rn(a, __dmul_rn(u, u));
-            }
-            s.d = a;
-        } break;
-        case F_QOSC:
-        case F_QEXP: {
-            uint64_t idx = 0;
-            for (int t = 0; t < nl; ++t) idx = (idx << 1) | (uint64_t)(e[t] - 1);
-            if (M) idx = (idx << 1) | (uint64_t)c;
-            s.i = (int64_t)idx;
-        } break;
-        }
-        out[R] = s;
+        out[R] = leg_state(f, I + (int64_t)i * nl, nl, 0, M ? c + 1 : 0);
     }
 }
 
@@ -382,62 +328,8 @@ __global__ void k_state_cols(FuncDev f, const int32_t* __restrict__ J, int n, in
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t j = gid; j < n; j += stride) {
-        const int32_t* e = J + j * nr;
-        St s;
-        s.i = 0;
-        switch (f.kind) {
-        case F_SUM:
-            for (int t = 0; t < nr; ++t) s.i += e[t];
-            break;
-        case F_LORENTZ:
-            for (int t = 0; t < nr; ++t) s.i += (int64_t)e[t] * e[t];
-            break;
-        case F_TABLE:
-            for (int t = 0; t < nr; ++t) s.i += (int64_t)(e[t] - 1) * f.strides[toff + t];
-            break;
-        case F_GAUSS: {
-            double a = 0.0;
-            for (int t = 0; t < nr; ++t) {
-                const double u = (double)e[t] - f.params[1];
-                a = __dadd_rn(a, __dmul_rn(u, u));
-            }
-            s.d = a;
-        } break;
-        case F_QOSC:
-        case F_QEXP: {
-            uint64_t idx = 0;
-            for (int t = 0; t < nr; ++t) idx = (idx << 1) | (uint64_t)(e[t] - 1);
-            s.i = (int64_t)idx;
-        } break;
-        }
-        out[j] = s;
+        out[j] = leg_state(f, J + j * nr, nr, toff, 0);
     }
-}
-
-// value of one Pi element from its row and column states. Lorentzian: the quotient
-// p0 / (s + 1) of the integer sum of squares s comes from a table of the same quotients
-// (s <= sum_t d_t^2): bitwise the same division, no per-element fp64 divide.
-template <int KIND>
-__device__ __forceinline__ double combine(const double* __restrict__ p, double p0, St r, St c, int nr,
-                                          int L, const double* __restrict__ tab, int64_t ntab) {
-    if (KIND == F_SUM) return (double)(r.i + c.i);
-    if (KIND == F_LORENTZ) {
-        const int64_t s = r.i + c.i;
-        return s < ntab ? tab[s] : p0 / (double)(s + 1);
-    }
-    if (KIND == F_TABLE) return p[r.i + c.i];
-    if (KIND == F_GAUSS) return exp(-(p0 * __dadd_rn(r.d, c.d)));
-    if (KIND == F_QOSC) {
-        const uint64_t idx = ((uint64_t)r.i << nr) | (uint64_t)c.i;
-        const double x = ldexp((double)idx, -L);
-        return exp(-(p0 * x)) * sin(p[1] * pow(x, p[2]));
-    }
-    if (KIND == F_QEXP) {
-        const uint64_t idx = ((uint64_t)r.i << nr) | (uint64_t)c.i;
-        const double x = ldexp((double)idx, -L);
-        return __dadd_rn(p0 * exp(-(p[1] * x)), p[2] * exp(-(p[3] * x)));
-    }
-    return 0.0;
 }
 
 __global__ void k_lorentz_table(FuncDev f, double* __restrict__ tab, int64_t ntab) {

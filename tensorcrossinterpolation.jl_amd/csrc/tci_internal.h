@@ -339,4 +339,42 @@ void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, cons
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
                              int* piv, int dense);
 
+// ---- device-resident small sweep (tci_sweep_small.hip)
+constexpr int kSwMaxL = 64;      // tensor-train length the kernel takes
+constexpr int kSwPE = 136;       // pivot errors per iteration (np <= 128 on the small path, + lu.error)
+constexpr int kSwCatCap = 4096;  // kronecker + extra entries of one combined set before the union
+// Host <-> kernel I/O (mapped host memory), byte offsets: int64 header[16] (0 status: 0 done,
+// 1 resume at (it, q), 2 / 3 NaN in L / U at bond [7]; 1 it, 2 q, 3 has_history, 4 extra banks
+// valid, 5 npe, 6 maxsample bits, 7 bond, 8 fill status (-1 not run, 0 done, 4 non-square pivot
+// matrix at bond [9], 5 a site too large for it), 9 bond), int64 counts[6 L] (banks: Iset, Jset, history I / J, extra I / J;
+// a width-0 set's count is its number of empty entries), double bonderrors[L], double
+// pivoterrors[kSwPE], then the sets bank by bank, site by site, entries row-major.
+struct SwIO {
+    size_t counts, bonderr, pe, sets;
+};
+__host__ __device__ inline SwIO sw_io(int L) {
+    SwIO o;
+    o.counts = 16 * 8;
+    o.bonderr = o.counts + (size_t)6 * L * 8;
+    o.pe = o.bonderr + (size_t)L * 8;
+    o.sets = o.pe + (size_t)kSwPE * 8;
+    return o;
+}
+struct SweepSmallArgs {
+    FuncDev f;
+    int L;
+    int32_t* ws;           // set banks: bank b, site p at ws + cap (b L (L-1) / 2 + widths of sites < p)
+    int64_t cap;           // entries per set slot
+    const char* inbuf;     // device copy of the input image (SwIO)
+    char* out;             // mapped host output image (SwIO)
+    int niter, iter1, strategy, strictlynested;
+    double abstol;
+    int64_t maxbonddim;
+    int mode;              // 0: sweep2site! iterations; 1: fillsitetensors!'s maxsample update only
+    int fill;              // mode 0: the maxsample update after the iterations too (header [8] / [9])
+};
+bool sweep_small_kind(int kind);
+size_t sweep_small_lds_bytes();
+hipError_t launch_sweep_small(hipStream_t s, const SweepSmallArgs& a);
+
 }  // namespace tci

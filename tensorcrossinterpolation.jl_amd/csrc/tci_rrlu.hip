@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "tci_internal.h"
+#include "tci_smalllu.h"
 
 #ifndef TCI_PASS2_U
 #define TCI_PASS2_U 4  // k_pass2: columns per chunk (two chunks in flight per lane)
@@ -87,11 +88,6 @@ __device__ __forceinline__ double sh_bound(const double* pv, int t0) {
     return t0 == 0 ? fabs(pv[0]) : 2.0 * fabs(pv[t0 - 1]);
 }
 
-__device__ __forceinline__ double jl_max(double x, double y) {
-    bool ysel = (y > x) || (signbit(y) < signbit(x));
-    if (ysel) return isnan(x) ? x : y;
-    return isnan(y) ? y : x;
-}
 
 // (v1,c1,r1) beats (v2,c2,r2): larger abs2, then smaller column position, then smaller row
 // position -- the order in which the reference's column-major scan with strict '>' meets them.
@@ -1166,9 +1162,6 @@ struct MfGeom {
     static constexpr int YS = ymem ? 1 : P;
 };
 
-#ifndef TCI_EXT_B
-#define TCI_EXT_B 16 // two-level epoch: pending loads in flight per thread in the x_k / y_k chains
-#endif
 // v - x_0 y_0 - x_1 y_1 - ... (cnt terms, in order; separate multiply and subtract, the
 // reference's arithmetic) with strided x / y loads, kB of each in flight at a time
 template <int kB>
@@ -1189,20 +1182,33 @@ __device__ __forceinline__ double pend_apply(double v, const double* __restrict_
     return v;
 }
 
-// the same with one side a uniform vector already in LDS (stride 1), kB loads of the other side
-// in flight at a time
-template <int kB>
-__device__ __forceinline__ double pend_apply_l(double v, const double* __restrict__ xp, int64_t xst,
-                                               const double* yl, int cnt, bool x_first) {
-    for (int s0 = 0; s0 < cnt; s0 += kB) {
-        double xv[kB];
+// Two-level epoch chains, v - p_0 u_0 - p_1 u_1 - ... (cnt <= kMaxPendR - 1 terms, in order;
+// separate multiply and subtract): p_s = xp[s xst] per thread, the first kPendPre of them loaded
+// early (PendPre: requested before the pivot is read), the rest in one batch after those are
+// applied (all at once would cost 62 VGPRs: spills); u_s wave-uniform, lane s of upl. IEEE
+// multiplication commutes, so p u is the reference's x y bit for bit.
+constexpr int kPendPre = 16;
+static_assert(kMaxPendR - 1 <= 2 * kPendPre, "two batches");
+struct PendPre {
+    double v[kPendPre];
+};
+__device__ __forceinline__ void pend_pre(PendPre& p, const double* __restrict__ xp, int64_t xst, int cnt) {
 #pragma unroll
-        for (int i = 0; i < kB; ++i)
-            if (s0 + i < cnt) xv[i] = xp[(int64_t)(s0 + i) * xst];
+    for (int i = 0; i < kPendPre; ++i) p.v[i] = i < cnt ? xp[(int64_t)i * xst] : 0.0;
+}
+__device__ __forceinline__ double pend_chain(double v, const PendPre& p, const double* __restrict__ xp,
+                                             int64_t xst, double upl, int cnt) {
 #pragma unroll
-        for (int i = 0; i < kB; ++i)
-            if (s0 + i < cnt)
-                v = __dsub_rn(v, x_first ? __dmul_rn(xv[i], yl[s0 + i]) : __dmul_rn(yl[s0 + i], xv[i]));
+    for (int i = 0; i < kPendPre; ++i)
+        if (i < cnt) v = __dsub_rn(v, __dmul_rn(p.v[i], readlane_dbl(upl, i)));
+    if (cnt > kPendPre) {
+        double r[kMaxPendR - 1 - kPendPre];
+#pragma unroll
+        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i)
+            r[i] = kPendPre + i < cnt ? xp[(int64_t)(kPendPre + i) * xst] : 0.0;
+#pragma unroll
+        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i)
+            if (kPendPre + i < cnt) v = __dsub_rn(v, __dmul_rn(r[i], readlane_dbl(upl, kPendPre + i)));
     }
     return v;
 }
@@ -1210,8 +1216,6 @@ __device__ __forceinline__ double pend_apply_l(double v, const double* __restric
 template <int P, bool EXT = false>
 struct P2MfLds {
     using Gm = MfGeom<P, EXT>;
-    double pxa[EXT ? kMaxPendR : 1];  // EXT: X[s][a] and Y[s][b] of the pivot (uniform), s < PE - 1
-    double pyb[EXT ? kMaxPendR : 1];
     double ys[kP2StageCols * Gm::YS];                 // exact y's of the staged columns (examinations)
     _Float16 yb[kP2StageCols * Gm::KSP];              // their B fragments (y splits)
     int cpos[kP2StageCols];
@@ -1325,26 +1329,40 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     const int nch0 = (gc0 + 15) / 16;
     if (rep < nch0) load_chunk(0, gc0, rep, va);
     if (rep + kMfReps < nch0) load_chunk(0, gc0, rep + kMfReps, vb);
+    // EXT: the pivot-independent side of this thread's chain (row thread: X[s][row]; stager:
+    // Y[s][column]), all PE - 1 of them requested before the pivot is read
+    [[maybe_unused]] PendPre pre;
+    if constexpr (EXT) {
+        if (!stager)
+            pend_pre(pre, g.X + (rrow < m ? rrow : 0), ldx, PE - 1);
+        else
+            pend_pre(pre, g.Y + (jst >= 0 && jst < n ? jst : 0), ldy, PE - 1);
+    }
     if (st->done) return false;
     const int a = (int)st->p, bq = (int)st->q;
     const double piv = st->pval;
-    if constexpr (EXT) {  // the pivot row's pending x's / column's pending y's, once per workgroup
-        if ((int)threadIdx.x < PE - 1) {
-            L.pxa[threadIdx.x] = g.X[(int64_t)threadIdx.x * ldx + a];
-            L.pyb[threadIdx.x] = g.Y[(int64_t)threadIdx.x * ldy + bq];
-        }
-        __syncthreads();
+    // EXT: lane s of every wave holds the pivot's side, X[s][a] (stager waves) or Y[s][bq] (row
+    // waves) -- one load per lane, no barrier. The chains that readlane it run on whole waves (the
+    // stager / row split is by wave): a spilled upl reloaded under a partial exec mask would leave
+    // the inactive lanes' values undefined.
+    [[maybe_unused]] double upl = 0.0;
+    if constexpr (EXT) {
+        if (lane < PE - 1) upl = stager ? g.X[(int64_t)lane * ldx + a] : g.Y[(int64_t)lane * ldy + bq];
     }
     if (!stager) {
         // row thread: x_k of its row (the reference's operation order), the split A fragment row
         // -(x_0 .. x_{P-1}) with the data masking of rows outside the trailing block
         const int rr = rrow < m ? rrow : 0;
         double xs[P];
+        if constexpr (!EXT) {
 #pragma unroll
-        for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
+            for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
+        }
         double xk = g.A[rr + (int64_t)bq * lda];
-        if constexpr (EXT) {  // all PE - 1 exact pending updates, 8 loads in flight at a time
-            xk = pend_apply_l<TCI_EXT_B>(xk, g.X + rr, ldx, L.pyb, PE - 1, true);
+        if constexpr (EXT) {  // all PE - 1 exact pending updates
+            xk = pend_chain(xk, pre, g.X + rr, ldx, upl, PE - 1);
+#pragma unroll
+            for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
         } else {
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
@@ -1376,6 +1394,15 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
 #pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = sl[8 * z + e];
             *reinterpret_cast<h8v*>(&L.u.xa[prow * KSP + 8 * z]) = w;
+        }
+    }
+    // EXT: the first staged group's y_k chain here (whole stager waves; columns that are not
+    // trailing compute a value nobody reads), so that pre is dead before the streaming loop
+    [[maybe_unused]] double yk0 = 0.0;
+    if constexpr (EXT) {
+        if (stager) {
+            const int jj = jst >= 0 && jst < n ? jst : 0;
+            yk0 = pend_chain(g.A[a + (int64_t)jj * lda], pre, g.Y + jj, ldy, upl, PE - 1);
         }
     }
     PPROF(1);
@@ -1524,6 +1551,15 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             }
             __syncthreads();
         }
+        [[maybe_unused]] double ykg = yk0;  // EXT: this group's y_k chain (whole stager waves)
+        if constexpr (EXT) {
+            if (g0 > 0 && stager) {
+                const int jj = jst >= 0 && jst < n ? jst : 0;
+                PendPre pg;
+                pend_pre(pg, g.Y + jj, ldy, PE - 1);
+                ykg = pend_chain(g.A[a + (int64_t)jj * lda], pg, g.Y + jj, ldy, upl, PE - 1);
+            }
+        }
         if (jst >= 0) {
             int lc = threadIdx.x;
             asm volatile("" : "+v"(lc));
@@ -1532,10 +1568,11 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                 double ysv[P];
 #pragma unroll
                 for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)(off + s) * ldy + jst];
-                double yk = g.A[a + (int64_t)jst * lda];
+                double yk;
                 if constexpr (EXT) {
-                    yk = pend_apply_l<TCI_EXT_B>(yk, g.Y + jst, ldy, L.pxa, PE - 1, false);
+                    yk = ykg;
                 } else {
+                    yk = g.A[a + (int64_t)jst * lda];
 #pragma unroll
                     for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
                 }
@@ -1910,6 +1947,11 @@ struct ShCert {
 };
 __device__ __forceinline__ ShCert sh_cert(const double* pv, int k, int PS, int PE, int nbs) {
     const int te = k - PE + 1, t0 = k - PS + 1;
+    // the pivot values pv[te - 1 .. k] (PE + 1 <= 33 of them), one load per lane, read back with
+    // readlane: a loop of dependent scalar loads cost ~5 us at PE ~ 26 (phase profile, round 3)
+    const int lane = threadIdx.x & 63, ix = te - 1 + lane;
+    const double w = (lane <= PE && ix >= 0) ? pv[ix] : 0.0;
+    auto at = [&](int t) { return readlane_dbl(w, t - te + 1); };
     double d = 0.0;
     ShCert c{0.0, 0.0, false};
     for (int e = te;; e += nbs) {
@@ -1918,16 +1960,16 @@ __device__ __forceinline__ ShCert sh_cert(const double* pv, int k, int PS, int P
         const int P = ke - e + 1;
         double sumM = 0.0, maxM = 0.0;
         for (int t = e; t <= ke; ++t) {
-            sumM += fabs(pv[t]);
-            maxM = fmax(maxM, fabs(pv[t]));
+            sumM += fabs(at(t));
+            maxM = fmax(maxM, fabs(at(t)));
         }
-        const double s = sh_scale(sh_bound(pv, e));
-        const double Mfd = fabs(pv[e]) + d;
+        const double s = sh_scale(e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1)));  // sh_bound(pv, e)
+        const double Mfd = fabs(at(e)) + d;
         const double mag = Mfd + 2.0 * sumM;
         const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 / s + 0x1p-19 * sumM +
                                         (double)P * 0x1p-24 / s + (double)(3 * P + 4) * 0x1p-23 * mag
                                   : 0.0;
-        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(pv[ke]) * s, -TCI_SH_TIGHT);
+        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -TCI_SH_TIGHT);
         if (cur) {
             c.eps = ea * s;
             c.shs = s;
@@ -2139,81 +2181,6 @@ void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* r
 #define TCI_SMALL_THREADS 1024
 #endif
 constexpr int kSmallThreads = TCI_SMALL_THREADS;
-#ifdef TCI_SMALL_PROF
-#define SPROF(i) (prof_t[i] = wall_clock64())
-#else
-#define SPROF(i) ((void)prof_t)
-#endif
-// Argmax reductions on DPP lane moves (VALU, no LDS round trip as ds_bpermute has): a candidate
-// is (abs2 value, key), larger value first, then the smaller key; NaN never wins.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-template <int CTRL>
-__device__ __forceinline__ void dpp_take(double& bv, unsigned& bk, double& bx) {
-    const double ov = dpp_f64<CTRL>(bv), ox = dpp_f64<CTRL>(bx);
-    const unsigned ok = (unsigned)__builtin_amdgcn_update_dpp(0, (int)bk, CTRL, 0xf, 0xf, false);
-    const bool better = (ov > bv) || (ov == bv && ok < bk);
-    bv = better ? ov : bv;
-    bk = better ? ok : bk;
-    bx = better ? ox : bx;
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-// winner of each row of 16 lanes, in every lane of that row (quad_perm [1,0,3,2], [2,3,0,1],
-// row_half_mirror, row_mirror)
-__device__ __forceinline__ void row16_argmax_dpp(double& bv, unsigned& bk, double& bx) {
-    dpp_take<0xb1>(bv, bk, bx);
-    dpp_take<0x4e>(bv, bk, bx);
-    dpp_take<0x141>(bv, bk, bx);
-    dpp_take<0x140>(bv, bk, bx);
-}
-
-// winner of lanes 0..15, uniform in every lane
-__device__ __forceinline__ void row_argmax_dpp(double& bv, unsigned& bk, double& bx) {
-    row16_argmax_dpp(bv, bk, bx);
-    bv = readlane_f64(bv, 0);
-    bk = (unsigned)__builtin_amdgcn_readlane((int)bk, 0);
-    bx = readlane_f64(bx, 0);
-}
-
-// winner of the whole wave, uniform in every lane
-__device__ __forceinline__ void wave_argmax_dpp(double& bv, unsigned& bk) {
-    double bx = 0.0;
-    row16_argmax_dpp(bv, bk, bx);
-    double v = readlane_f64(bv, 0);
-    unsigned key = (unsigned)__builtin_amdgcn_readlane((int)bk, 0);
-#pragma unroll
-    for (int r = 16; r < 64; r += 16) {
-        const double ov = readlane_f64(bv, r);
-        const unsigned ok = (unsigned)__builtin_amdgcn_readlane((int)bk, r);
-        const bool better = (ov > v) || (ov == v && ok < key);
-        v = better ? ov : v;
-        key = better ? ok : key;
-    }
-    bv = v;
-    bk = key;
-}
-
-struct SmallCand {
-    double v;
-    unsigned key;
-    unsigned pad;
-    double val;
-};
-constexpr int64_t kSmallElems = 16384;  // 128 KiB of fp64 in LDS
-constexpr int64_t kSmallPerm = 2048;    // m + n
 
 bool rrlu_small_fits(int64_t m, int64_t n) {
     return m > 0 && n > 0 && (m | 1) * n <= kSmallElems && m + n <= kSmallPerm;
@@ -2245,136 +2212,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_rrlu_small(
     constexpr int NW = kSmallThreads / 64;
     for (int j = w; j < n; j += NW)
         for (int i = l; i < m; i += 64) S[i + j * ldS] = A[i + (int64_t)j * lda];
-    for (int i = tid; i < m; i += kSmallThreads) rp[i] = i;
-    for (int j = tid; j < n; j += kSmallThreads) cp[j] = j;
-    // every thread tracks the loop state (identical everywhere); thread 0 publishes it
-    double maxerror = 0.0, error = __longlong_as_double(0x7ff8000000000000LL);
-    int np = 0;
-    __syncthreads();
-    // argmax of abs2 over the trailing block (submatrixargmax, matrixlu.jl:46-87): the candidate
-    // order (value, column, row) is the reference's column-major scan with strict '>'
-    // a candidate is (abs2, key = column << 16 | row): larger abs2 wins, then the smaller key
-    double bv = -1.0;
-    unsigned bk = 0xffffffffu;
-    auto take = [&](double a2, unsigned key) {
-        const bool better = (a2 > bv) || (a2 == bv && key < bk);  // NaN never wins
-        bv = better ? a2 : bv;
-        bk = better ? key : bk;
-    };
-    for (int j = w; j < n; j += NW)
-        for (int i = l; i < m; i += 64) {
-            const double v = S[i + j * ldS];
-            take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
-        }
-    SmallCand* red2 = reinterpret_cast<SmallCand*>(red);
-    long long prof_t[8];
-    for (int k = 0; k < mr; ++k) {
-        SPROF(0);
-        wave_argmax_dpp(bv, bk);  // every lane now holds the wave's winner
-        if (l == 0)  // the wave's winner and its value (no swap can be under way here)
-            red2[w] = SmallCand{bv, bk, 0u, bv >= 0.0 ? S[(bk & 0xffffu) + (bk >> 16) * ldS] : 0.0};
-        __syncthreads();
-        SPROF(1);
-        // the workgroup's winner: lanes 0..NW-1 of every wave take one wave's entry each
-        SmallCand b = l < NW ? red2[l] : SmallCand{-1.0, 0xffffffffu, 0u, 0.0};
-        row_argmax_dpp(b.v, b.key, b.val);
-        int p = (int)(b.key & 0xffffu), q = (int)(b.key >> 16);
-        double val = b.val;
-        if (!(b.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
-            p = q = k;
-            val = S[k + k * ldS];
-        }
-        error = fabs(val);
-        if (((fabs(error) < reltol * maxerror) || (fabs(error) < abstol)) && k > 0) break;
-        maxerror = jl_max(maxerror, error);
-        np = k + 1;
-        if (tid == 0) pivvals[k] = val;
-        SPROF(2);
-        // swaprow!(k, p) then swapcol!(k, q) (matrixlu.jl:254-275)
-        if (p != k) {
-            for (int j = tid; j < n; j += kSmallThreads) {
-                const double t = S[k + j * ldS];
-                S[k + j * ldS] = S[p + j * ldS];
-                S[p + j * ldS] = t;
-            }
-            if (tid == 0) {
-                const int t = rp[k];
-                rp[k] = rp[p];
-                rp[p] = t;
-            }
-            __syncthreads();
-        }
-        if (q != k) {
-            for (int i = tid; i < m; i += kSmallThreads) {
-                const double t = S[i + k * ldS];
-                S[i + k * ldS] = S[i + q * ldS];
-                S[i + q * ldS] = t;
-            }
-            if (tid == 0) {
-                const int t = cp[k];
-                cp[k] = cp[q];
-                cp[q] = t;
-            }
-            __syncthreads();
-        }
-        SPROF(3);
-        // normalisation by the pivot (true division; matrixlu.jl:300-305) into S and xv / yv
-        const double piv = S[k + k * ldS];
-        for (int i = k + 1 + tid; i < m; i += kSmallThreads) {
-            const double x = leftorth ? S[i + k * ldS] / piv : S[i + k * ldS];
-            xv[i] = x;
-            S[i + k * ldS] = x;
-        }
-        for (int j = k + 1 + tid; j < n; j += kSmallThreads) {
-            const double y = leftorth ? S[k + j * ldS] : S[k + j * ldS] / piv;
-            yv[j] = y;
-            S[k + j * ldS] = y;
-        }
-        __syncthreads();
-        SPROF(4);
-        // rank-1 update (mul then sub, matrixlu.jl:314-320) fused with the next pivot's argmax
-        bv = -1.0;
-        bk = 0xffffffffu;
-        if (m <= 64 * 4) {  // this lane's (at most 4) rows: their x's stay in registers
-            double xr[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const int i = l + 64 * a;
-                xr[a] = (i < m && i > k) ? xv[i] : 0.0;
-            }
-            // (the update is fp64-VALU-bound here: ~3 us/pivot at 14k elements on one CU)
-            for (int j = w; j < n; j += NW) {
-                if (j <= k) continue;
-                const double y = yv[j];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    const int i = l + 64 * a;
-                    if (i >= m || i <= k) continue;
-                    const double v = __dsub_rn(S[i + j * ldS], __dmul_rn(xr[a], y));
-                    S[i + j * ldS] = v;
-                    take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
-                }
-            }
-        } else {
-            for (int j = w; j < n; j += NW) {
-                if (j <= k) continue;
-                const double y = yv[j];
-                for (int i = l; i < m; i += 64) {
-                    if (i <= k) continue;
-                    const double v = __dsub_rn(S[i + j * ldS], __dmul_rn(xv[i], y));
-                    S[i + j * ldS] = v;
-                    take(__dmul_rn(v, v), ((unsigned)j << 16) | (unsigned)i);
-                }
-            }
-        }
-        SPROF(5);
-#ifdef TCI_SMALL_PROF
-        if (tid == 0 && k == 5)
-            printf("small k=5 m=%d n=%d: reduce %lld decide %lld swap %lld norm %lld update %lld\n", m, n,
-                   prof_t[1] - prof_t[0], prof_t[2] - prof_t[1], prof_t[3] - prof_t[2], prof_t[4] - prof_t[3],
-                   prof_t[5] - prof_t[4]);
-#endif
-    }
+    double maxerror, error;
+    int np = small_lu_core<kSmallThreads>(S, ldS, m, n, mr, reltol, abstol, leftorth, rp, cp,
+                                          reinterpret_cast<SmallCand*>(red), xv, yv, pivvals, error, maxerror);
     if (tid == 0) {
         st->np = np;
         st->done = 1;

@@ -15,6 +15,14 @@
 #include <vector>
 
 #include "../../include/tci_hip.h"
+#include "tci_internal.h"
+
+// tci_abi.cpp: the device-resident small sweep (tci_sweep_small.hip)
+bool tci_sweep_small_ok(tci_ctx* c, const tci_func* f, int L);
+int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
+                        int mode, int fill, int niter, int iter1, int strategy, int strictlynested, double abstol,
+                        int64_t maxbonddim, std::vector<char>& out);
+int tci_sweep_small_error(tci_ctx* c, int status, int64_t bond);
 
 namespace {
 
@@ -188,24 +196,188 @@ int tci_tci2_set_errors(tci_tci2* s, double maxsample, const double* bonderrors,
     return TCI_OK;
 }
 
-// sweepstrategy: 0 = backandforth, 1 = forward, 2 = backward (sweepstrategies.jl:41-50)
-int tci_tci2_sweep2site(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
-                        int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested) {
-    if (!s || !f || niter < 0) return TCI_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// The SwIO image of the state (tci_internal.h): banks 0..3 = Iset, Jset, the history's.
+int64_t sw_capacity(const tci_tci2* s) {
+    int64_t cap = 128;  // the small path's bonds keep at most min(m, n) <= 128 pivots
+    for (int p = 0; p < s->L; ++p)
+        cap = std::max({cap, s->I[p].count(), s->J[p].count(), s->hI[p].count(), s->hJ[p].count()});
+    return cap;
+}
+
+std::vector<char> sw_pack(const tci_tci2* s) {
     const int L = s->L;
-    for (int it = iter1; it < iter1 + niter; ++it) {
-        const bool extra = !strictlynested && s->has_history;
-        std::vector<ISet> eI, eJ;
-        if (extra) {
-            eI = s->hI;
-            eJ = s->hJ;
+    const tci::SwIO io = tci::sw_io(L);
+    const ISet* banks[4] = {s->I.data(), s->J.data(), s->hI.data(), s->hJ.data()};
+    size_t bytes = io.sets;
+    for (int b = 0; b < 4; ++b)
+        for (int p = 0; p < L; ++p) bytes += banks[b][p].v.size() * 4;
+    std::vector<char> img(bytes, 0);
+    int64_t* hdr = reinterpret_cast<int64_t*>(img.data());
+    hdr[3] = s->has_history ? 1 : 0;
+    double ms = s->maxsample;
+    memcpy(&hdr[6], &ms, 8);
+    int64_t* cn = reinterpret_cast<int64_t*>(img.data() + io.counts);
+    double* be = reinterpret_cast<double*>(img.data() + io.bonderr);
+    for (int i = 0; i < L - 1; ++i) be[i] = s->bonderrors[i];
+    char* dst = img.data() + io.sets;
+    for (int b = 0; b < 4; ++b)
+        for (int p = 0; p < L; ++p) {
+            cn[(size_t)b * L + p] = banks[b][p].count();
+            const size_t nbytes = banks[b][p].v.size() * 4;
+            if (nbytes) memcpy(dst, banks[b][p].v.data(), nbytes);
+            dst += nbytes;
         }
-        s->hI = s->I;
-        s->hJ = s->J;
-        s->has_history = true;
-        s->pivoterrors.clear();  // flushpivoterror!
+    return img;
+}
+
+struct SwOut {
+    int64_t status = 0, it = 0, q = 0, bond = 0, fstatus = -1;
+    bool extra = false;
+    std::vector<ISet> eI, eJ;
+};
+
+// the kernel's results into the state (mode 0: sets, errors, maxsample; mode 1: maxsample)
+SwOut sw_unpack(tci_tci2* s, const std::vector<char>& img, int mode) {
+    const int L = s->L;
+    const tci::SwIO io = tci::sw_io(L);
+    const int64_t* hdr = reinterpret_cast<const int64_t*>(img.data());
+    SwOut o;
+    o.status = hdr[0];
+    o.it = hdr[1];
+    o.q = hdr[2];
+    o.bond = hdr[7];
+    o.fstatus = hdr[8];
+    o.extra = o.status == 1 && hdr[4] != 0;
+    memcpy(&s->maxsample, &hdr[6], 8);
+    if (mode != 0) return o;
+    s->has_history = hdr[3] != 0;
+    const int64_t* cn = reinterpret_cast<const int64_t*>(img.data() + io.counts);
+    const double* be = reinterpret_cast<const double*>(img.data() + io.bonderr);
+    s->bonderrors.assign(be, be + (L - 1));
+    const double* pe = reinterpret_cast<const double*>(img.data() + io.pe);
+    s->pivoterrors.assign(pe, pe + hdr[5]);
+    o.eI.resize(L);
+    o.eJ.resize(L);
+    std::vector<ISet>* banks[6] = {&s->I, &s->J, &s->hI, &s->hJ, &o.eI, &o.eJ};
+    const char* src = img.data() + io.sets;
+    for (int b = 0; b < (o.extra ? 6 : 4); ++b)
+        for (int p = 0; p < L; ++p) {
+            ISet& t = (*banks[b])[p];
+            t.w = (b & 1) ? L - 1 - p : p;
+            const int64_t c = cn[(size_t)b * L + p];
+            if (t.w == 0) {
+                t.v.clear();
+                t.ncount0 = c;
+            } else {
+                t.v.resize((size_t)(c * t.w));
+                memcpy(t.v.data(), src, (size_t)(c * t.w) * 4);
+                src += (size_t)(c * t.w) * 4;
+            }
+        }
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tci_tci2_set_sets(tci_tci2* s, int which, const int64_t* counts, const int32_t* packed) {
+    if (!s || !counts || which < 0 || which > 3) return TCI_ERR_ARG;
+    std::vector<ISet>& bank = which == 0 ? s->I : which == 1 ? s->J : which == 2 ? s->hI : s->hJ;
+    const int32_t* src = packed;
+    for (int p = 0; p < s->L; ++p) {
+        ISet& t = bank[p];
+        if (counts[p] < 0 || (counts[p] > 0 && t.w > 0 && !src)) return TCI_ERR_ARG;
+        if (t.w == 0) {
+            t.v.clear();
+            t.ncount0 = counts[p];
+        } else {
+            t.v.assign(src, src + counts[p] * t.w);
+            src += counts[p] * t.w;
+        }
+    }
+    if (which >= 2) s->has_history = true;
+    return TCI_OK;
+}
+
+int tci_tci2_get_sets(tci_tci2* s, int which, int64_t* counts, int32_t* packed, int64_t capacity) {
+    if (!s || !counts || which < 0 || which > 3) return TCI_ERR_ARG;
+    const std::vector<ISet>& bank = which == 0 ? s->I : which == 1 ? s->J : which == 2 ? s->hI : s->hJ;
+    int64_t need = 0;
+    for (int p = 0; p < s->L; ++p) {
+        counts[p] = bank[p].count();
+        need += (int64_t)bank[p].v.size();
+    }
+    if (!packed) return TCI_OK;
+    if (capacity < need) return TCI_ERR_ARG;
+    int32_t* dst = packed;
+    for (int p = 0; p < s->L; ++p) {
+        if (!bank[p].v.empty()) memcpy(dst, bank[p].v.data(), bank[p].v.size() * 4);
+        dst += bank[p].v.size();
+    }
+    return TCI_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// sweepstrategy: 0 = backandforth, 1 = forward, 2 = backward (sweepstrategies.jl:41-50). fill:
+// also fillsitetensors!'s maxsample update on the device after the iterations (*filled = 1 when
+// it was done there).
+int sweep2site_impl(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
+                    int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested, int fill, int* filled) {
+    if (!s || !f || niter < 0) return TCI_ERR_ARG;
+    if (filled) *filled = 0;
+    const int L = s->L;
+    int it0 = iter1, q0 = 1;
+    bool resume = false;
+    SwOut so;
+    if (niter > 0 && tci_sweep_small_ok(s->ctx, f, L)) {
+        // whole iterations in one launch while every bond fits the one-workgroup rrLU
+        const std::vector<char> in = sw_pack(s);
+        std::vector<char> out;
+        int st = tci_sweep_small_run(s->ctx, f, L, sw_capacity(s), in.data(), in.size(), 0, fill ? 1 : 0, niter,
+                                     iter1, sweepstrategy, strictlynested, abstol, maxbonddim, out);
+        if (st) return st;
+        so = sw_unpack(s, out, 0);
+        if (so.status == 0) {
+            // a fill that stopped (non-square pivot matrix, a site too large) is redone by the
+            // caller's loop: the sites it covered only repeat their maxima
+            if (filled) *filled = fill && so.fstatus == 0;
+            return TCI_OK;
+        }
+        if (so.status != 1) return tci_sweep_small_error(s->ctx, (int)so.status, so.bond);
+        it0 = (int)so.it;  // a bond outgrew it: this loop continues from there
+        q0 = (int)so.q;
+        resume = true;
+    }
+    for (int it = it0; it < iter1 + niter; ++it) {
+        std::vector<ISet> eI, eJ;
+        bool extra;
+        int qs = 1;
+        if (resume && it == it0) {  // the kernel already began this iteration
+            extra = so.extra;
+            eI.swap(so.eI);
+            eJ.swap(so.eJ);
+            qs = q0;
+        } else {
+            extra = !strictlynested && s->has_history;
+            if (extra) {
+                eI = s->hI;
+                eJ = s->hJ;
+            }
+            s->hI = s->I;
+            s->hJ = s->J;
+            s->has_history = true;
+            s->pivoterrors.clear();  // flushpivoterror!
+        }
         const bool fwd = sweepstrategy == 1 || (sweepstrategy == 0 && it % 2 == 1);
-        for (int q = 1; q < L; ++q) {
+        for (int q = qs; q < L; ++q) {
             const int b = fwd ? q : L - q;  // 1-based bond
             const ISet Ik = kron_right(s->I[b - 1], s->localdims[b - 1]);
             const ISet Jk = kron_left(s->localdims[b], s->J[b]);
@@ -236,6 +408,41 @@ int tci_tci2_sweep2site(tci_tci2* s, const tci_func* f, int32_t niter, int32_t i
             s->pivoterrors.swap(upd);
         }
     }
+    return TCI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tci_tci2_sweep2site(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
+                        int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested) {
+    return sweep2site_impl(s, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested, 0, nullptr);
+}
+
+int tci_tci2_sweep2site_fill(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
+                             int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested, int* filled) {
+    if (!filled) return TCI_ERR_ARG;
+    return sweep2site_impl(s, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested, 1, filled);
+}
+
+
+int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) {
+    if (!s || !f || !handled) return TCI_ERR_ARG;
+    *handled = 0;
+    if (!tci_sweep_small_ok(s->ctx, f, s->L)) return TCI_OK;
+    const std::vector<char> in = sw_pack(s);
+    std::vector<char> out;
+    const double before = s->maxsample;
+    int st = tci_sweep_small_run(s->ctx, f, s->L, sw_capacity(s), in.data(), in.size(), 1, 0, 0, 1, 0, 0, 0.0,
+                                 0, out);
+    if (st) return st;
+    const SwOut so = sw_unpack(s, out, 1);
+    if (so.fstatus != 0) {  // the caller's loop reports it / evaluates the large site
+        s->maxsample = before;
+        return TCI_OK;
+    }
+    *handled = 1;
     return TCI_OK;
 }
 

@@ -1,0 +1,770 @@
+// tci_sweep_small.hip -- sweep2site! (tensorci2.jl:1195-1258) resident on the device while every
+// bond's Pi fits one workgroup's LDS (the small rrLU of tci_smalllu.h: (m|1) n <= 16384 and
+// m + n <= 2048), for the staged integrand kinds. One launch runs niter iterations: per bond the
+// kronecker products of the index sets (tensorci2.jl:512-529), Julia's first-seen `union` with
+// the previous sweep's sets (:1214-1216), Pi = f(Icomb x Jcomb) evaluated straight into LDS with
+// the batched assembly's own arithmetic (tci_funcdev.h), updatemaxsample! (:636-638), the rrLU
+// (matrixlu.jl:346-396), the new pivot sets and updateerrors! (:281-289) -- no host round trip
+// between bonds (the small configs were bound by ~50 us of host sync per
+// bond). A bond that does not fit ends the launch with a resume point; the host loop
+// (tci_sweep.cpp) continues from there with the same state. Mode 1 is fillsitetensors!'s
+// maxsample update (globalsearch.jl:202-208 with the solve unobservable: max |Pi1| of every site).
+//
+// State in HBM: six banks of index sets (0 Iset, 1 Jset, then the history and the extra pair,
+// whose roles swap per iteration), site p of bank b at ws + off[b L + p], cap entries each;
+// per-bond scratch (the concatenated kronecker + extra entries, the combined sets) beside it.
+// Host I/O through mapped host memory (SwIO layout, tci_internal.h): read once at the start,
+// written once at the end.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "tci_funcdev.h"
+#include "tci_internal.h"
+#include "tci_smalllu.h"
+
+namespace tci {
+
+constexpr int kSwThreads = 256;  // 4 waves, one per SIMD: the small rrLU's per-pivot barriers are cheap
+constexpr int kSwWaves = kSwThreads / 64;
+
+// dynamic LDS: S (also the union's scratch) | perms (rows, then columns) | x / y (row / column
+// states while Pi is evaluated) | per-wave candidates
+constexpr size_t kSwLdsS = (size_t)kSmallElems * 8;
+constexpr size_t kSwLdsPerm = (size_t)kSmallPerm * 4;
+constexpr size_t kSwLdsXY = (size_t)kSmallPerm * 8;
+constexpr size_t kSwLds = kSwLdsS + kSwLdsPerm + kSwLdsXY + kSwWaves * sizeof(SmallCand);
+static_assert((size_t)kSwCatCap * 5 <= kSwLdsS, "union scratch (hash + flag per entry) inside S");
+
+__host__ __device__ constexpr size_t sw_al16(size_t b) { return (b + 15) / 16 * 16; }
+
+// dst[0 .. n) = src[0 .. n) by the whole workgroup with kSwCopyB loads in flight per thread (an
+// HBM / L2 round trip per kSwCopyB x 256 ints, not one per int)
+constexpr int kSwCopyB = 8;
+__device__ __forceinline__ void sw_copy(int32_t* dst, const int32_t* src, int n) {
+    for (int base = 0; base < n; base += kSwCopyB * kSwThreads) {
+        int32_t v[kSwCopyB];
+#pragma unroll
+        for (int u = 0; u < kSwCopyB; ++u) {
+            const int e = base + (int)threadIdx.x + u * kSwThreads;
+            v[u] = e < n ? src[e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kSwCopyB; ++u) {
+            const int e = base + (int)threadIdx.x + u * kSwThreads;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
+
+#ifdef TCI_SW_PROF  // phase profile (thread 0, wall clock ticks): kron+union, Pi, rrLU, selection
+#define SWP(i) (swp_t[i] = wall_clock64())
+#else
+#define SWP(i) ((void)0)
+#endif
+
+__device__ __forceinline__ uint32_t sw_hash(const int32_t* e, int w) {
+    uint32_t h = 2166136261u;
+    for (int t = 0; t < w; ++t) h = (h ^ (uint32_t)e[t]) * 16777619u;
+    return h;
+}
+
+// exclusive prefix sum of v over the workgroup in thread order; *total gets the sum
+__device__ __forceinline__ int sw_scan(int v, int* scr, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) scr[w] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < kSwWaves; ++q) {
+        const int s = scr[q];
+        base += q < w ? s : 0;
+        tot += s;
+    }
+    __syncthreads();  // scr reusable
+    *total = tot;
+    return base + x - v;
+}
+
+// union of the n entries cat[0 .. n) (width w, n <= kSwCatCap): the first occurrence of every
+// distinct entry, in order, into dst; returns the count (Julia's union over Vector{MultiIndex},
+// the order of tci_sweep.cpp's union_sets)
+__device__ int sw_union(const int32_t* __restrict__ cat, int n, int w, int32_t* __restrict__ dst,
+                        char* scratch, int* scr) {
+    const int tid = threadIdx.x;
+    uint32_t* hs = reinterpret_cast<uint32_t*>(scratch);
+    unsigned char* keep = reinterpret_cast<unsigned char*>(scratch) + (size_t)n * 4;
+    for (int t = tid; t < n; t += kSwThreads) hs[t] = sw_hash(cat + (int64_t)t * w, w);
+    __syncthreads();
+    for (int t = tid; t < n; t += kSwThreads) {
+        const uint32_t h = hs[t];
+        const int32_t* et = cat + (int64_t)t * w;
+        bool dup = false;
+        for (int s = 0; s < t && !dup; ++s) {
+            if (hs[s] != h) continue;
+            const int32_t* es = cat + (int64_t)s * w;
+            bool eq = true;
+            for (int z = 0; z < w && eq; ++z) eq = es[z] == et[z];
+            dup = eq;
+        }
+        keep[t] = dup ? 0 : 1;
+    }
+    __syncthreads();
+    // stable compaction: thread tid owns the contiguous chunk [t0, t1)
+    const int per = (n + kSwThreads - 1) / kSwThreads;
+    const int t0 = min(n, tid * per), t1 = min(n, t0 + per);
+    int nk = 0;
+    for (int t = t0; t < t1; ++t) nk += keep[t];
+    int total;
+    int pos = sw_scan(nk, scr, &total);
+    for (int t = t0; t < t1; ++t)
+        if (keep[t]) {
+            for (int z = 0; z < w; ++z) dst[(int64_t)pos * w + z] = cat[(int64_t)t * w + z];
+            ++pos;
+        }
+    __syncthreads();
+    return total;
+}
+
+// Julia's max over |v| (NaN-propagating) across the workgroup, as the unsigned maximum of the bit
+// patterns of |v| (the batched assembly's block_maxabs order): the same in every thread
+__device__ __forceinline__ double sw_maxabs(double mx, unsigned long long* slot) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(fabs(mx));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(b, off);
+        b = o > b ? o : b;
+    }
+    if (threadIdx.x == 0) *slot = 0ull;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax(slot, b);
+    __syncthreads();
+    const double r = __longlong_as_double((long long)*slot);
+    __syncthreads();
+    return r;
+}
+
+
+// ---- one-wave union (every bond of the small configs: a few dozen entries): the hashes stay in
+// registers and are broadcast with readlane, so the duplicate test is a register compare per
+// earlier entry, not a chain of dependent LDS loads; the compaction is a ballot prefix
+constexpr int kSwWaveU = 512;  // entries a one-wave union takes
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one whole wave: the union of cat[0 .. n) (LDS, width w, n <= kSwWaveU) into dst (LDS), first
+// occurrences in order; returns the count (the same in every lane)
+__device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
+    constexpr int U = kSwWaveU / 64;
+    const int lane = threadIdx.x & 63;
+    const int nu = (n + 63) >> 6;
+    uint32_t h[U];
+    bool keep[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = lane + 64 * u;
+        keep[u] = t < n;
+        h[u] = keep[u] ? sw_hash(cat + t * w, w) : 0u;
+    }
+#pragma unroll
+    for (int su = 0; su < U; ++su) {
+        if (su >= nu) break;
+        for (int sl = 0; sl < 64; ++sl) {
+            const int s = su * 64 + sl;
+            if (s >= n) break;
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)h[su], sl);
+#pragma unroll
+            for (int u = su; u < U; ++u) {
+                const int t = lane + 64 * u;
+                if (u < nu && keep[u] && t > s && h[u] == hs) {
+                    bool eq = true;
+                    for (int z = 0; z < w && eq; ++z) eq = cat[s * w + z] == cat[t * w + z];
+                    if (eq) keep[u] = false;
+                }
+            }
+        }
+    }
+    int base = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t bal = __ballot(keep[u]);
+        if (keep[u]) {
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+            const int t = lane + 64 * u;
+            for (int z = 0; z < w; ++z) dst[pos * w + z] = cat[t * w + z];
+        }
+        base += __popcll(bal);
+    }
+    return base;
+}
+
+// ---- register-tile rrLU for m, n <= 64: tci_smalllu.h's algorithm with the matrix in registers
+// (thread (tr, tc) of a 16 x 16 grid owns rows tr + 16 a, columns tc + 16 b) and position maps in
+// place of the physical swaps -- the same candidates in the same (value, column position, row
+// position) order, the same multiply / subtract / divide on the same values, so the same pivots
+// and bits. Two barriers per pivot (winner; pivot row / column), no LDS traffic per element.
+constexpr int kSwRegN = 64;
+#ifdef TCI_SW_PROF
+__device__ unsigned long long g_swlu[12];
+#define LUP(i)                                                       \
+    do {                                                             \
+        if (threadIdx.x == 0) {                                      \
+            const unsigned long long t_ = wall_clock64();            \
+            g_swlu[i] += t_ - lup_t;                                 \
+            lup_t = t_;                                              \
+        }                                                            \
+    } while (0)
+#else
+#define LUP(i) ((void)0)
+#endif
+
+__device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
+                          int leftorth, int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red,
+                          double* pvl, int* nslot, double* dslot, double& error, double& maxerror, int& nanfl) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tr = tid & 15, tc = tid >> 4;
+#ifdef TCI_SW_PROF
+    unsigned long long lup_t = wall_clock64();
+#endif
+    double v[4][4];
+    int rpos[4], cpos[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) rpos[a] = tr + 16 * a < m ? tr + 16 * a : -1;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) cpos[b] = tc + 16 * b < n ? tc + 16 * b : -1;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            v[a][b] = (rpos[a] >= 0 && cpos[b] >= 0) ? S[tr + 16 * a + (tc + 16 * b) * ldS] : 0.0;
+    for (int i = tid; i < m; i += kSwThreads) rowphys[i] = i;
+    for (int j = tid; j < n; j += kSwThreads) colphys[j] = j;
+    if (tid == 0) *nslot = 0;
+    double bv = -1.0, bx = 0.0;
+    unsigned bk = 0xffffffffu;
+    auto take = [&](double a2, unsigned key, double val) {
+        const bool better = (a2 > bv) || (a2 == bv && key < bk);  // NaN never wins
+        bv = better ? a2 : bv;
+        bk = better ? key : bk;
+        bx = better ? val : bx;
+    };
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (rpos[a] >= 0 && cpos[b] >= 0)
+                take(__dmul_rn(v[a][b], v[a][b]), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], v[a][b]);
+    maxerror = 0.0;
+    error = __longlong_as_double(0x7ff8000000000000LL);
+    int np = 0;
+    LUP(0);
+    for (int k = 0; k < mr; ++k) {
+        wave_argmax3(bv, bk, bx);
+        LUP(1);
+        if (lane == 0) red[w] = SmallCand{bv, bk, 0u, bx};
+        __syncthreads();
+        LUP(2);
+        SmallCand c = lane < kSwWaves ? red[lane] : SmallCand{-1.0, 0xffffffffu, 0u, 0.0};
+        row_argmax_dpp(c.v, c.key, c.val);
+        LUP(3);
+        int pp = (int)(c.key & 0xffffu), qq = (int)(c.key >> 16);
+        double val = c.val;
+        if (!(c.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
+            pp = qq = k;
+            const int r0 = rowphys[k], c0 = colphys[k];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (tr + 16 * a == r0 && tc + 16 * b == c0) *dslot = v[a][b];
+            __syncthreads();
+            val = *dslot;
+        }
+        error = fabs(val);
+        if (((fabs(error) < reltol * maxerror) || (fabs(error) < abstol)) && k > 0) break;
+        maxerror = jl_max(maxerror, error);
+        np = k + 1;
+        if (tid == 0) pvl[k] = val;
+        const int pr = rowphys[pp], pc = colphys[qq];
+        LUP(4);
+        // swaprow!(k, pp) / swapcol!(k, qq) as position swaps
+#pragma unroll
+        for (int a = 0; a < 4; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
+        // normalisation (true division) of the pivot column / row below / right of the pivot
+        const double piv = val;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                if (tc + 16 * b == pc && rpos[a] > k) {
+                    const double x = leftorth ? v[a][b] / piv : v[a][b];
+                    v[a][b] = x;
+                    xv[tr + 16 * a] = x;
+                }
+                if (tr + 16 * a == pr && cpos[b] > k) {
+                    const double y = leftorth ? v[a][b] : v[a][b] / piv;
+                    v[a][b] = y;
+                    yv[tc + 16 * b] = y;
+                }
+            }
+        LUP(5);
+        __syncthreads();
+        LUP(6);
+        if (tid == 0) {
+            int t = rowphys[k];
+            rowphys[k] = rowphys[pp];
+            rowphys[pp] = t;
+            t = colphys[k];
+            colphys[k] = colphys[qq];
+            colphys[qq] = t;
+        }
+        // rank-1 update of the trailing block (mul then sub), fused with the next argmax
+        bv = -1.0;
+        bk = 0xffffffffu;
+        bx = 0.0;
+        double xr[4], yc[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) xr[a] = rpos[a] > k ? xv[tr + 16 * a] : 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) yc[b] = cpos[b] > k ? yv[tc + 16 * b] : 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (rpos[a] > k && cpos[b] > k) {
+                    const double nv = __dsub_rn(v[a][b], __dmul_rn(xr[a], yc[b]));
+                    v[a][b] = nv;
+                    take(__dmul_rn(nv, nv), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], nv);
+                }
+        LUP(7);
+    }
+    LUP(8);
+    // tril(A[:, 1:np]) / triu(A[1:np, :]) NaN checks (matrixlu.jl:376-381), position coordinates
+    int fl = 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (rpos[a] >= 0 && cpos[b] >= 0 && isnan(v[a][b])) {
+                if (cpos[b] < np && rpos[a] >= cpos[b]) fl |= 1;
+                if (rpos[a] < np && cpos[b] >= rpos[a]) fl |= 2;
+            }
+    if (fl) atomicOr(nslot, fl);
+    __syncthreads();  // also publishes thread 0's last position swap
+    nanfl = *nslot;
+    LUP(9);
+    return np;
+}
+
+// ---- the kernel
+// Index-set slots: every site has three slots per kind (I / J), physical banks 2 s (I) and 2 s + 1
+// (J) of slot s; per site the roles current / history / extra point at slots. An iteration's
+// history is its starting sets (tensorci2.jl:1211-1212): history := current (no copy, the slot is
+// shared until the site is written), extra := the old history; a bond writes its new set into the
+// slot that is neither the history nor the extra (copy-on-write). The host's image arrives as
+// current = slot 0, history = slot 1.
+__device__ __forceinline__ int sw_other(int h, int e) { return h != e ? 3 - h - e : (h + 1) % 3; }
+
+template <int KIND>
+__global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* S = reinterpret_cast<double*>(smem);
+    int* perm = reinterpret_cast<int*>(smem + kSwLdsS);
+    double* xy = reinterpret_cast<double*>(smem + kSwLdsS + kSwLdsPerm);
+    SmallCand* red = reinterpret_cast<SmallCand*>(smem + kSwLdsS + kSwLdsPerm + kSwLdsXY);
+    __shared__ int cnt[6 * kSwMaxL];                    // set counts per physical bank and site
+    __shared__ unsigned char rol[2][3][kSwMaxL];        // [I / J][current / history / extra][site] -> slot
+    __shared__ int ldm[kSwMaxL];                        // localdims
+    __shared__ double bonderr[kSwMaxL];
+    __shared__ double pe[kSwPE];                        // pivoterrors of the current iteration
+    __shared__ double pvl[kSwPE];                       // the bond's pivot values
+    __shared__ int scr[kSwWaves + 4];
+    __shared__ unsigned long long mxs;
+    __shared__ int nanflag;
+    __shared__ int mn[2];
+    __shared__ double dslot;
+    __shared__ int64_t hdr[16];
+
+    const int tid = threadIdx.x;
+    const int L = a.L;
+    const FuncDev& f = a.f;
+    const double* p = f.params;
+    const double p0 = (KIND == F_SUM || KIND == F_TABLE) ? 0.0 : p[0];
+    const SwIO io = sw_io(L);
+#ifdef TCI_SW_PROF
+    unsigned long long swp_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, swp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int swp_n = 0, swp_piv = 0;
+    const unsigned long long swp_c0 = clock64(), swp_w0 = wall_clock64();
+#endif
+    const int64_t half = (int64_t)L * (L - 1) / 2;
+    auto width = [&](int bank, int site) { return (bank & 1) ? L - 1 - site : site; };
+    // bank b, site p at ws + cap (b half + sum of the widths before p) (the host's layout)
+    auto bank_ptr = [&](int bank, int site) -> int32_t* {
+        const int64_t pre = (bank & 1) ? (int64_t)site * (L - 1) - (int64_t)site * (site - 1) / 2
+                                       : (int64_t)site * (site - 1) / 2;
+        return a.ws + a.cap * (bank * half + pre);
+    };
+    // logical role r (0 current, 1 history, 2 extra) of kind k (0 I, 1 J) at a site
+    auto bank_of = [&](int k, int r, int site) { return 2 * (int)rol[k][r][site] + k; };
+    auto set_ptr = [&](int k, int r, int site) { return bank_ptr(bank_of(k, r, site), site); };
+    auto set_cnt = [&](int k, int r, int site) -> int& { return cnt[bank_of(k, r, site) * kSwMaxL + site]; };
+
+    // ---- input (DMA'd to a.inbuf by the host): header, counts, bond errors, the four banks
+    if (tid < 16) hdr[tid] = reinterpret_cast<const int64_t*>(a.inbuf)[tid];
+    for (int i = tid; i < 6 * L; i += kSwThreads)
+        cnt[(i / L) * kSwMaxL + i % L] = i < 4 * L ? (int)reinterpret_cast<const int64_t*>(a.inbuf + io.counts)[i] : 0;
+    for (int i = tid; i < L - 1; i += kSwThreads) bonderr[i] = reinterpret_cast<const double*>(a.inbuf + io.bonderr)[i];
+    for (int i = tid; i < L; i += kSwThreads) {
+        ldm[i] = f.localdims[i];
+        for (int k = 0; k < 2; ++k)
+            for (int r = 0; r < 3; ++r) rol[k][r][i] = (unsigned char)r;
+    }
+    __syncthreads();
+    {
+        const int32_t* src = reinterpret_cast<const int32_t*>(a.inbuf + io.sets);
+        for (int bank = 0; bank < 4; ++bank)
+            for (int s = 0; s < L; ++s) {
+                const int ne = cnt[bank * kSwMaxL + s] * width(bank, s);
+                sw_copy(bank_ptr(bank, s), src, ne);
+                src += ne;
+            }
+    }
+    int has_history = (int)hdr[3];
+    double maxsample = __longlong_as_double((long long)hdr[6]);
+    int npe = 0;
+    int status = 0, s_it = 0, s_q = 0, esite = 0, extra_valid = 0, fstatus = -1, fsite = 0;
+    __syncthreads();
+
+    if (a.mode == 0) {
+        for (int it = a.iter1; it < a.iter1 + a.niter && status == 0; ++it) {
+            const bool extra = !a.strictlynested && has_history;
+            for (int i = tid; i < L; i += kSwThreads)
+                for (int k = 0; k < 2; ++k) {
+                    if (extra) rol[k][2][i] = rol[k][1][i];  // extra := the previous history
+                    rol[k][1][i] = rol[k][0][i];             // history := the current sets
+                }
+            has_history = 1;
+            extra_valid = extra;
+            npe = 0;  // flushpivoterror!
+            __syncthreads();
+            const bool fwd = a.strategy == 1 || (a.strategy == 0 && it % 2 == 1);
+            for (int q = 1; q < L; ++q) {
+                const int b = fwd ? q : L - q;  // 1-based bond
+                SWP(0);
+                // Icomb = union(kronecker(Iset[b-1], d), extra Iset[b]) (width b);
+                // Jcomb = union(kronecker(d, Jset[b]), extra Jset[b-1]) (width L - b)
+                const int dI = ldm[b - 1], nI = set_cnt(0, 0, b - 1), wI0 = b - 1;
+                const int neI = extra ? set_cnt(0, 2, b) : 0;
+                const int dJ = ldm[b], nJ = set_cnt(1, 0, b), wJ0 = L - 1 - b, wJ1 = wJ0 + 1;
+                const int neJ = extra ? set_cnt(1, 2, b - 1) : 0;
+                const int catI = nI * dI + neI, catJ = nJ * dJ + neJ;
+                const int gI = nI * wI0, gJ = nJ * wJ0, gEI = neI * b, gEJ = neJ * wJ1;  // staged ints
+                // LDS: [staged sources | concatenation I | concatenation J | hash / flags] at the
+                // bottom of S, Icomb / Jcomb at its top (below them, later, Pi)
+                const size_t bI = sw_al16((size_t)catI * b * 4), bJ = sw_al16((size_t)catJ * wJ1 * 4);
+                const size_t bG = sw_al16((size_t)(gI + gJ + gEI + gEJ) * 4);
+                const size_t bH = sw_al16((size_t)max(catI, catJ) * 5);
+                const bool room = catI <= kSwCatCap && catJ <= kSwCatCap && nI * dI <= kSmallPerm &&
+                                  nJ * dJ <= kSmallPerm && bG + 2 * (bI + bJ) + bH <= kSwLdsS;
+                char* const R = reinterpret_cast<char*>(S);
+                int32_t* const gs = reinterpret_cast<int32_t*>(R);
+                int32_t* const catIp = reinterpret_cast<int32_t*>(R + bG);
+                int32_t* const catJp = reinterpret_cast<int32_t*>(R + bG + bI);
+                char* const uscr = R + bG + bI + bJ;
+                int32_t* Ic = reinterpret_cast<int32_t*>(R + kSwLdsS - bI - bJ);
+                int32_t* Jc = reinterpret_cast<int32_t*>(R + kSwLdsS - bJ);
+                int m = 0, n = 0;
+                if (room) {
+                    // the four source sets into LDS in one batched round of loads
+                    {
+                        const int32_t* s0 = set_ptr(0, 0, b - 1);
+                        const int32_t* s1 = set_ptr(1, 0, b);
+                        const int32_t* s2 = set_ptr(0, 2, b);
+                        const int32_t* s3 = set_ptr(1, 2, b - 1);
+                        const int n01 = gI + gJ, n012 = n01 + gEI, tot = n012 + gEJ;
+                        for (int base = 0; base < tot; base += kSwCopyB * kSwThreads) {
+                            int32_t v[kSwCopyB];
+#pragma unroll
+                            for (int u = 0; u < kSwCopyB; ++u) {
+                                const int e = base + tid + u * kSwThreads;
+                                v[u] = e < gI ? s0[e] : e < n01 ? s1[e - gI] : e < n012 ? s2[e - n01] : e < tot ? s3[e - n012] : 0;
+                            }
+#pragma unroll
+                            for (int u = 0; u < kSwCopyB; ++u) {
+                                const int e = base + tid + u * kSwThreads;
+                                if (e < tot) gs[e] = v[u];
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    SWP(5);
+                    const int32_t* Ib = gs;
+                    const int32_t* Jb = gs + gI;
+                    const int32_t* Ex = gs + gI + gJ;
+                    const int32_t* Ey = gs + gI + gJ + gEI;
+                    const bool wunion = catI <= kSwWaveU && catJ <= kSwWaveU;
+                    auto build_I = [&](int t0, int stride) {
+                        for (int e = t0; e < nI * dI; e += stride) {
+                            const int i = e % nI, j = e / nI;
+                            int32_t* o = catIp + e * b;
+                            for (int t = 0; t < wI0; ++t) o[t] = Ib[i * wI0 + t];
+                            o[wI0] = j + 1;
+                        }
+                        for (int e = t0; e < gEI; e += stride) catIp[nI * dI * b + e] = Ex[e];
+                    };
+                    auto build_J = [&](int t0, int stride) {
+                        for (int e = t0; e < nJ * dJ; e += stride) {
+                            const int i = e % dJ, jj = e / dJ;
+                            int32_t* o = catJp + e * wJ1;
+                            o[0] = i + 1;
+                            for (int t = 0; t < wJ0; ++t) o[1 + t] = Jb[jj * wJ0 + t];
+                        }
+                        for (int e = t0; e < gEJ; e += stride) catJp[nJ * dJ * wJ1 + e] = Ey[e];
+                    };
+                    if (wunion) {  // waves 0 and 1 at once
+                        const int wv = tid >> 6, ln = tid & 63;
+                        if (wv == 0) {
+                            build_I(ln, 64);
+                            wave_sync();
+                            const int c = sw_union_wave(catIp, catI, b, Ic);
+                            if (ln == 0) mn[0] = c;
+                        } else if (wv == 1) {
+                            build_J(ln, 64);
+                            wave_sync();
+                            const int c = sw_union_wave(catJp, catJ, wJ1, Jc);
+                            if (ln == 0) mn[1] = c;
+                        }
+                        __syncthreads();
+                        m = mn[0];
+                        n = mn[1];
+                    } else {
+                        build_I(tid, kSwThreads);
+                        build_J(tid, kSwThreads);
+                        __syncthreads();
+                        m = sw_union(catIp, catI, b, Ic, uscr, scr);
+                        n = sw_union(catJp, catJ, wJ1, Jc, uscr, scr);
+                    }
+                }
+                const bool fits = m > 0 && n > 0 && (int64_t)(m | 1) * n <= kSmallElems && m + n <= kSmallPerm;  // rrlu_small_fits
+                const int ldS = m | 1;
+                if (!room || !fits || a.maxbonddim <= 0 || (size_t)ldS * n * 8 > kSwLdsS - bI - bJ) {
+                    status = 1;  // resume on the host at (it, q)
+                    s_it = it;
+                    s_q = q;
+                    break;
+                }
+                const int wI = b, wJ = L - b;
+                const int mr = (int)(a.maxbonddim < (int64_t)min(m, n) ? a.maxbonddim : (int64_t)min(m, n));
+                SWP(1);
+                // Pi = f(Icomb x Jcomb) into S (ld m | 1): the row / column states in the x / y space,
+                // then one compact loop over the elements (one inlined copy of f, for the I-cache)
+                St* rs = reinterpret_cast<St*>(xy);
+                St* cs = rs + m;
+                for (int i = tid; i < m; i += kSwThreads) rs[i] = leg_state(f, Ic + i * wI, wI, 0, 0);
+                for (int j = tid; j < n; j += kSwThreads) cs[j] = leg_state(f, Jc + j * wJ, wJ, wI, 0);
+                __syncthreads();
+                SWP(6);
+                double mx = 0.0, error, maxerror;
+#pragma unroll 1
+                for (int e = tid; e < m * n; e += kSwThreads) {
+                    const int i = e % m, j = e / m;
+                    const double v = combine<KIND>(p, p0, rs[i], cs[j], wJ, L, nullptr, 0);
+                    S[i + j * ldS] = v;
+                    const double av = fabs(v);
+                    mx = (isnan(av) || av > mx) ? av : mx;
+                }
+                SWP(7);
+                mx = sw_maxabs(mx, &mxs);
+                SWP(2);
+                int* rp = perm;
+                int* cp = perm + m;
+                int np, fl;
+                if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
+                    np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                                    &nanflag, &dslot, error, maxerror, fl);
+                } else {
+                    np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, red, xy,
+                                                   xy + m, pvl, error, maxerror);
+                    fl = small_lu_nanflags<kSwThreads>(S, ldS, m, n, np, &nanflag);
+                }
+                SWP(3);
+                if (fl) {  // tci_update_pivots_h's NaN errors: the state stays as before this bond
+                    status = (fl & 1) ? 2 : 3;
+                    s_it = it;
+                    s_q = q;
+                    esite = b;
+                    break;
+                }
+                const double err = np >= min(m, n) ? 0.0 : error;  // matrixlu.jl:391-393
+                maxsample = jl_max(fabs(maxsample), fabs(mx));
+                // Iset[b] = Icomb[rowidx], Jset[b-1] = Jcomb[colidx], each into its free slot
+                const int tIs = sw_other(rol[0][1][b], rol[0][2][b]);
+                const int tJs = sw_other(rol[1][1][b - 1], rol[1][2][b - 1]);
+                int32_t* Io = bank_ptr(2 * tIs, b);
+                int32_t* Jo = bank_ptr(2 * tJs + 1, b - 1);
+                for (int e = tid; e < np * wI; e += kSwThreads) Io[e] = Ic[rp[e / wI] * wI + e % wI];
+                for (int e = tid; e < np * wJ; e += kSwThreads) Jo[e] = Jc[cp[e / wJ] * wJ + e % wJ];
+                // updateerrors!(tci, b, pivoterrors(lu)): elementwise max over zero-padded vectors
+                const int ne = max(npe, np + 1);
+                for (int i = tid; i < ne; i += kSwThreads) {
+                    const double nv = i < np ? fabs(pvl[i]) : (i == np ? err : 0.0);
+                    pe[i] = jl_max(i < npe ? pe[i] : 0.0, nv);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    rol[0][0][b] = (unsigned char)tIs;
+                    rol[1][0][b - 1] = (unsigned char)tJs;
+                    cnt[(2 * tIs) * kSwMaxL + b] = np;
+                    cnt[(2 * tJs + 1) * kSwMaxL + b - 1] = np;
+                    bonderr[b - 1] = err;
+                }
+                npe = ne;
+                __syncthreads();
+#ifdef TCI_SW_PROF
+                SWP(4);
+                if (tid == 0) {
+                    swp_acc[0] += swp_t[1] - swp_t[0];
+                    swp_acc[1] += swp_t[2] - swp_t[1];
+                    swp_acc[2] += swp_t[3] - swp_t[2];
+                    swp_acc[3] += swp_t[4] - swp_t[3];
+                    swp_acc[4] += swp_t[5] - swp_t[0];  // staging
+                    swp_acc[5] += swp_t[6] - swp_t[1];  // states
+                    swp_acc[6] += swp_t[7] - swp_t[6];  // Pi loop
+                    swp_acc[7] += swp_t[2] - swp_t[7];  // maxabs
+                    swp_n += 1;
+                    swp_piv += np;
+                }
+#endif
+            }
+        }
+#ifdef TCI_SW_PROF
+        if (tid == 0 && swp_n > 0)
+            printf("[sweep_small] %d bonds %d pivots: union %.2f (staging %.2f) | Pi %.2f (states %.2f loop %.2f maxabs %.2f) | "
+                   "rrLU %.2f | select %.2f us per bond\n",
+                   swp_n, swp_piv, swp_acc[0] * 0.01 / swp_n, swp_acc[4] * 0.01 / swp_n, swp_acc[1] * 0.01 / swp_n,
+                   swp_acc[5] * 0.01 / swp_n, swp_acc[6] * 0.01 / swp_n, swp_acc[7] * 0.01 / swp_n,
+                   swp_acc[2] * 0.01 / swp_n, swp_acc[3] * 0.01 / swp_n);
+        if (tid == 0)
+            printf("[sweep_small] regs-LU us total: load+take %.1f | wave argmax %.1f | barrier1 %.1f | row argmax %.1f | "
+                   "decide+maps %.1f | normalise %.1f | barrier2 %.1f | update %.1f | loop exit %.1f | NaN %.1f\n",
+                   g_swlu[0] * 0.01, g_swlu[1] * 0.01, g_swlu[2] * 0.01, g_swlu[3] * 0.01, g_swlu[4] * 0.01,
+                   g_swlu[5] * 0.01, g_swlu[6] * 0.01, g_swlu[7] * 0.01, g_swlu[8] * 0.01, g_swlu[9] * 0.01);
+        if (tid == 0)
+            for (int i = 0; i < 12; ++i) g_swlu[i] = 0;
+        if (tid == 0)
+            printf("[sweep_small] shader clock %.3f GHz over %.1f us\n",
+                   (double)(clock64() - swp_c0) / ((double)(wall_clock64() - swp_w0) * 10.0),
+                   (double)(wall_clock64() - swp_w0) * 0.01);
+#endif
+    }
+    if ((a.mode == 1 || a.fill) && status == 0) {
+        // fillsitetensors!(tci, f) with the solve unobservable: updatemaxsample!(tci, Pi1) per site
+        fstatus = 0;
+        for (int s = 0; s < L; ++s) {
+            const int nI = set_cnt(0, 0, s), nJ = set_cnt(1, 0, s), d = ldm[s];
+            if (s < L - 1 && set_cnt(0, 0, s + 1) != nJ) {
+                fstatus = 4;  // "Pivot matrix at bond b is not square!"
+                fsite = s + 1;
+                break;
+            }
+            const int R = nI * d;
+            if ((int64_t)R + nJ > kSmallElems) {
+                fstatus = 5;  // too many states for LDS: the host evaluates it
+                fsite = s + 1;
+                break;
+            }
+            St* rs = reinterpret_cast<St*>(S);
+            St* cs = rs + R;
+            const int wI = s, wJ = L - 1 - s;
+            const int32_t* Ib = set_ptr(0, 0, s);
+            const int32_t* Jb = set_ptr(1, 0, s);
+            for (int r = tid; r < R; r += kSwThreads) rs[r] = leg_state(f, Ib + (r % nI) * wI, wI, 0, r / nI + 1);
+            for (int j = tid; j < nJ; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, s + 1, 0);
+            __syncthreads();
+            double mx = 0.0;
+#pragma unroll 1
+            for (int64_t e = tid; e < (int64_t)R * nJ; e += kSwThreads) {
+                const double v = combine<KIND>(p, p0, rs[e % R], cs[e / R], wJ, L, nullptr, 0);
+                const double av = fabs(v);
+                mx = (isnan(av) || av > mx) ? av : mx;
+            }
+            mx = sw_maxabs(mx, &mxs);
+            maxsample = jl_max(fabs(maxsample), fabs(mx));
+        }
+    }
+    __syncthreads();
+
+    // ---- output: header, counts (logical banks), bond errors, pivot errors, the sets
+    int64_t* out_hdr = reinterpret_cast<int64_t*>(a.out);
+    int64_t* out_cnt = reinterpret_cast<int64_t*>(a.out + io.counts);
+    if (tid == 0) {
+        out_hdr[0] = status;
+        out_hdr[1] = s_it;
+        out_hdr[2] = s_q;
+        out_hdr[3] = has_history;
+        out_hdr[4] = extra_valid;
+        out_hdr[5] = npe;
+        out_hdr[6] = (int64_t)__double_as_longlong(maxsample);
+        out_hdr[7] = esite;
+        out_hdr[8] = fstatus;
+        out_hdr[9] = fsite;
+    }
+    // logical bank lb: 0 / 1 current I / J, 2 / 3 history, 4 / 5 extra
+    for (int i = tid; i < 6 * L; i += kSwThreads) {
+        const int lb = i / L, s = i % L;
+        out_cnt[i] = (lb >= 4 && !extra_valid) ? 0 : set_cnt(lb & 1, lb >> 1, s);
+    }
+    for (int i = tid; i < L - 1; i += kSwThreads) reinterpret_cast<double*>(a.out + io.bonderr)[i] = bonderr[i];
+    for (int i = tid; i < npe; i += kSwThreads) reinterpret_cast<double*>(a.out + io.pe)[i] = pe[i];
+    {
+        int32_t* dst = reinterpret_cast<int32_t*>(a.out + io.sets);
+        for (int lb = 0; lb < (extra_valid ? 6 : 4); ++lb)
+            for (int s = 0; s < L; ++s) {
+                const int ne = set_cnt(lb & 1, lb >> 1, s) * width(lb, s);
+                sw_copy(dst, set_ptr(lb & 1, lb >> 1, s), ne);
+                dst += ne;
+            }
+    }
+}
+
+size_t sweep_small_lds_bytes() { return kSwLds; }
+
+hipError_t launch_sweep_small(hipStream_t s, const SweepSmallArgs& a) {
+    const void* fn = nullptr;
+    switch (a.f.kind) {
+    case F_SUM: fn = reinterpret_cast<const void*>(&k_sweep_small<F_SUM>); break;
+    case F_LORENTZ: fn = reinterpret_cast<const void*>(&k_sweep_small<F_LORENTZ>); break;
+    case F_TABLE: fn = reinterpret_cast<const void*>(&k_sweep_small<F_TABLE>); break;
+    case F_GAUSS: fn = reinterpret_cast<const void*>(&k_sweep_small<F_GAUSS>); break;
+    case F_QOSC: fn = reinterpret_cast<const void*>(&k_sweep_small<F_QOSC>); break;
+    case F_QEXP: fn = reinterpret_cast<const void*>(&k_sweep_small<F_QEXP>); break;
+    default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSwLds);
+    if (e != hipSuccess) return e;
+    switch (a.f.kind) {
+#define TCI_SW(K)                                                                                    \
+    case K: hipLaunchKernelGGL(k_sweep_small<K>, dim3(1), dim3(kSwThreads), kSwLds, s, a); break;
+        TCI_SW(F_SUM) TCI_SW(F_LORENTZ) TCI_SW(F_TABLE) TCI_SW(F_GAUSS) TCI_SW(F_QOSC) TCI_SW(F_QEXP)
+#undef TCI_SW
+    default: break;
+    }
+    return hipGetLastError();
+}
+
+bool sweep_small_kind(int kind) { return staged_kind(kind); }
+
+}  // namespace tci

@@ -316,8 +316,13 @@ class TensorCI2:
         self.invalidatesitetensors()
         n = len(self)
         if native is not False and NATIVE_SWEEP and _native_ok(f) and fillsitetensors:
-            self._sweep2site_native(f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested)
-            self.fillsitetensors(f, solve=not lazy_sitetensors)
+            # with lazy site tensors (solve unobservable) fillsitetensors! is only updatemaxsample!
+            # over every site's Pi1: the native object does it on the device in the same call
+            # sequence when it can (tci_tci2_fill_maxsample)
+            done = self._sweep2site_native(f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
+                                           fill_maxsample=lazy_sitetensors)
+            if not done:
+                self.fillsitetensors(f, solve=not lazy_sitetensors)
             return
         for it in range(iter1, iter1 + niter):
             extraI = [None] * n
@@ -341,7 +346,11 @@ class TensorCI2:
         if fillsitetensors:
             self.fillsitetensors(f, solve=not lazy_sitetensors)
 
-    def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested):
+    def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
+                           fill_maxsample=False):
+        """The iterations in C++ / on the device (tci_tci2_sweep2site): the state goes in and comes
+        back bank by bank (a few ABI calls, not one per set). Returns whether fillsitetensors!'s
+        maxsample update was done natively too (fill_maxsample and tci_tci2_fill_maxsample handled it)."""
         ctx = f.ctx
         lib = ctx.lib
         n = len(self)
@@ -351,18 +360,21 @@ class TensorCI2:
             ctx.check(lib.tci_tci2_create(ctx.h, n, np.ascontiguousarray(self.localdims, np.int32), C.byref(h)))
             self._native_h, self._native_ctx = h, ctx
             self._native_owner = ctx.own(_NativeTCI2(ctx, h))
+        widths = [list(range(n)), [n - 1 - p for p in range(n)]]
 
-        def push(which, p, a):
-            a = np.ascontiguousarray(a, np.int32)
-            ctx.check(lib.tci_tci2_set_set(h, which, p, a.ctypes.data_as(C.c_void_p), len(a)))
+        def push(which, sets):
+            counts = np.array([len(a) for a in sets], np.int64)
+            parts = [np.ascontiguousarray(a, np.int32).ravel() for a in sets]
+            packed = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+            packed = np.ascontiguousarray(packed, np.int32)
+            ctx.check(lib.tci_tci2_set_sets(h, which, counts.ctypes.data_as(C.c_void_p),
+                                            packed.ctypes.data_as(C.c_void_p)))
 
-        for p in range(n):
-            push(0, p, self.Iset[p])
-            push(1, p, self.Jset[p])
+        push(0, self.Iset)
+        push(1, self.Jset)
         if self.Iset_history:
-            for p in range(n):
-                push(2, p, self.Iset_history[-1][p])
-                push(3, p, self.Jset_history[-1][p])
+            push(2, self.Iset_history[-1])
+            push(3, self.Jset_history[-1])
         else:
             ctx.check(lib.tci_tci2_clear_history(h))
         pe = np.ascontiguousarray(self.pivoterrors, np.float64)
@@ -370,30 +382,49 @@ class TensorCI2:
                                           np.ascontiguousarray(self.bonderrors, np.float64).ctypes.data_as(C.c_void_p),
                                           pe.ctypes.data_as(C.c_void_p), len(pe)))
         strat = {"backandforth": 0, "forward": 1, "backward": 2}[sweepstrategy]
-        ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol), int(min(maxbonddim, INT64_MAX)),
-                                          strat, int(bool(strictlynested))))
+        handled = C.c_int(0)
+        if fill_maxsample and niter > 0:
+            ctx.check(lib.tci_tci2_sweep2site_fill(h, f.h, int(niter), int(iter1), float(abstol),
+                                                   int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested)),
+                                                   C.byref(handled)))
+        else:
+            ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol),
+                                              int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested))))
+            if fill_maxsample:
+                ctx.check(lib.tci_tci2_fill_maxsample(h, f.h, C.byref(handled)))
 
-        def pull(which, p, w):
-            cnt = C.c_int64()
-            ctx.check(lib.tci_tci2_get_set(h, which, p, None, 0, C.byref(cnt)))
-            a = np.zeros((cnt.value, w), np.int32)
-            if w and cnt.value:
-                ctx.check(lib.tci_tci2_get_set(h, which, p, a.ctypes.data_as(C.c_void_p), cnt.value, C.byref(cnt)))
-            return a
+        def pull(which):
+            counts = np.zeros(n, np.int64)
+            ctx.check(lib.tci_tci2_get_sets(h, which, counts.ctypes.data_as(C.c_void_p), None, 0))
+            w = widths[which % 2]
+            tot = int(sum(int(c) * w[p] for p, c in enumerate(counts)))
+            packed = np.zeros(max(tot, 1), np.int32)
+            ctx.check(lib.tci_tci2_get_sets(h, which, counts.ctypes.data_as(C.c_void_p),
+                                            packed.ctypes.data_as(C.c_void_p), len(packed)))
+            out, o = [], 0
+            for p, c in enumerate(counts):
+                k = int(c) * w[p]
+                out.append(packed[o:o + k].reshape(int(c), w[p]).copy())
+                o += k
+            return out
 
-        self.Iset = [pull(0, p, p) for p in range(n)]
-        self.Jset = [pull(1, p, n - 1 - p) for p in range(n)]
-        self.Iset_history = [[pull(2, p, p) for p in range(n)]]
-        self.Jset_history = [[pull(3, p, n - 1 - p) for p in range(n)]]
+        self.Iset = pull(0)
+        self.Jset = pull(1)
+        self.Iset_history = [pull(2)]
+        self.Jset_history = [pull(3)]
         ms, npe = C.c_double(), C.c_int64()
         be = np.zeros(n - 1)
-        ctx.check(lib.tci_tci2_errors(h, C.byref(ms), be.ctypes.data_as(C.c_void_p), None, 0, C.byref(npe)))
-        pe = np.zeros(max(npe.value, 1))
+        pe = np.zeros(2048 + 1)
         ctx.check(lib.tci_tci2_errors(h, C.byref(ms), be.ctypes.data_as(C.c_void_p), pe.ctypes.data_as(C.c_void_p),
-                                      npe.value, C.byref(npe)))
+                                      len(pe), C.byref(npe)))
+        if npe.value > len(pe):
+            pe = np.zeros(npe.value)
+            ctx.check(lib.tci_tci2_errors(h, C.byref(ms), be.ctypes.data_as(C.c_void_p),
+                                          pe.ctypes.data_as(C.c_void_p), npe.value, C.byref(npe)))
         self.maxsamplevalue = ms.value
         self.bonderrors = be
         self.pivoterrors = pe[: npe.value].copy()
+        return bool(handled.value)
 
     def optimize(self, f, tolerance=None, pivottolerance=None, maxbonddim=INT64_MAX, maxiter=20,
                  sweepstrategy="backandforth", pivotsearch="full", verbosity=0, loginterval=10,
