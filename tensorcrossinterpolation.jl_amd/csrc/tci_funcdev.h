@@ -32,6 +32,21 @@ union St {
     double d;
 };
 
+// fn(t, e[t]) for t = 0 .. w-1 in order, the loads issued eight at a time (a runtime-length loop
+// of dependent LDS / L2 round trips otherwise)
+template <class Fn>
+__device__ __forceinline__ void for_legs(const int32_t* e, int w, Fn fn) {
+    int t = 0;
+    for (; t + 8 <= w; t += 8) {
+        int32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = e[t + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) fn(t + u, x[u]);
+    }
+    for (; t < w; ++t) fn(t, e[t]);
+}
+
 // The state of legs e[0 .. w-1] at global positions toff .. toff + w - 1, then, if cval > 0, one
 // more leg of value cval at position toff + w (the centre index of a site tensor's Pi1 row).
 __device__ __forceinline__ St leg_state(const FuncDev& f, const int32_t* e, int w, int toff, int cval) {
@@ -39,25 +54,26 @@ __device__ __forceinline__ St leg_state(const FuncDev& f, const int32_t* e, int 
     s.i = 0;
     switch (f.kind) {
     case F_SUM:
-        for (int t = 0; t < w; ++t) s.i += e[t];
+        for_legs(e, w, [&](int, int32_t x) { s.i += x; });
         if (cval > 0) s.i += cval;
         break;
     case F_LORENTZ:
-        for (int t = 0; t < w; ++t) s.i += (int64_t)e[t] * e[t];
+        for_legs(e, w, [&](int, int32_t x) { s.i += (int64_t)x * x; });
         if (cval > 0) s.i += (int64_t)cval * cval;
         break;
     case F_TABLE:
-        for (int t = 0; t < w; ++t) s.i += (int64_t)(e[t] - 1) * f.strides[toff + t];
+        for_legs(e, w, [&](int t, int32_t x) { s.i += (int64_t)(x - 1) * f.strides[toff + t]; });
         if (cval > 0) s.i += (int64_t)(cval - 1) * f.strides[toff + w];
         break;
     case F_GAUSS: {
         double a = 0.0;
-        for (int t = 0; t < w; ++t) {
-            const double u = (double)e[t] - f.params[1];
+        const double c = f.params[1];
+        for_legs(e, w, [&](int, int32_t x) {
+            const double u = (double)x - c;
             a = __dadd_rn(a, __dmul_rn(u, u));
-        }
+        });
         if (cval > 0) {
-            const double u = (double)cval - f.params[1];
+            const double u = (double)cval - c;
             a = __dadd_rn(a, __dmul_rn(u, u));
         }
         s.d = a;
@@ -65,7 +81,7 @@ __device__ __forceinline__ St leg_state(const FuncDev& f, const int32_t* e, int 
     case F_QOSC:
     case F_QEXP: {
         uint64_t idx = 0;
-        for (int t = 0; t < w; ++t) idx = (idx << 1) | (uint64_t)(e[t] - 1);
+        for_legs(e, w, [&](int, int32_t x) { idx = (idx << 1) | (uint64_t)(x - 1); });
         if (cval > 0) idx = (idx << 1) | (uint64_t)(cval - 1);
         s.i = (int64_t)idx;
     } break;

@@ -23,6 +23,8 @@
 #include "tci_internal.h"
 #include "tci_smalllu.h"
 
+#include <type_traits>
+
 namespace tci {
 
 constexpr int kSwThreads = 256;  // 4 waves, one per SIMD: the small rrLU's per-pivot barriers are cheap
@@ -57,6 +59,9 @@ __device__ __forceinline__ void sw_copy(int32_t* dst, const int32_t* src, int n)
     }
 }
 
+#ifndef TCI_SW_PROF
+#define SWP_ACC nullptr
+#endif
 #ifdef TCI_SW_PROF  // phase profile (thread 0, wall clock ticks): kron+union, Pi, rrLU, selection
 #define SWP(i) (swp_t[i] = wall_clock64())
 #else
@@ -65,8 +70,13 @@ __device__ __forceinline__ void sw_copy(int32_t* dst, const int32_t* src, int n)
 
 __device__ __forceinline__ uint32_t sw_hash(const int32_t* e, int w) {
     uint32_t h = 2166136261u;
-    for (int t = 0; t < w; ++t) h = (h ^ (uint32_t)e[t]) * 16777619u;
+    for_legs(e, w, [&](int, int32_t x) { h = (h ^ (uint32_t)x) * 16777619u; });
     return h;
+}
+
+// dst[0 .. w) = src[0 .. w), eight loads in flight
+__device__ __forceinline__ void sw_copy_row(int32_t* dst, const int32_t* src, int w) {
+    for_legs(src, w, [&](int t, int32_t x) { dst[t] = x; });
 }
 
 // exclusive prefix sum of v over the workgroup in thread order; *total gets the sum
@@ -125,7 +135,7 @@ __device__ int sw_union(const int32_t* __restrict__ cat, int n, int w, int32_t* 
     int pos = sw_scan(nk, scr, &total);
     for (int t = t0; t < t1; ++t)
         if (keep[t]) {
-            for (int z = 0; z < w; ++z) dst[(int64_t)pos * w + z] = cat[(int64_t)t * w + z];
+            sw_copy_row(dst + (int64_t)pos * w, cat + (int64_t)t * w, w);
             ++pos;
         }
     __syncthreads();
@@ -167,6 +177,24 @@ __device__ __forceinline__ void wave_sync() {
 __device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
     constexpr int U = kSwWaveU / 64;
     const int lane = threadIdx.x & 63;
+    if (n <= 64) {  // one entry per lane (every bond of the small configs)
+        bool keep = lane < n;
+        const uint32_t h = keep ? sw_hash(cat + lane * w, w) : 0u;
+        for (int s = 0; s < n - 1; ++s) {
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)h, s);
+            if (keep && lane > s && h == hs) {
+                bool eq = true;
+                for (int z = 0; z < w && eq; ++z) eq = cat[s * w + z] == cat[lane * w + z];
+                if (eq) keep = false;
+            }
+        }
+        const uint64_t bal = __ballot(keep);
+        if (keep) {
+            const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+            sw_copy_row(dst + pos * w, cat + lane * w, w);
+        }
+        return __popcll(bal);
+    }
     const int nu = (n + 63) >> 6;
     uint32_t h[U];
     bool keep[U];
@@ -202,7 +230,7 @@ __device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
             const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
             const int t = lane + 64 * u;
-            for (int z = 0; z < w; ++z) dst[pos * w + z] = cat[t * w + z];
+            sw_copy_row(dst + pos * w, cat + t * w, w);
         }
         base += __popcll(bal);
     }
@@ -215,15 +243,47 @@ __device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
 // position) order, the same multiply / subtract / divide on the same values, so the same pivots
 // and bits. Two barriers per pivot (winner; pivot row / column), no LDS traffic per element.
 constexpr int kSwRegN = 64;
+
+// the wave's best candidate (larger abs2, then the smaller key; abs2 is -1 or >= 0, never NaN),
+// uniform in every lane: the maximum abs2 by DPP (IEEE max) within rows of 16 and readlane across
+// them, then, unless one lane holds it alone, the smallest key among the lanes that hold it --
+// a short dependent chain, not the full (value, key, payload) tournament of wave_argmax3
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_min_u32(unsigned v) {
+    return min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ void wave_best(double& bv, unsigned& bk, double& bx) {
+    double m = bv;
+    m = fmax(m, dpp_f64<0xb1>(m));
+    m = fmax(m, dpp_f64<0x4e>(m));
+    m = fmax(m, dpp_f64<0x141>(m));
+    m = fmax(m, dpp_f64<0x140>(m));
+    const double vmax = fmax(fmax(readlane_f64(m, 0), readlane_f64(m, 16)), fmax(readlane_f64(m, 32), readlane_f64(m, 48)));
+    const uint64_t hold = __ballot(bv == vmax);
+    int lane;
+    if (__popcll(hold) == 1) {
+        lane = __builtin_ctzll(hold);
+    } else {
+        unsigned k = bv == vmax ? bk : 0xffffffffu;
+        k = dpp_min_u32<0xb1>(k);
+        k = dpp_min_u32<0x4e>(k);
+        k = dpp_min_u32<0x141>(k);
+        k = dpp_min_u32<0x140>(k);
+        const unsigned kmin = min(min((unsigned)__builtin_amdgcn_readlane((int)k, 0), (unsigned)__builtin_amdgcn_readlane((int)k, 16)),
+                                  min((unsigned)__builtin_amdgcn_readlane((int)k, 32), (unsigned)__builtin_amdgcn_readlane((int)k, 48)));
+        lane = __builtin_ctzll(__ballot(bv == vmax && bk == kmin));
+    }
+    bk = (unsigned)__builtin_amdgcn_readlane((int)bk, lane);
+    bx = readlane_f64(bx, lane);
+    bv = vmax;
+}
+
 #ifdef TCI_SW_PROF
-__device__ unsigned long long g_swlu[12];
 #define LUP(i)                                                       \
     do {                                                             \
-        if (threadIdx.x == 0) {                                      \
-            const unsigned long long t_ = wall_clock64();            \
-            g_swlu[i] += t_ - lup_t;                                 \
-            lup_t = t_;                                              \
-        }                                                            \
+        const unsigned long long t_ = wall_clock64();                \
+        lup_acc[i] += t_ - lup_t;                                    \
+        lup_t = t_;                                                  \
     } while (0)
 #else
 #define LUP(i) ((void)0)
@@ -231,7 +291,9 @@ __device__ unsigned long long g_swlu[12];
 
 __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
                           int leftorth, int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red,
-                          double* pvl, int* nslot, double* dslot, double& error, double& maxerror, int& nanfl) {
+                          double* pvl, int* nslot, double* dslot, double& error, double& maxerror, int& nanfl,
+                          unsigned long long* lup_acc) {
+    (void)lup_acc;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tr = tid & 15, tc = tid >> 4;
 #ifdef TCI_SW_PROF
@@ -251,36 +313,51 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
     for (int i = tid; i < m; i += kSwThreads) rowphys[i] = i;
     for (int j = tid; j < n; j += kSwThreads) colphys[j] = j;
     if (tid == 0) *nslot = 0;
-    double bv = -1.0, bx = 0.0;
-    unsigned bk = 0xffffffffu;
+    double bv, bx;
+    unsigned bk;
     auto take = [&](double a2, unsigned key, double val) {
         const bool better = (a2 > bv) || (a2 == bv && key < bk);  // NaN never wins
         bv = better ? a2 : bv;
         bk = better ? key : bk;
         bx = better ? val : bx;
     };
+    // candidates of the trailing block (positions >= k0): abs2, key = (column << 16 | row) positions
+    auto scan = [&](int k0) {
+        bv = -1.0;
+        bk = 0xffffffffu;
+        bx = 0.0;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-            if (rpos[a] >= 0 && cpos[b] >= 0)
-                take(__dmul_rn(v[a][b], v[a][b]), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], v[a][b]);
+            for (int b = 0; b < 4; ++b)
+                if (rpos[a] >= k0 && cpos[b] >= k0)
+                    take(__dmul_rn(v[a][b], v[a][b]), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], v[a][b]);
+    };
+    scan(0);
     maxerror = 0.0;
     error = __longlong_as_double(0x7ff8000000000000LL);
-    int np = 0;
+    int np = 0, fl = 0;
     LUP(0);
     for (int k = 0; k < mr; ++k) {
-        wave_argmax3(bv, bk, bx);
+        wave_best(bv, bk, bx);
         LUP(1);
         if (lane == 0) red[w] = SmallCand{bv, bk, 0u, bx};
         __syncthreads();
         LUP(2);
-        SmallCand c = lane < kSwWaves ? red[lane] : SmallCand{-1.0, 0xffffffffu, 0u, 0.0};
-        row_argmax_dpp(c.v, c.key, c.val);
+        double cv = red[0].v, cx = red[0].val;
+        unsigned ck = red[0].key;
+#pragma unroll
+        for (int q = 1; q < kSwWaves; ++q) {
+            const SmallCand o = red[q];
+            const bool t = (o.v > cv) || (o.v == cv && o.key < ck);
+            cv = t ? o.v : cv;
+            ck = t ? o.key : ck;
+            cx = t ? o.val : cx;
+        }
         LUP(3);
-        int pp = (int)(c.key & 0xffffu), qq = (int)(c.key >> 16);
-        double val = c.val;
-        if (!(c.v >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
+        int pp = (int)(ck & 0xffffu), qq = (int)(ck >> 16);
+        double val = cx;
+        if (!(cv >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
             pp = qq = k;
             const int r0 = rowphys[k], c0 = colphys[k];
 #pragma unroll
@@ -296,6 +373,7 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
         maxerror = jl_max(maxerror, error);
         np = k + 1;
         if (tid == 0) pvl[k] = val;
+        if (isnan(val)) fl |= 3;  // the pivot sits on both tril and triu
         const int pr = rowphys[pp], pc = colphys[qq];
         LUP(4);
         // swaprow!(k, pp) / swapcol!(k, qq) as position swaps
@@ -303,23 +381,47 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
         for (int a = 0; a < 4; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
 #pragma unroll
         for (int b = 0; b < 4; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
-        // normalisation (true division) of the pivot column / row below / right of the pivot
+        // normalisation (true division) of the pivot column below / pivot row right of the pivot:
+        // the owners are one thread column / row, the tile slot b = pc / 16 (a = pr / 16) uniform
         const double piv = val;
+        auto norm_col = [&](auto bc) {
+            constexpr int b = decltype(bc)::value;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                if (tc + 16 * b == pc && rpos[a] > k) {
+            for (int a = 0; a < 4; ++a)
+                if (rpos[a] > k) {
                     const double x = leftorth ? v[a][b] / piv : v[a][b];
                     v[a][b] = x;
                     xv[tr + 16 * a] = x;
+                    fl |= isnan(x) ? 1 : 0;
                 }
-                if (tr + 16 * a == pr && cpos[b] > k) {
+        };
+        auto norm_row = [&](auto ac) {
+            constexpr int a = decltype(ac)::value;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (cpos[b] > k) {
                     const double y = leftorth ? v[a][b] : v[a][b] / piv;
                     v[a][b] = y;
                     yv[tc + 16 * b] = y;
+                    fl |= isnan(y) ? 2 : 0;
                 }
+        };
+        if (tc == (pc & 15)) {
+            switch (pc >> 4) {
+            case 0: norm_col(std::integral_constant<int, 0>{}); break;
+            case 1: norm_col(std::integral_constant<int, 1>{}); break;
+            case 2: norm_col(std::integral_constant<int, 2>{}); break;
+            default: norm_col(std::integral_constant<int, 3>{}); break;
             }
+        }
+        if (tr == (pr & 15)) {
+            switch (pr >> 4) {
+            case 0: norm_row(std::integral_constant<int, 0>{}); break;
+            case 1: norm_row(std::integral_constant<int, 1>{}); break;
+            case 2: norm_row(std::integral_constant<int, 2>{}); break;
+            default: norm_row(std::integral_constant<int, 3>{}); break;
+            }
+        }
         LUP(5);
         __syncthreads();
         LUP(6);
@@ -331,15 +433,15 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
             colphys[k] = colphys[qq];
             colphys[qq] = t;
         }
-        // rank-1 update of the trailing block (mul then sub), fused with the next argmax
-        bv = -1.0;
-        bk = 0xffffffffu;
-        bx = 0.0;
+        // rank-1 update of the trailing block (mul then sub), then the next pivot's candidates
         double xr[4], yc[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) xr[a] = rpos[a] > k ? xv[tr + 16 * a] : 0.0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) yc[b] = cpos[b] > k ? yv[tc + 16 * b] : 0.0;
+        bv = -1.0;
+        bk = 0xffffffffu;
+        bx = 0.0;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -352,16 +454,8 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
         LUP(7);
     }
     LUP(8);
-    // tril(A[:, 1:np]) / triu(A[1:np, :]) NaN checks (matrixlu.jl:376-381), position coordinates
-    int fl = 0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            if (rpos[a] >= 0 && cpos[b] >= 0 && isnan(v[a][b])) {
-                if (cpos[b] < np && rpos[a] >= cpos[b]) fl |= 1;
-                if (rpos[a] < np && cpos[b] >= rpos[a]) fl |= 2;
-            }
+    // tril(A[:, 1:np]) / triu(A[1:np, :]) NaN checks (matrixlu.jl:376-381): their entries are the
+    // pivots and the normalised column / row values, flagged as they were made
     if (fl) atomicOr(nslot, fl);
     __syncthreads();  // also publishes thread 0's last position swap
     nanfl = *nslot;
@@ -405,6 +499,8 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     const double p0 = (KIND == F_SUM || KIND == F_TABLE) ? 0.0 : p[0];
     const SwIO io = sw_io(L);
 #ifdef TCI_SW_PROF
+    unsigned long long lu_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define SWP_ACC lu_acc
     unsigned long long swp_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, swp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int swp_n = 0, swp_piv = 0;
     const unsigned long long swp_c0 = clock64(), swp_w0 = wall_clock64();
@@ -520,7 +616,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                         for (int e = t0; e < nI * dI; e += stride) {
                             const int i = e % nI, j = e / nI;
                             int32_t* o = catIp + e * b;
-                            for (int t = 0; t < wI0; ++t) o[t] = Ib[i * wI0 + t];
+                            sw_copy_row(o, Ib + i * wI0, wI0);
                             o[wI0] = j + 1;
                         }
                         for (int e = t0; e < gEI; e += stride) catIp[nI * dI * b + e] = Ex[e];
@@ -530,7 +626,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                             const int i = e % dJ, jj = e / dJ;
                             int32_t* o = catJp + e * wJ1;
                             o[0] = i + 1;
-                            for (int t = 0; t < wJ0; ++t) o[1 + t] = Jb[jj * wJ0 + t];
+                            sw_copy_row(o + 1, Jb + jj * wJ0, wJ0);
                         }
                         for (int e = t0; e < gEJ; e += stride) catJp[nJ * dJ * wJ1 + e] = Ey[e];
                     };
@@ -594,7 +690,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int np, fl;
                 if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
                     np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
-                                    &nanflag, &dslot, error, maxerror, fl);
+                                    &nanflag, &dslot, error, maxerror, fl, SWP_ACC);
                 } else {
                     np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, red, xy,
                                                    xy + m, pvl, error, maxerror);
@@ -660,10 +756,8 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
         if (tid == 0)
             printf("[sweep_small] regs-LU us total: load+take %.1f | wave argmax %.1f | barrier1 %.1f | row argmax %.1f | "
                    "decide+maps %.1f | normalise %.1f | barrier2 %.1f | update %.1f | loop exit %.1f | NaN %.1f\n",
-                   g_swlu[0] * 0.01, g_swlu[1] * 0.01, g_swlu[2] * 0.01, g_swlu[3] * 0.01, g_swlu[4] * 0.01,
-                   g_swlu[5] * 0.01, g_swlu[6] * 0.01, g_swlu[7] * 0.01, g_swlu[8] * 0.01, g_swlu[9] * 0.01);
-        if (tid == 0)
-            for (int i = 0; i < 12; ++i) g_swlu[i] = 0;
+                   lu_acc[0] * 0.01, lu_acc[1] * 0.01, lu_acc[2] * 0.01, lu_acc[3] * 0.01, lu_acc[4] * 0.01,
+                   lu_acc[5] * 0.01, lu_acc[6] * 0.01, lu_acc[7] * 0.01, lu_acc[8] * 0.01, lu_acc[9] * 0.01);
         if (tid == 0)
             printf("[sweep_small] shader clock %.3f GHz over %.1f us\n",
                    (double)(clock64() - swp_c0) / ((double)(wall_clock64() - swp_w0) * 10.0),
