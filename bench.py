@@ -241,7 +241,7 @@ def main():
     }
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
-    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, shadow, sh_bytes))
+    out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, args.epochs, shadow, sh_bytes))
     # roofline calibration on the same buffers: 16-B stream read and stream copy, best grid
     import ctypes as C
     nel = A.ld * n
@@ -296,13 +296,13 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_final_pmc_summary.json")
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 11, "shadow": True, "sh_bytes": 2}  # the profiled command
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 3, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 
-def pmc_traffic(fam, m, n, r, nb, shadow, sh_bytes):
+def pmc_traffic(fam, m, n, r, nb, epochs, shadow, sh_bytes):
     """HBM bytes per launch of kernel family `fam` from the committed rocprofv3 PMC summary."""
-    if ({"m": m, "n": n, "r": r, "nb": nb, "shadow": shadow, "sh_bytes": sh_bytes} != PMC_CONFIG
+    if ({"m": m, "n": n, "r": r, "nb": nb, "epochs": epochs, "shadow": shadow, "sh_bytes": sh_bytes} != PMC_CONFIG
             or not os.path.exists(PMC_SUMMARY)):
         return {"traffic": None}
     with open(PMC_SUMMARY) as fh:

@@ -18,8 +18,13 @@ from collections import defaultdict
 
 def family(name):
     short = name.split("(")[0].replace("void ", "").strip()
-    if short.startswith(("tci::k_pass_sh<", "tci::k_pass_mf<")):
+    if short.startswith("tci::k_pass_mf<"):  # <P, EXT, RF>: RF = the shadow refresh pass
+        targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
+        return "rrlu_refresh_pass" if len(targs) > 2 and targs[2] == "true" else "rrlu_read_only_pass"
+    if short.startswith("tci::k_pass_sh<"):
         return "rrlu_read_only_pass"
+    if short.startswith("tci::k_pass_x<"):  # <MODE>: 1 write-back, 0 / 2 exact fallbacks
+        return {"1": "rrlu_write_back_pass", "2": "rrlu_refresh_pass"}.get(short[-2], "rrlu_read_only_pass")
     if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
         targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
         return "rrlu_write_back_pass" if targs[1] == "true" else "rrlu_read_only_pass"
