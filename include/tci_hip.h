@@ -296,6 +296,18 @@ int tci_tci2_get_sets(tci_tci2* tci, int which, int64_t* counts, int32_t* packed
  * kinds. *handled = 0: not done here (other kinds, a non-square pivot matrix, a site too large);
  * the caller runs its own loop (tci_sitetensor_h / a batch maxabs per site). */
 int tci_tci2_fill_maxsample(tci_tci2* tci, const tci_func* f, int* handled);
+/* Replaces sweep1site!(tci, f, sweepdirection; reltol, abstol, maxbonddim, updatetensors)
+ * (tensorci2.jl:659-725) for the staged catalog kinds when every bond fits the one-workgroup
+ * rrLU: the whole sweep in one device launch (per bond kronecker product on the sweep's side, Pi,
+ * updatemaxsample!, rrLU, the new sets, updateerrors!, and with updatetensors the MatrixLUCI
+ * left (forward) / right (backward) factor as the bond's site tensor, then Pi1 of the last site).
+ * Tensors: site p's at tensors[offsets[2p]], offsets[2p+1] doubles, column-major
+ * (len(Iset[p]) d) x len(Jset[p]) (forward) or len(Iset[p]) x (d len(Jset[p])) (backward bonds);
+ * capacity in doubles. *handled = 0 leaves the state untouched: the caller runs the sweep itself
+ * (other kinds, a bond too large, a NaN: the host loop raises the reference's error). */
+int tci_tci2_sweep1site(tci_tci2* tci, const tci_func* f, int32_t forward, double reltol, double abstol,
+                        int64_t maxbonddim, int32_t updatetensors, double* tensors, int64_t capacity,
+                        int64_t* offsets, int* handled);
 /* Device-resident sweeps (tci_sweep_small.hip): while every bond's Pi fits the one-workgroup rrLU,
  * tci_tci2_sweep2site runs whole iterations in one kernel launch for the staged catalog kinds
  * (SUM, LORENTZ, TABLE, GAUSS, QOSC, QEXP), bitwise the per-bond loop; on by default (env

@@ -78,6 +78,8 @@ struct tci_ctx {
     char* sw_out = nullptr;
     char* sw_out_d = nullptr;
     size_t capSwOut = 0;
+    double* sw_tens = nullptr;  // sweep1site's site tensors (device)
+    size_t capSwTens = 0;
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
@@ -929,7 +931,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->hin) hipHostFree(c->hin);
     if (c->hout) hipHostFree(c->hout);
     if (c->zbuf) hipHostFree(c->zbuf);
-    fr(c->sw_ws); fr(c->sw_inbuf);
+    fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens);
     if (c->sw_in) hipHostFree(c->sw_in);
     if (c->sw_out) hipHostFree(c->sw_out);
     if (c->hfn) hipHostFree(c->hfn);
@@ -2408,7 +2410,7 @@ bool tci_sweep_small_ok(tci_ctx* c, const tci_func* f, int L) {
 
 int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
                         int mode, int fill, int niter, int iter1, int strategy, int strictlynested, double abstol,
-                        int64_t maxbonddim, std::vector<char>& out) {
+                        int64_t maxbonddim, std::vector<char>& out, const tci::SwSweep1* s1) {
     auto width = [&](int bank, int p) { return (bank & 1) ? L - 1 - p : p; };
     const int64_t tot = 6 * cap * ((int64_t)L * (L - 1) / 2);  // six banks (tci_sweep_small.hip)
     const tci::SwIO io = tci::sw_io(L);
@@ -2435,6 +2437,16 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
     a.maxbonddim = maxbonddim;
     a.mode = mode;
     a.fill = fill;
+    a.s1fwd = s1 ? s1->forward : 0;
+    a.s1tens = s1 ? s1->tensors : 0;
+    a.reltol = s1 ? s1->reltol : 1e-14;
+    a.tens = nullptr;
+    a.tcap = 0;
+    if (s1 && s1->tensors) {  // the site tensors in HBM: [site] (offset, count), then the data
+        if ((st = ensure(c, &c->sw_tens, &c->capSwTens, (size_t)(2 * L + s1->tcap)))) return st;
+        a.tens = c->sw_tens;
+        a.tcap = s1->tcap;
+    }
     HIPCHK(c, tci::launch_sweep_small(c->stream, a));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t* hdr = reinterpret_cast<const int64_t*>(c->sw_out);
@@ -2445,6 +2457,14 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
         for (int p = 0; p < L; ++p) bytes += (size_t)cn[(size_t)b * L + p] * width(b, p) * 4;
     if (bytes > outcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: output image overflow");
     out.assign(c->sw_out, c->sw_out + bytes);
+    if (s1 && s1->tensors && hdr[0] == 0 && s1->table) {  // the tensors the sweep wrote, one copy
+        const int64_t used = hdr[10];
+        if (used < 0 || used > s1->tcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: tensor overflow");
+        HIPCHK(c, hipMemcpyAsync(s1->table, c->sw_tens, (size_t)(2 * L) * 8, hipMemcpyDeviceToHost, c->stream));
+        if (used > 0)
+            HIPCHK(c, hipMemcpyAsync(s1->data, c->sw_tens + 2 * L, (size_t)used * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     return TCI_OK;
 }
 

@@ -117,6 +117,24 @@ __global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
 
     const int nst = (g.k + kDgKB - 1) / kDgKB;
     load(0);
+    // beta != 0 (the Schur update, the blocked solves' updates): the C tile's loads go out now,
+    // so their latency hides behind the k loop instead of following it (at nb = 32-64 the C round
+    // trip is most of the kernel)
+    double cpre[FM][FN][4];
+    const bool hasC = g.beta != 0.0;
+    if (hasC) {
+#pragma unroll
+        for (int x = 0; x < FM; ++x) {
+            const int i = i0 + wr + 16 * x + r;
+#pragma unroll
+            for (int y = 0; y < FN; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int j = j0 + wc + 16 * y + kk + 4 * q;
+                    cpre[x][y][q] = (i < g.m && j < g.n) ? g.C[(int64_t)i + (int64_t)j * g.ldc] : 0.0;
+                }
+        }
+    }
     store(0);
     __syncthreads();
     int cur = 0;
@@ -155,7 +173,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
                 const int j = j0 + wc + 16 * y + kk + 4 * q;
                 if (j >= g.n) continue;
                 double v = g.alpha * acc[x][y][q];
-                if (g.beta != 0.0) v = g.beta * g.C[(int64_t)i + (int64_t)j * g.ldc] + v;
+                if (hasC) v = g.beta * cpre[x][y][q] + v;
                 const int64_t ocol = g.cmap ? g.cmap[j] : j;
                 g.Out[orow + ocol * g.ldo] = v;
                 const unsigned long long b = (unsigned long long)__double_as_longlong(fabs(v));

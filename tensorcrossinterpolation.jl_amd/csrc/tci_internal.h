@@ -370,8 +370,21 @@ struct SweepSmallArgs {
     int niter, iter1, strategy, strictlynested;
     double abstol;
     int64_t maxbonddim;
-    int mode;              // 0: sweep2site! iterations; 1: fillsitetensors!'s maxsample update only
+    int mode;              // 0: sweep2site! iterations; 1: fillsitetensors!'s maxsample update only;
+                           // 2: sweep1site! (s1fwd, s1tens, reltol below)
     int fill;              // mode 0: the maxsample update after the iterations too (header [8] / [9])
+    int s1fwd, s1tens;     // mode 2: forward sweep; site tensors (MatrixLUCI factors) wanted
+    double reltol;         // mode 2: the rrLU's reltol
+    double* tens;          // mode 2: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
+    int64_t tcap;          // mode 2: doubles available after the 2 L table entries
+};
+// sweep1site! on the device (mode 2): the host's request and where the site tensors go
+struct SwSweep1 {
+    int forward, tensors;
+    double reltol;
+    int64_t tcap;      // doubles of tensor data the caller can take
+    int64_t* table;    // [site] (offset, count) into data, 2 L entries (host)
+    double* data;      // host
 };
 bool sweep_small_kind(int kind);
 size_t sweep_small_lds_bytes();

@@ -1691,7 +1691,10 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
 // again, which the bound recursion of k_pass_mf knows -- it re-derives every past decision). Same
 // grid, tiles, candidates and tail as k_pass2, so it also serves as k_pass_mf's fallback body.
 constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
-constexpr int kXStage = 128;  // staged columns per group
+#ifndef TCI_XSTAGE
+#define TCI_XSTAGE 128
+#endif
+constexpr int kXStage = TCI_XSTAGE;  // staged columns per group
 constexpr int kXU = 4;        // columns per chunk (two chunks in flight per lane)
 constexpr int kXSlices = kXHalf / 128;
 constexpr int kXReps = kP2Threads / 64 / kXSlices;

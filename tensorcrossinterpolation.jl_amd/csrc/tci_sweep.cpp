@@ -21,7 +21,7 @@
 bool tci_sweep_small_ok(tci_ctx* c, const tci_func* f, int L);
 int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
                         int mode, int fill, int niter, int iter1, int strategy, int strictlynested, double abstol,
-                        int64_t maxbonddim, std::vector<char>& out);
+                        int64_t maxbonddim, std::vector<char>& out, const tci::SwSweep1* s1 = nullptr);
 int tci_sweep_small_error(tci_ctx* c, int status, int64_t bond);
 
 namespace {
@@ -426,6 +426,33 @@ int tci_tci2_sweep2site_fill(tci_tci2* s, const tci_func* f, int32_t niter, int3
     return sweep2site_impl(s, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested, 1, filled);
 }
 
+
+// sweep1site! (tensorci2.jl:659-725) in one launch of the device-resident sweep (mode 2) when every
+// bond fits the one-workgroup rrLU; *handled = 0 (state untouched) otherwise or on any error, and the
+// host loop runs it. Site tensors (updatetensors) into tensors[offsets[2 p] ..] of offsets[2 p + 1]
+// doubles (column-major, the shape of site p: len(Iset[p]) * d x len(Jset[p]) or its transpose
+// layout of the right factor, as tci_update_pivots_h returns them).
+int tci_tci2_sweep1site(tci_tci2* s, const tci_func* f, int32_t forward, double reltol, double abstol,
+                        int64_t maxbonddim, int32_t updatetensors, double* tensors, int64_t capacity,
+                        int64_t* offsets, int* handled) {
+    if (!s || !f || !handled || (updatetensors && (!tensors || !offsets || capacity < 0))) return TCI_ERR_ARG;
+    *handled = 0;
+    if (!tci_sweep_small_ok(s->ctx, f, s->L)) return TCI_OK;
+    const std::vector<char> in = sw_pack(s);
+    std::vector<char> out;
+    tci::SwSweep1 s1{forward ? 1 : 0, updatetensors ? 1 : 0, reltol, updatetensors ? capacity : 0,
+                     updatetensors ? offsets : nullptr, updatetensors ? tensors : nullptr};
+    if (updatetensors)
+        for (int i = 0; i < 2 * s->L; ++i) offsets[i] = 0;
+    int st = tci_sweep_small_run(s->ctx, f, s->L, sw_capacity(s), in.data(), in.size(), 2, 0, 0, 1, 0, 0, abstol,
+                                 maxbonddim, out, &s1);
+    if (st) return st;
+    const int64_t status = reinterpret_cast<const int64_t*>(out.data())[0];
+    if (status != 0) return TCI_OK;  // the host loop redoes it (and raises the reference's errors)
+    sw_unpack(s, out, 0);
+    *handled = 1;
+    return TCI_OK;
+}
 
 int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) {
     if (!s || !f || !handled) return TCI_ERR_ARG;

@@ -74,6 +74,23 @@ __device__ __forceinline__ uint32_t sw_hash(const int32_t* e, int w) {
     return h;
 }
 
+// e[0 .. w) == f[0 .. w), eight loads of each in flight at a time (a chain of dependent LDS round
+// trips per leg otherwise)
+__device__ __forceinline__ bool sw_rows_equal(const int32_t* e, const int32_t* f, int w) {
+    bool eq = true;
+    for (int z0 = 0; z0 < w; z0 += 8) {
+        int32_t x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            x[u] = z0 + u < w ? e[z0 + u] : 0;
+            y[u] = z0 + u < w ? f[z0 + u] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) eq = eq && x[u] == y[u];
+    }
+    return eq;
+}
+
 // dst[0 .. w) = src[0 .. w), eight loads in flight
 __device__ __forceinline__ void sw_copy_row(int32_t* dst, const int32_t* src, int w) {
     for_legs(src, w, [&](int t, int32_t x) { dst[t] = x; });
@@ -118,10 +135,7 @@ __device__ int sw_union(const int32_t* __restrict__ cat, int n, int w, int32_t* 
         bool dup = false;
         for (int s = 0; s < t && !dup; ++s) {
             if (hs[s] != h) continue;
-            const int32_t* es = cat + (int64_t)s * w;
-            bool eq = true;
-            for (int z = 0; z < w && eq; ++z) eq = es[z] == et[z];
-            dup = eq;
+            dup = sw_rows_equal(cat + (int64_t)s * w, et, w);
         }
         keep[t] = dup ? 0 : 1;
     }
@@ -180,12 +194,27 @@ __device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
     if (n <= 64) {  // one entry per lane (every bond of the small configs)
         bool keep = lane < n;
         const uint32_t h = keep ? sw_hash(cat + lane * w, w) : 0u;
+        // the first earlier entry with the same hash, found in registers; then every lane compares
+        // its pair at once (the duplicates are the extra sets' entries already in the kronecker
+        // product). A hash collision that is not an equal entry falls back to the remaining
+        // earlier entries, one at a time (rare).
+        int cand = -1;
         for (int s = 0; s < n - 1; ++s) {
             const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)h, s);
-            if (keep && lane > s && h == hs) {
-                bool eq = true;
-                for (int z = 0; z < w && eq; ++z) eq = cat[s * w + z] == cat[lane * w + z];
-                if (eq) keep = false;
+            if (cand < 0 && keep && lane > s && h == hs) cand = s;
+        }
+        bool fb = false;
+        if (cand >= 0) {
+            if (sw_rows_equal(cat + cand * w, cat + lane * w, w))
+                keep = false;
+            else
+                fb = true;
+        }
+        if (__any(fb)) {  // uniform loop: readlane needs every lane
+            for (int s = 0; s < n - 1; ++s) {
+                const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)h, s);
+                if (fb && keep && s > cand && lane > s && h == hs && sw_rows_equal(cat + s * w, cat + lane * w, w))
+                    keep = false;
             }
         }
         const uint64_t bal = __ballot(keep);
@@ -214,11 +243,8 @@ __device__ int sw_union_wave(const int32_t* cat, int n, int w, int32_t* dst) {
 #pragma unroll
             for (int u = su; u < U; ++u) {
                 const int t = lane + 64 * u;
-                if (u < nu && keep[u] && t > s && h[u] == hs) {
-                    bool eq = true;
-                    for (int z = 0; z < w && eq; ++z) eq = cat[s * w + z] == cat[t * w + z];
-                    if (eq) keep[u] = false;
-                }
+                if (u < nu && keep[u] && t > s && h[u] == hs && sw_rows_equal(cat + s * w, cat + t * w, w))
+                    keep[u] = false;
             }
         }
     }
@@ -289,10 +315,10 @@ __device__ __forceinline__ void wave_best(double& bv, unsigned& bk, double& bx) 
 #define LUP(i) ((void)0)
 #endif
 
-__device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
+__device__ int sw_lu_regs(double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
                           int leftorth, int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red,
                           double* pvl, int* nslot, double* dslot, double& error, double& maxerror, int& nanfl,
-                          unsigned long long* lup_acc) {
+                          unsigned long long* lup_acc, bool posout = false) {
     (void)lup_acc;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tr = tid & 15, tc = tid >> 4;
@@ -457,7 +483,16 @@ __device__ int sw_lu_regs(const double* S, int ldS, int m, int n, int mr, double
     // tril(A[:, 1:np]) / triu(A[1:np, :]) NaN checks (matrixlu.jl:376-381): their entries are the
     // pivots and the normalised column / row values, flagged as they were made
     if (fl) atomicOr(nslot, fl);
-    __syncthreads();  // also publishes thread 0's last position swap
+    if (posout) {
+        // the packed factors in position order into S (what small_lu_core's physical swaps leave
+        // there), for the MatrixLUCI factors: every tile was read at the start, barriers since
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (rpos[a] >= 0 && cpos[b] >= 0) S[rpos[a] + cpos[b] * ldS] = v[a][b];
+    }
+    __syncthreads();  // also publishes thread 0's last position swap (and the position-order S)
     nanfl = *nslot;
     LUP(9);
     return np;
@@ -517,6 +552,46 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     auto bank_of = [&](int k, int r, int site) { return 2 * (int)rol[k][r][site] + k; };
     auto set_ptr = [&](int k, int r, int site) { return bank_ptr(bank_of(k, r, site), site); };
     auto set_cnt = [&](int k, int r, int site) -> int& { return cnt[bank_of(k, r, site) * kSwMaxL + site]; };
+    // Copies between the packed image (segments bank-major, site-minor, ne(i) ints each) and the set
+    // slots: the packed offsets by one workgroup scan (two segments per thread), then every wave
+    // copies segments wave, wave + 4, ... two at a time with all their loads in flight -- a few
+    // round trips per launch instead of one per segment (up to 6 L of them, each ~1 us).
+    __shared__ int segoff[6 * kSwMaxL];
+    auto copy_segments = [&](int nseg, auto ne_of, auto src_of, auto dst_of) {
+        {
+            const int i0 = 2 * tid, i1 = i0 + 1;
+            const int n0 = i0 < nseg ? ne_of(i0) : 0, n1 = i1 < nseg ? ne_of(i1) : 0;
+            int total;
+            const int o = sw_scan(n0 + n1, scr, &total);
+            if (i0 < nseg) segoff[i0] = o;
+            if (i1 < nseg) segoff[i1] = o + n0;
+        }
+        __syncthreads();
+        const int lane = tid & 63, w = tid >> 6;
+        for (int sg = w; sg < nseg; sg += 2 * kSwWaves) {
+            const int sa = sg, sb = sg + kSwWaves;
+            const int na = ne_of(sa), nb = sb < nseg ? ne_of(sb) : 0;
+            const int32_t* pa = src_of(sa, segoff[sa]);
+            const int32_t* pb = sb < nseg ? src_of(sb, segoff[sb]) : pa;
+            int32_t* da = dst_of(sa, segoff[sa]);
+            int32_t* db = sb < nseg ? dst_of(sb, segoff[sb]) : da;
+            for (int base = 0; base < max(na, nb); base += 4 * 64) {
+                int32_t va[4], vb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e = base + lane + 64 * u;
+                    va[u] = e < na ? pa[e] : 0;
+                    vb[u] = e < nb ? pb[e] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e = base + lane + 64 * u;
+                    if (e < na) da[e] = va[u];
+                    if (e < nb) db[e] = vb[u];
+                }
+            }
+        }
+    };
 
     // ---- input (DMA'd to a.inbuf by the host): header, counts, bond errors, the four banks
     if (tid < 16) hdr[tid] = reinterpret_cast<const int64_t*>(a.inbuf)[tid];
@@ -531,12 +606,9 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     __syncthreads();
     {
         const int32_t* src = reinterpret_cast<const int32_t*>(a.inbuf + io.sets);
-        for (int bank = 0; bank < 4; ++bank)
-            for (int s = 0; s < L; ++s) {
-                const int ne = cnt[bank * kSwMaxL + s] * width(bank, s);
-                sw_copy(bank_ptr(bank, s), src, ne);
-                src += ne;
-            }
+        copy_segments(
+            4 * L, [&](int i) { return cnt[(i / L) * kSwMaxL + i % L] * width(i / L, i % L); },
+            [&](int, int off) { return src + off; }, [&](int i, int) { return bank_ptr(i / L, i % L); });
     }
     int has_history = (int)hdr[3];
     double maxsample = __longlong_as_double((long long)hdr[6]);
@@ -764,6 +836,217 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                    (double)(wall_clock64() - swp_w0) * 0.01);
 #endif
     }
+    if (a.mode == 2) {
+        // sweep1site! (tensorci2.jl:659-725) with every bond in LDS: per bond b the sets of site
+        // p = b - 1 combined with the site's leg on the sweep's side -- forward Icomb =
+        // kronecker(Iset[p], d) (:671), Jcomb = Jset[p]; backward Icomb = Iset[p], Jcomb =
+        // kronecker(d, Jset[p]) (:675) -- Pi, updatemaxsample!, the rrLU (reltol, abstol,
+        // maxbonddim; leftorthogonal = forward), the new Iset[p + 1] / Jset[p] (forward) or Iset[p]
+        // / Jset[p - 1], updateerrors! at bond b (forward) / b - 1, and with updatetensors the
+        // site tensor T[b] = left(luci) / right(luci) (:703-711: the MatrixLUCI factors in
+        // k_rrlu_small's operation order) and finally T[L] / T[1] = Pi1 of the last site (:717-722).
+        // Any status but 0 leaves the host state untouched: the host loop then runs the sweep
+        // (and raises the reference's error where there is one).
+        const bool fwd = a.s1fwd != 0;
+        int64_t* ttab = reinterpret_cast<int64_t*>(a.tens);
+        double* tdat = a.tens + 2 * L;
+        int64_t tused = 0;
+        npe = 0;  // flushpivoterror!
+        for (int q = 1; q < L && status == 0; ++q) {
+            const int b = fwd ? q : L + 1 - q;  // 1-based: 1 .. L-1 forward, L .. 2 backward (:667)
+            const int ps = b - 1;
+            const int d = ldm[ps];
+            const int nI = set_cnt(0, 0, ps), nJ = set_cnt(1, 0, ps);
+            const int wIs = ps, wJs = L - 1 - ps;  // widths of Iset[p] / Jset[p]
+            const int m = fwd ? nI * d : nI, n = fwd ? nJ : nJ * d;
+            const int wI = fwd ? ps + 1 : ps, wJ = fwd ? L - 1 - ps : L - ps;
+            const size_t bI = sw_al16((size_t)m * wI * 4), bJ = sw_al16((size_t)n * wJ * 4);
+            const size_t bG = sw_al16((size_t)(nI * wIs + nJ * wJs) * 4);
+            const int ldS = m | 1;
+            const bool fits = m > 0 && n > 0 && (int64_t)ldS * n <= kSmallElems && m + n <= kSmallPerm &&
+                              a.maxbonddim > 0 && bG + bI + bJ <= kSwLdsS && (size_t)ldS * n * 8 + bI + bJ <= kSwLdsS;
+            if (!fits) {
+                status = 1;
+                break;
+            }
+            char* const R = reinterpret_cast<char*>(S);
+            int32_t* const gs = reinterpret_cast<int32_t*>(R);
+            int32_t* const Ic = reinterpret_cast<int32_t*>(R + kSwLdsS - bI - bJ);
+            int32_t* const Jc = reinterpret_cast<int32_t*>(R + kSwLdsS - bJ);
+            {  // Iset[p] and Jset[p] into LDS in one batched round of loads
+                const int32_t* s0 = set_ptr(0, 0, ps);
+                const int32_t* s1 = set_ptr(1, 0, ps);
+                const int g0 = nI * wIs, tot = g0 + nJ * wJs;
+                for (int base = 0; base < tot; base += kSwCopyB * kSwThreads) {
+                    int32_t v[kSwCopyB];
+#pragma unroll
+                    for (int u = 0; u < kSwCopyB; ++u) {
+                        const int e = base + tid + u * kSwThreads;
+                        v[u] = e < g0 ? s0[e] : e < tot ? s1[e - g0] : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSwCopyB; ++u) {
+                        const int e = base + tid + u * kSwThreads;
+                        if (e < tot) gs[e] = v[u];
+                    }
+                }
+            }
+            __syncthreads();
+            const int32_t* Ib = gs;
+            const int32_t* Jb = gs + nI * wIs;
+            if (fwd) {
+                for (int e = tid; e < m; e += kSwThreads) {  // kronecker(Iset, d): Iset fastest
+                    const int i = e % nI, j = e / nI;
+                    sw_copy_row(Ic + e * wI, Ib + i * wIs, wIs);
+                    Ic[e * wI + wIs] = j + 1;
+                }
+                for (int e = tid; e < n * wJ; e += kSwThreads) Jc[e] = Jb[e];
+            } else {
+                for (int e = tid; e < m * wI; e += kSwThreads) Ic[e] = Ib[e];
+                for (int e = tid; e < n; e += kSwThreads) {  // kronecker(d, Jset): the leg fastest
+                    const int i = e % d, jj = e / d;
+                    Jc[e * wJ] = i + 1;
+                    sw_copy_row(Jc + e * wJ + 1, Jb + jj * wJs, wJs);
+                }
+            }
+            __syncthreads();
+            St* rs = reinterpret_cast<St*>(xy);
+            St* cs = rs + m;
+            for (int i = tid; i < m; i += kSwThreads) rs[i] = leg_state(f, Ic + i * wI, wI, 0, 0);
+            for (int j = tid; j < n; j += kSwThreads) cs[j] = leg_state(f, Jc + j * wJ, wJ, wI, 0);
+            __syncthreads();
+            double mx = 0.0, error, maxerror;
+#pragma unroll 1
+            for (int e = tid; e < m * n; e += kSwThreads) {
+                const int i = e % m, j = e / m;
+                const double v = combine<KIND>(p, p0, rs[i], cs[j], wJ, L, nullptr, 0);
+                S[i + j * ldS] = v;
+                const double av = fabs(v);
+                mx = (isnan(av) || av > mx) ? av : mx;
+            }
+            mx = sw_maxabs(mx, &mxs);
+            const int mr = (int)(a.maxbonddim < (int64_t)min(m, n) ? a.maxbonddim : (int64_t)min(m, n));
+            int* rp = perm;
+            int* cp = perm + m;
+            int np, fl;
+            if (m <= kSwRegN && n <= kSwRegN) {
+                np = sw_lu_regs(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                                &nanflag, &dslot, error, maxerror, fl, SWP_ACC, a.s1tens != 0);
+            } else {
+                np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, red, xy,
+                                               xy + m, pvl, error, maxerror);
+                fl = small_lu_nanflags<kSwThreads>(S, ldS, m, n, np, &nanflag);
+            }
+            if (fl) {
+                status = (fl & 1) ? 2 : 3;
+                esite = b;
+                break;
+            }
+            const double err = np >= min(m, n) ? 0.0 : error;  // matrixlu.jl:391-393
+            maxsample = jl_max(fabs(maxsample), fabs(mx));
+            // the site tensor first (it reads the packed factors in S), then the new sets
+            if (a.s1tens) {
+                const int64_t cntT = fwd ? (int64_t)m * np : (int64_t)np * n;
+                if (tused + cntT > a.tcap) {
+                    status = 1;
+                    break;
+                }
+                double* T = tdat + tused;
+                if (fwd) {  // colstimespivotinv: rows >= np solve X L11 = L21 in place (matrixluci.jl:207)
+                    for (int i = np + tid; i < m; i += kSwThreads)
+                        for (int j = np - 1; j >= 0; --j) {
+                            double s = S[i + j * ldS];
+                            for (int t = j + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[i + t * ldS], S[t + j * ldS]));
+                            S[i + j * ldS] = s;
+                        }
+                    __syncthreads();
+                    int tf = 0;
+                    for (int e = tid; e < m * np; e += kSwThreads) {
+                        const int i = e % m, j = e / m;
+                        const double x = i < np ? (i == j ? 1.0 : 0.0) : S[i + j * ldS];
+                        T[rp[i] + (int64_t)j * m] = x;
+                        tf |= isnan(x) ? 1 : 0;
+                    }
+                    if (tf) atomicOr(&nanflag, 4);
+                } else {  // pivotinvtimesrows: columns >= np solve U11 x = U[:, c] in place (:235)
+                    for (int c = np + tid; c < n; c += kSwThreads)
+                        for (int r = np - 1; r >= 0; --r) {
+                            double s = S[r + c * ldS];
+                            for (int t = r + 1; t < np; ++t) s = __dsub_rn(s, __dmul_rn(S[r + t * ldS], S[t + c * ldS]));
+                            S[r + c * ldS] = s;
+                        }
+                    __syncthreads();
+                    int tf = 0;
+                    for (int e = tid; e < np * n; e += kSwThreads) {
+                        const int r = e % np, j = e / np;
+                        const double x = j < np ? (r == j ? 1.0 : 0.0) : S[r + j * ldS];
+                        T[r + (int64_t)cp[j] * np] = x;
+                        tf |= isnan(x) ? 1 : 0;
+                    }
+                    if (tf) atomicOr(&nanflag, 4);
+                }
+                __syncthreads();
+                if (nanflag & 4) {  // "Error: NaN in tensor T[b]" (tensorci2.jl:706): the host raises it
+                    status = 5;
+                    esite = b;
+                    break;
+                }
+                if (tid == 0) {
+                    ttab[2 * ps] = tused;
+                    ttab[2 * ps + 1] = cntT;
+                }
+                tused += cntT;
+            }
+            const int siteI = fwd ? ps + 1 : ps, siteJ = fwd ? ps : ps - 1;
+            int32_t* Io = set_ptr(0, 0, siteI);
+            int32_t* Jo = set_ptr(1, 0, siteJ);
+            for (int e = tid; e < np * wI; e += kSwThreads) Io[e] = Ic[rp[e / wI] * wI + e % wI];
+            for (int e = tid; e < np * wJ; e += kSwThreads) Jo[e] = Jc[cp[e / wJ] * wJ + e % wJ];
+            // updateerrors!(tci, b (forward) / b - 1 (backward), pivoterrors(lu))
+            const int ne = max(npe, np + 1);
+            for (int i = tid; i < ne; i += kSwThreads) {
+                const double nv = i < np ? fabs(pvl[i]) : (i == np ? err : 0.0);
+                pe[i] = jl_max(i < npe ? pe[i] : 0.0, nv);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                set_cnt(0, 0, siteI) = np;
+                set_cnt(1, 0, siteJ) = np;
+                bonderr[(fwd ? b : b - 1) - 1] = err;
+            }
+            npe = ne;
+            __syncthreads();
+        }
+        if (status == 0 && a.s1tens) {
+            // the last site's tensor: Pi1 = f(kronecker(Iset[p], d) x Jset[p]) (sitetensor, no solve)
+            const int ps = fwd ? L - 1 : 0;
+            const int nI = set_cnt(0, 0, ps), nJ = set_cnt(1, 0, ps), d = ldm[ps];
+            const int Rr = nI * d;
+            const int64_t cntT = (int64_t)Rr * nJ;
+            if ((int64_t)Rr + nJ > kSmallElems || tused + cntT > a.tcap) {
+                status = 1;
+            } else {
+                St* rs = reinterpret_cast<St*>(S);
+                St* cs = rs + Rr;
+                const int wI = ps, wJ = L - 1 - ps;
+                const int32_t* Ib = set_ptr(0, 0, ps);
+                const int32_t* Jb = set_ptr(1, 0, ps);
+                for (int r = tid; r < Rr; r += kSwThreads) rs[r] = leg_state(f, Ib + (r % nI) * wI, wI, 0, r / nI + 1);
+                for (int j = tid; j < nJ; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, ps + 1, 0);
+                __syncthreads();
+                double* T = tdat + tused;
+#pragma unroll 1
+                for (int64_t e = tid; e < cntT; e += kSwThreads)
+                    T[e] = combine<KIND>(p, p0, rs[e % Rr], cs[e / Rr], wJ, L, nullptr, 0);
+                if (tid == 0) {
+                    ttab[2 * ps] = tused;
+                    ttab[2 * ps + 1] = cntT;
+                }
+                tused += cntT;
+            }
+        }
+        if (tid == 0) reinterpret_cast<int64_t*>(a.out)[10] = tused;
+    }
     if ((a.mode == 1 || a.fill) && status == 0) {
         // fillsitetensors!(tci, f) with the solve unobservable: updatemaxsample!(tci, Pi1) per site
         fstatus = 0;
@@ -825,12 +1108,11 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     for (int i = tid; i < npe; i += kSwThreads) reinterpret_cast<double*>(a.out + io.pe)[i] = pe[i];
     {
         int32_t* dst = reinterpret_cast<int32_t*>(a.out + io.sets);
-        for (int lb = 0; lb < (extra_valid ? 6 : 4); ++lb)
-            for (int s = 0; s < L; ++s) {
-                const int ne = set_cnt(lb & 1, lb >> 1, s) * width(lb, s);
-                sw_copy(dst, set_ptr(lb & 1, lb >> 1, s), ne);
-                dst += ne;
-            }
+        copy_segments(
+            (extra_valid ? 6 : 4) * L,
+            [&](int i) { const int lb = i / L; return set_cnt(lb & 1, lb >> 1, i % L) * width(lb, i % L); },
+            [&](int i, int) { const int lb = i / L; return (const int32_t*)set_ptr(lb & 1, lb >> 1, i % L); },
+            [&](int, int off) { return dst + off; });
     }
 }
 

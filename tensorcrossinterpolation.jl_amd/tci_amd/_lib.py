@@ -107,6 +107,7 @@ SIGNATURES = {
     "tci_tci2_get_sets": ([vp, C.c_int, vp, vp, i64], C.c_int),
     "tci_tci2_fill_maxsample": ([vp, vp, C.POINTER(C.c_int)], C.c_int),
     "tci_tci2_sweep2site_fill": ([vp, vp, i32, i32, dbl, i64, i32, i32, C.POINTER(C.c_int)], C.c_int),
+    "tci_tci2_sweep1site": ([vp, vp, i32, dbl, dbl, i64, i32, vp, i64, vp, C.POINTER(C.c_int)], C.c_int),
     "tci_set_sweep_small": ([vp, C.c_int], C.c_int),
     "tci_cache_create": ([vp, i32p, i32, i64, C.POINTER(vp)], C.c_int),
     "tci_cache_destroy": ([vp], C.c_int),

@@ -107,6 +107,11 @@ class TensorCI2:
             raise ValueError("localdims should have at least 2 elements!")
         n = len(localdims)
         self.localdims = localdims
+        # the index sets may live in the native object between native sweeps (_native_* below):
+        # _py_stale = the native copy is newer (pulled on first access), _native_dirty = the Python
+        # copy may have changed since the last push
+        self._py_stale = False
+        self._native_dirty = True
         self.Iset = [np.zeros((0, b), np.int32) for b in range(n)]
         self.Jset = [np.zeros((0, n - 1 - b), np.int32) for b in range(n)]
         self.sitetensors = [np.zeros((0, d, 0)) for d in localdims]
@@ -153,11 +158,34 @@ class TensorCI2:
         tci.invalidatesitetensors()
         return tci
 
+    # -- index sets (lazily synchronised with the native object)
+    def _sets_get(name):
+        def get(self):
+            if self._py_stale:
+                self._native_pull_sets()
+            self._native_dirty = True  # the caller may modify what it gets
+            return self.__dict__[name]
+
+        def put(self, v):
+            if self._py_stale:
+                self._native_pull_sets()
+            self.__dict__[name] = v
+            self._native_dirty = True
+        return property(get, put)
+
+    Iset = _sets_get("_Iset")
+    Jset = _sets_get("_Jset")
+    Iset_history = _sets_get("_Iset_history")
+    Jset_history = _sets_get("_Jset_history")
+    del _sets_get
+
     # -- basic accessors (tensorci2.jl:189-289)
     def __len__(self):
         return len(self.localdims)
 
     def linkdims(self):
+        if self._py_stale:  # the native object's counts: no pull of the sets themselves
+            return [int(c) for c in self._native_counts(0)[1:]]
         return [len(self.Iset[b + 1]) for b in range(len(self) - 1)]
 
     def rank(self):
@@ -271,6 +299,9 @@ class TensorCI2:
             raise ValueError(f"Unknown sweep direction {sweepdirection}: choose between :forward, :backward.")
         fwd = sweepdirection == "forward"
         L = len(self)
+        if NATIVE_SWEEP and _native_ok(f) and self._sweep1site_native(f, fwd, reltol, abstol, maxbonddim,
+                                                                        updatetensors):
+            return
         bonds = range(1, L) if fwd else range(L, 1, -1)
         for b in bonds:
             p = b - 1
@@ -346,6 +377,41 @@ class TensorCI2:
         if fillsitetensors:
             self.fillsitetensors(f, solve=not lazy_sitetensors)
 
+    def _native_handle(self, ctx):
+        h = getattr(self, "_native_h", None)
+        if h is None or getattr(self, "_native_ctx", None) is not ctx:
+            h = C.c_void_p()
+            ctx.check(ctx.lib.tci_tci2_create(ctx.h, len(self), np.ascontiguousarray(self.localdims, np.int32),
+                                              C.byref(h)))
+            self._native_h, self._native_ctx = h, ctx
+            self._native_owner = ctx.own(_NativeTCI2(ctx, h))
+        return h
+
+    def _sweep1site_native(self, f, fwd, reltol, abstol, maxbonddim, updatetensors):
+        """sweep1site! in one device launch (tci_tci2_sweep1site) when every bond fits the
+        one-workgroup rrLU; False (state untouched) when the host loop has to run it."""
+        ctx = f.ctx
+        lib = ctx.lib
+        n = len(self)
+        h = self._native_handle(ctx)
+        self._native_push(ctx, h)
+        cap = n * 16384 if updatetensors else 0  # each site's tensor fits the small path's LDS
+        tens = np.empty(max(cap, 1))
+        offs = np.zeros(2 * n, np.int64)
+        handled = C.c_int(0)
+        ctx.check(lib.tci_tci2_sweep1site(h, f.h, int(bool(fwd)), float(reltol), float(abstol),
+                                          int(min(maxbonddim, INT64_MAX)), int(bool(updatetensors)),
+                                          tens.ctypes.data_as(C.c_void_p), cap, offs.ctypes.data_as(C.c_void_p),
+                                          C.byref(handled)))
+        if not handled.value:
+            return False
+        self._native_pull(ctx, h)  # sweep1site! leaves the history alone (so does the kernel)
+        if updatetensors:
+            for p in range(n):
+                o, c = int(offs[2 * p]), int(offs[2 * p + 1])
+                self.setsitetensor_(p + 1, tens[o:o + c].copy())
+        return True
+
     def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
                            fill_maxsample=False):
         """The iterations in C++ / on the device (tci_tci2_sweep2site): the state goes in and comes
@@ -353,34 +419,8 @@ class TensorCI2:
         maxsample update was done natively too (fill_maxsample and tci_tci2_fill_maxsample handled it)."""
         ctx = f.ctx
         lib = ctx.lib
-        n = len(self)
-        h = getattr(self, "_native_h", None)
-        if h is None or getattr(self, "_native_ctx", None) is not ctx:
-            h = C.c_void_p()
-            ctx.check(lib.tci_tci2_create(ctx.h, n, np.ascontiguousarray(self.localdims, np.int32), C.byref(h)))
-            self._native_h, self._native_ctx = h, ctx
-            self._native_owner = ctx.own(_NativeTCI2(ctx, h))
-        widths = [list(range(n)), [n - 1 - p for p in range(n)]]
-
-        def push(which, sets):
-            counts = np.array([len(a) for a in sets], np.int64)
-            parts = [np.ascontiguousarray(a, np.int32).ravel() for a in sets]
-            packed = np.concatenate(parts) if parts else np.zeros(0, np.int32)
-            packed = np.ascontiguousarray(packed, np.int32)
-            ctx.check(lib.tci_tci2_set_sets(h, which, counts.ctypes.data_as(C.c_void_p),
-                                            packed.ctypes.data_as(C.c_void_p)))
-
-        push(0, self.Iset)
-        push(1, self.Jset)
-        if self.Iset_history:
-            push(2, self.Iset_history[-1])
-            push(3, self.Jset_history[-1])
-        else:
-            ctx.check(lib.tci_tci2_clear_history(h))
-        pe = np.ascontiguousarray(self.pivoterrors, np.float64)
-        ctx.check(lib.tci_tci2_set_errors(h, float(self.maxsamplevalue),
-                                          np.ascontiguousarray(self.bonderrors, np.float64).ctypes.data_as(C.c_void_p),
-                                          pe.ctypes.data_as(C.c_void_p), len(pe)))
+        h = self._native_handle(ctx)
+        self._native_push(ctx, h)
         strat = {"backandforth": 0, "forward": 1, "backward": 2}[sweepstrategy]
         handled = C.c_int(0)
         if fill_maxsample and niter > 0:
@@ -392,6 +432,63 @@ class TensorCI2:
                                               int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested))))
             if fill_maxsample:
                 ctx.check(lib.tci_tci2_fill_maxsample(h, f.h, C.byref(handled)))
+        if niter > 0:
+            self._native_has_hist = True  # every iteration starts a history
+        self._native_pull(ctx, h)
+        return bool(handled.value)
+
+    def _native_counts(self, which):
+        ctx = self._native_ctx
+        counts = np.zeros(len(self), np.int64)
+        ctx.check(ctx.lib.tci_tci2_get_sets(self._native_h, which, counts.ctypes.data_as(C.c_void_p), None, 0))
+        return counts
+
+    def _native_push(self, ctx, h):
+        """The state into the native object, bank by bank (the sets only when the Python copy may
+        have changed since the native object last had them)."""
+        lib = ctx.lib
+        if not self._native_dirty and getattr(self, "_native_synced_h", None) is h:
+            self._native_push_errors(ctx, h)
+            return
+
+        def push(which, sets):
+            counts = np.array([len(a) for a in sets], np.int64)
+            parts = [np.ascontiguousarray(a, np.int32).ravel() for a in sets]
+            packed = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+            packed = np.ascontiguousarray(packed, np.int32)
+            ctx.check(lib.tci_tci2_set_sets(h, which, counts.ctypes.data_as(C.c_void_p),
+                                            packed.ctypes.data_as(C.c_void_p)))
+
+        push(0, self._Iset)
+        push(1, self._Jset)
+        if self._Iset_history:
+            push(2, self._Iset_history[-1])
+            push(3, self._Jset_history[-1])
+        else:
+            ctx.check(lib.tci_tci2_clear_history(h))
+        self._native_has_hist = bool(self._Iset_history)
+        self._native_dirty = False
+        self._native_synced_h = h
+        self._native_push_errors(ctx, h)
+
+    def _native_push_errors(self, ctx, h):
+        lib = ctx.lib
+        pe = np.ascontiguousarray(self.pivoterrors, np.float64)
+        ctx.check(lib.tci_tci2_set_errors(h, float(self.maxsamplevalue),
+                                          np.ascontiguousarray(self.bonderrors, np.float64).ctypes.data_as(C.c_void_p),
+                                          pe.ctypes.data_as(C.c_void_p), len(pe)))
+
+    def _native_pull(self, ctx, h):
+        """After a native sweep: errors and maxsamplevalue now; the sets when first read."""
+        self._py_stale = True
+        self._native_dirty = False
+        self._native_pull_errors(ctx, h)
+
+    def _native_pull_sets(self):
+        ctx, h = self._native_ctx, self._native_h
+        lib = ctx.lib
+        n = len(self)
+        widths = [list(range(n)), [n - 1 - p for p in range(n)]]
 
         def pull(which):
             counts = np.zeros(n, np.int64)
@@ -408,10 +505,17 @@ class TensorCI2:
                 o += k
             return out
 
-        self.Iset = pull(0)
-        self.Jset = pull(1)
-        self.Iset_history = [pull(2)]
-        self.Jset_history = [pull(3)]
+        d = self.__dict__
+        d["_Iset"], d["_Jset"] = pull(0), pull(1)
+        if self._native_has_hist:
+            d["_Iset_history"], d["_Jset_history"] = [pull(2)], [pull(3)]
+        else:
+            d["_Iset_history"], d["_Jset_history"] = [], []
+        self._py_stale = False
+
+    def _native_pull_errors(self, ctx, h):
+        lib = ctx.lib
+        n = len(self)
         ms, npe = C.c_double(), C.c_int64()
         be = np.zeros(n - 1)
         pe = np.zeros(2048 + 1)
@@ -424,7 +528,6 @@ class TensorCI2:
         self.maxsamplevalue = ms.value
         self.bonderrors = be
         self.pivoterrors = pe[: npe.value].copy()
-        return bool(handled.value)
 
     def optimize(self, f, tolerance=None, pivottolerance=None, maxbonddim=INT64_MAX, maxiter=20,
                  sweepstrategy="backandforth", pivotsearch="full", verbosity=0, loginterval=10,

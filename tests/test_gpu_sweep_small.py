@@ -169,3 +169,34 @@ def test_bulk_set_transfer_roundtrip():
                                             out.ctypes.data_as(C.c_void_p), 3))
     finally:
         lib.tci_tci2_destroy(h)
+
+
+@pytest.mark.parametrize("name", ["lorentz", "qosc40", "table", "lorentz_maxbond"])
+@pytest.mark.parametrize("direction,tensors", [("forward", True), ("backward", True), ("backward", False)])
+def test_device_sweep1site_equals_host_loop(name, direction, tensors):
+    """sweep1site! (tensorci2.jl:659-725) in one launch (tci_tci2_sweep1site) against the host loop
+    (one tci_update_pivots_h per bond): sets, bond / pivot errors, maxsamplevalue and the site
+    tensors (MatrixLUCI left / right factors and the last site's Pi1) bit for bit, with the
+    history untouched."""
+    ctx = T.context(0)
+    mk, ld, kw = CASES[name]
+    f = mk(ctx)
+    kw = dict(kw, maxiter=2)
+    kw.pop("sweepstrategy", None)
+    base, _, _ = T.crossinterpolate2(f, ld, [T.optfirstpivot(f, ld)], nsearchglobalpivot=0, **kw)
+    out = []
+    for small in (True, False):
+        t = TT.TensorCI2.from_sets(f, ld, [s.copy() for s in base.Iset], [s.copy() for s in base.Jset])
+        t.Iset_history = [[s.copy() for s in base.Iset_history[-1]]]
+        t.Jset_history = [[s.copy() for s in base.Jset_history[-1]]]
+        t.maxsamplevalue = base.maxsamplevalue
+        t.bonderrors = base.bonderrors.copy()
+        ctx.check(ctx.lib.tci_set_sweep_small(ctx.h, int(small)))
+        try:
+            t.sweep1site(f, direction, abstol=1e-9 * base.maxsamplevalue, maxbonddim=kw.get("maxbonddim", TT.INT64_MAX),
+                         updatetensors=tensors)
+        finally:
+            ctx.check(ctx.lib.tci_set_sweep_small(ctx.h, 1))
+        out.append(t)
+    _same(out[0], out[1])
+    assert all(np.array_equal(a, b) for a, b in zip(out[0].Iset_history[-1], base.Iset_history[-1]))
