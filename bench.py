@@ -156,10 +156,14 @@ def main():
     ro_ms, ro_launches = ctx.kernel_stats(2)
     rf_ms, rf_launches = ctx.kernel_stats(23)
     by_pending = {}  # read-only pass time by pending depth P (sub-families 3 + P)
+    by_pending_ext = {}  # the same in the later shadow epochs of an exact epoch (EXT passes, 24 + P)
     for P in range(1, args.nb):
         pm, pn = ctx.kernel_stats(3 + P)
         if pn:
             by_pending[P] = round(pm / pn, 5)
+        pm, pn = ctx.kernel_stats(24 + P)
+        if pn:
+            by_pending_ext[P] = round(pm / pn, 5)
     ctx.set_timing(False)
     # the benchmarked factorisation once more with permutations and pivot errors, for the parity
     # check against the CPU runs on the same matrix (rank 0 factorises the seed-0 matrix)
@@ -207,7 +211,8 @@ def main():
              "read_only_pass": {"launches": ro_launches, "avg_ms": round(ro_ms / max(ro_launches, 1), 5),
                                 "GBps": round(ro_b / max(ro_n, 1) / (ro_ms / max(ro_launches, 1) * 1e-3) / 1e9, 1)
                                 if ro_launches else None,
-                                "avg_ms_by_pending_depth": by_pending},
+                                "avg_ms_by_pending_depth": by_pending,
+                                "avg_ms_by_pending_depth_ext": by_pending_ext},
              "refresh_pass": {"launches": rf_launches, "avg_ms": round(rf_ms / max(rf_launches, 1), 5),
                               "GBps": round(rf_b / max(rf_n, 1) / (rf_ms / max(rf_launches, 1) * 1e-3) / 1e9, 1)
                               if rf_launches else None},
@@ -675,7 +680,7 @@ def dense_extras(T, ctx, only_k3=False):
         Pi1.fill_uniform(seed=7)
         Tm = T.DeviceMatrix(R, r, ctx=ctx, ld=R)
         rec = {"r": r, "R": R}
-        for tag, mask in (("mfma", 7), ("round1_scalar", 0), ("mfma_getrs_only", 4)):
+        for tag, mask in (("mfma", 15), ("mfma_lds_panel", 7), ("round1_scalar", 0), ("mfma_getrs_only", 4)):
             ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
             P.copy_from(P0)
             T.sitetensor_solve_device(P, Pi1, Tm)
@@ -689,7 +694,7 @@ def dense_extras(T, ctx, only_k3=False):
             fl = 2.0 / 3.0 * r ** 3 + 2.0 * R * r * r
             rec[tag] = {"ms": round(sec * 1e3, 3), "TFLOPs": round(fl / sec / 1e12, 2),
                         "frac_of_spec": round(fl / sec / 1e12 / MFMA_F64_SPEC_TFLOPS, 4)}
-        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 7))
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
         solves.append(rec)
         for x in (P0, P, Pi1, Tm):
             x.free()
@@ -704,14 +709,14 @@ def dense_extras(T, ctx, only_k3=False):
         # GEMM with K = np over the full np x n (or m x np) block + TRSM m np^2 (or n np^2)
         fl = 2.0 * npv * npv * 8192 + 1.0 * (8192 - npv) * npv * npv
         rec = {"m": 8192, "n": 8192, "np": npv, "leftorthogonal": lo}
-        for tag, mask in (("mfma", 7), ("round1_scalar", 0)):
+        for tag, mask in (("mfma", 15), ("round1_scalar", 0)):
             ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
             ctx.set_timing(True)
             T.MatrixLUCI(Ah, maxrank=npv, leftorthogonal=lo, ctx=ctx).left()
             kms, kn = ctx.kernel_stats(21)
             ctx.set_timing(False)
             rec[tag] = {"ms": round(kms / max(kn, 1), 3), "TFLOPs": round(fl / (kms / max(kn, 1) * 1e-3) / 1e12, 2)}
-        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 7))
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
         lucis.append(rec)
     out["luci_factors_k4"] = lucis
     return out

@@ -84,9 +84,10 @@ int tci_ctx_synchronize(tci_ctx* ctx);
  * measured with hipEvents on the context stream: family 0 = rrLU pass that writes the Schur
  * update back, 2 = rrLU read-only pass (pending updates applied on the fly + argmax),
  * 1 = batch evaluation; 3 + P (P = 1..16) = the read-only passes that applied P pending updates
- * (a breakdown of family 2); 20 = site-tensor solve (getrf + getrs of P^T), 21 = MatrixLUCI
- * factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d, 23 = rrLU refresh
- * passes (read-only passes that also rewrite the fp16 shadow, two-level epoch). */
+ * in the first shadow epoch after a write-back, 24 + P the same in the later shadow epochs of
+ * the exact epoch (a breakdown of family 2); 20 = site-tensor solve (getrf + getrs of P^T),
+ * 21 = MatrixLUCI factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d, 23 =
+ * rrLU refresh passes (read-only passes that also rewrite the fp16 shadow, two-level epoch). */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
@@ -124,8 +125,10 @@ int tci_rrlu_shadow_bytes(void);
 int tci_set_c128_shadow(tci_ctx* ctx, int enabled);
 
 /* fp64 MFMA forms of the MatrixLUCI factors (bit 1), the site-tensor getrf
- * (bit 2) and getrs (bit 4); default 7 (env TCI_DENSE_MFMA). 0 restores the round-1 scalar
- * kernels (A/B). Factors / solutions agree to the parity tolerances either way. */
+ * (bit 2) and getrs (bit 4), and the getrf's panels held in registers (bit 8; without it the
+ * panels are factorised in LDS -- bitwise the same factors); default 15 (env TCI_DENSE_MFMA). 0
+ * restores the round-1 scalar kernels (A/B). Factors / solutions agree to the parity tolerances
+ * either way. */
 int tci_set_dense_mfma(tci_ctx* ctx, int mask);
 
 /* ------------------------------------------------------------ integrands */

@@ -152,7 +152,9 @@ struct tci_ctx {
         size_t idx;
     };
     std::vector<EvPair> evpairs;
-    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 4;  // + 20 solve, 21 LUCI factors, 22 K3, 23 refresh
+    // + 20 solve, 21 LUCI factors, 22 K3, 23 refresh, 24 + P read-only passes of a later shadow epoch
+    // (EXT: the exact epoch is longer; 3 + P: the first shadow epoch after a write-back)
+    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 4 + tci::kMaxPend + 1;
     double fam_ms[kFams] = {};
     int64_t fam_n[kFams] = {};
 };
@@ -539,7 +541,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
             g.selk = !last ? (int)(kk + 1) : -1;
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
-            ev_begin(c, flush ? 0 : refresh ? 23 : 2, sampled, flush || refresh ? -1 : 3 + PS);
+            ev_begin(c, flush ? 0 : refresh ? 23 : 2, sampled, flush || refresh ? -1 : (PE > PS ? 24 : 3) + PS);
             tci::launch_pass(c->stream, PE, flush, shadow, g, grid, flush ? 1 : refresh ? 2 : 0);
             ev_end(c, sampled);
             if (flush) te = ts = kk + 1;

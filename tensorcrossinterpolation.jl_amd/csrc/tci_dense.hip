@@ -449,6 +449,187 @@ __global__ __launch_bounds__(1024) void k_getrf_panel(double* __restrict__ A, in
     }
 }
 
+// The same panel factorisation with the panel in REGISTERS (rows <= 1024 RPT): thread t owns rows
+// t + 1024 u, u < RPT, and their NBP values. Per column c: the thread's first maximal |a| over its
+// rows >= c, a DPP + readlane wave argmax, the 16 wave results through LDS (barrier 1), then the
+// owners of rows p and c publish their whole panel rows (barrier 2) and swap them in registers,
+// and every thread scales its rows > c and applies the rank-1 update with the pivot row read as
+// LDS broadcasts, taking column c + 1's argmax partial on the way. Same arithmetic as
+// k_getrf_panel (true division, separate multiply and subtract, the same pivot rule): bitwise the
+// same factors, without its per-update LDS round trips.
+template <int CTRL>
+__device__ __forceinline__ void dpp_take_max(double& bv, int& bi) {
+    const uint64_t b = (uint64_t)__double_as_longlong(bv);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    const double ov = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    const int oi = __builtin_amdgcn_update_dpp(0, bi, CTRL, 0xf, 0xf, false);
+    if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+    }
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// every lane ends with the wave's (first) maximum; -1 / INT_MAX when no lane has a candidate
+__device__ __forceinline__ void wave_argmax(double& bv, int& bi) {
+    dpp_take_max<0xb1>(bv, bi);   // quad_perm [1,0,3,2]
+    dpp_take_max<0x4e>(bv, bi);   // quad_perm [2,3,0,1]
+    dpp_take_max<0x141>(bv, bi);  // row_half_mirror
+    dpp_take_max<0x140>(bv, bi);  // row_mirror: every lane of a 16-lane row has the row's best
+    double v = readlane_d(bv, 0);
+    int i = __builtin_amdgcn_readlane(bi, 0);
+#pragma unroll
+    for (int rr = 16; rr < 64; rr += 16) {
+        const double ov = readlane_d(bv, rr);
+        const int oi = __builtin_amdgcn_readlane(bi, rr);
+        if (ov > v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+    bv = v;
+    bi = i;
+}
+
+constexpr int kRegPanelThreads = 1024;
+
+template <int NBP, int RPT>
+struct RegPanel {  // one thread's state (the column steps are unrolled by recursion: every index of v
+    double v[RPT][NBP];  // is a constant, so v lives in registers)
+    double bv;
+    int bi;
+    int tid, rows, nbp, jb;
+    int* piv;
+    double* sv;
+    int* si;
+    double* prow;
+    double* crow;
+};
+
+template <int NBP, int RPT, int C>
+__device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
+    if constexpr (C < NBP) {
+        constexpr int NT = kRegPanelThreads, NW = NT / 64;
+        if (C < S.nbp) {
+            const int tid = S.tid;
+            wave_argmax(S.bv, S.bi);
+            if ((tid & 63) == 0) { S.sv[tid >> 6] = S.bv; S.si[tid >> 6] = S.bi; }
+            __syncthreads();  // barrier 1
+            double b = S.sv[0];
+            int p = S.si[0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) {
+                const double ov = S.sv[w];
+                const int oi = S.si[w];
+                if (ov > b || (ov == b && oi < p)) { b = ov; p = oi; }
+            }
+            if (p == 0x7fffffff) p = C;
+            if (tid == 0) S.piv[S.jb + C] = S.jb + p;
+            // the owners of rows p and C publish their panel rows
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int i = tid + u * NT;
+                if (i == p) {
+#pragma unroll
+                    for (int cc = 0; cc < NBP; ++cc) S.prow[cc] = S.v[u][cc];
+                }
+                if (i == C && p != C) {
+#pragma unroll
+                    for (int cc = 0; cc < NBP; ++cc) S.crow[cc] = S.v[u][cc];
+                }
+            }
+            __syncthreads();  // barrier 2
+            if (p != C) {
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const int i = tid + u * NT;
+                    if (i == C) {
+#pragma unroll
+                        for (int cc = 0; cc < NBP; ++cc) S.v[u][cc] = S.prow[cc];
+                    } else if (i == p) {
+#pragma unroll
+                        for (int cc = 0; cc < NBP; ++cc) S.v[u][cc] = S.crow[cc];
+                    }
+                }
+            }
+            const double d = S.prow[C];
+            S.bv = -1.0;
+            S.bi = 0x7fffffff;
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int i = tid + u * NT;
+                if (i > C && i < S.rows) {
+                    const double l = S.v[u][C] / d;
+                    S.v[u][C] = l;
+#pragma unroll
+                    for (int cc = C + 1; cc < NBP; ++cc) S.v[u][cc] = __dsub_rn(S.v[u][cc], __dmul_rn(l, S.prow[cc]));
+                    if constexpr (C + 1 < NBP) {
+                        if (C + 1 < S.nbp) {
+                            const double a = fabs(S.v[u][C + 1]);
+                            if (a > S.bv) { S.bv = a; S.bi = i; }
+                        }
+                    }
+                }
+            }
+        }
+        reg_panel_col<NBP, RPT, C + 1>(S);
+    }
+}
+
+template <int NBP, int RPT>
+__global__ __launch_bounds__(kRegPanelThreads) void k_getrf_panel_reg(double* __restrict__ A, int r, int jb,
+                                                                      int nbp, int* __restrict__ piv) {
+    constexpr int NT = kRegPanelThreads, NW = NT / 64;
+    __shared__ double sv[NW];
+    __shared__ int si[NW];
+    __shared__ double prow[NBP], crow[NBP];
+    RegPanel<NBP, RPT> S;
+    S.tid = threadIdx.x;
+    S.rows = r - jb;
+    S.nbp = nbp;
+    S.jb = jb;
+    S.piv = piv;
+    S.sv = sv;
+    S.si = si;
+    S.prow = prow;
+    S.crow = crow;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int i = S.tid + u * NT;
+#pragma unroll
+        for (int c = 0; c < NBP; ++c)
+            S.v[u][c] = (i < S.rows && c < nbp) ? A[(int64_t)(jb + i) + (int64_t)(jb + c) * r] : 0.0;
+    }
+    // column 0's partial: ascending rows, strict '>' (first maximum)
+    S.bv = -1.0;
+    S.bi = 0x7fffffff;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int i = S.tid + u * NT;
+        if (i < S.rows) {
+            const double a = fabs(S.v[u][0]);
+            if (a > S.bv) { S.bv = a; S.bi = i; }
+        }
+    }
+    reg_panel_col<NBP, RPT, 0>(S);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int i = S.tid + u * NT;
+        if (i < S.rows) {
+#pragma unroll
+            for (int c = 0; c < NBP; ++c)
+                if (c < nbp) A[(int64_t)(jb + i) + (int64_t)(jb + c) * r] = S.v[u][c];
+        }
+    }
+}
+
 // The panel's interchanges applied to every column outside it (laswp). They compose to a
 // permutation of at most 2 nbp rows (the panel's and the rows swapped into it), computed once per
 // workgroup in LDS: every thread (one per column) then moves its column's affected values with
@@ -511,15 +692,25 @@ static int panel_width(int rows) {
 
 bool getrf_blocked_fits(int r) { return (int64_t)r * 4 * 8 <= kPanelLds; }
 
-void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv) {
+void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv, bool reg) {
     hipLaunchKernelGGL(k_transpose_sq, dim3(std::min(2048, std::max(1, (r * r + 255) / 256))), dim3(256), 0, s,
                        A, r);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_getrf_panel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         kPanelLds);
+    // panels in registers (k_getrf_panel_reg) unless the context's dense mask drops kDenseGetrfReg
     for (int jb = 0; jb < r;) {
         const int rows = r - jb;
-        const int nbp = std::min(panel_width(rows), rows);
-        hipLaunchKernelGGL(k_getrf_panel, dim3(1), dim3(1024), (size_t)rows * nbp * 8, s, A, r, jb, nbp, piv);
+        int nbp;
+        if (reg && rows <= kRegPanelThreads) {
+            nbp = std::min(24, rows);
+            hipLaunchKernelGGL((k_getrf_panel_reg<24, 1>), dim3(1), dim3(kRegPanelThreads), 0, s, A, r, jb, nbp, piv);
+        } else if (reg && rows <= 2 * kRegPanelThreads) {
+            nbp = std::min(16, rows);
+            hipLaunchKernelGGL((k_getrf_panel_reg<16, 2>), dim3(1), dim3(kRegPanelThreads), 0, s, A, r, jb, nbp, piv);
+        } else {
+            nbp = std::min(panel_width(rows), rows);
+            hipLaunchKernelGGL(k_getrf_panel, dim3(1), dim3(1024), (size_t)rows * nbp * 8, s, A, r, jb, nbp, piv);
+        }
         const int je = jb + nbp, nother = r - nbp;
         if (nother > 0) {
             const dim3 g((nother + 255) / 256), b(256);

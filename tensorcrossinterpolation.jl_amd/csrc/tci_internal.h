@@ -298,7 +298,7 @@ void launch_cache_rehash(hipStream_t s, const unsigned long long* ok, const doub
 // columns >= np (otherwise) are overwritten by the triangular solve.
 // dense: bit mask of the fp64 MFMA forms (tci_dense.hip) to use, kDense* below; 0 = the
 // round-1 scalar GEMMs / LDS TRSMs / single-workgroup getrf (kept for A/B)
-constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseAll = 7;
+constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseGetrfReg = 8, kDenseAll = 15;
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
                          const int64_t* colperm, double* left, double* right, int dense);

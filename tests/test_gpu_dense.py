@@ -89,6 +89,32 @@ def test_sitetensor_solve_mfma(ctx, r, R):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("r,R", [(1024, 256), (1500, 64), (97, 300), (24, 50), (2100, 16)])
+def test_getrf_register_panel_bitwise(ctx, r, R):
+    """The getrf panels held in registers (k_getrf_panel_reg, dense mask bit 8) against the LDS panel
+    kernel (mask 7) and the oracle. Inside a panel both do the same arithmetic (true division,
+    separate multiply and subtract, the first maximal |a| pivot), but the panel widths differ (24 /
+    16 in registers, 16-64 in LDS), so the K3 trailing updates sum in a different blocking: equal to
+    rounding, both within the parity tolerance of the oracle. r = 1500 runs two rows per thread,
+    r = 2100 the LDS form for its first panels."""
+    rng = np.random.default_rng(r + 7 * R)
+    P = rng.random((r, r)) + 0.5 * np.sqrt(r) * np.eye(r) * rng.choice([-1, 1], r)
+    Pi1 = rng.random((R, r))
+    out = {}
+    try:
+        for mask in (15, 7):
+            ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+            dP, dPi1, dT = _dev(ctx, P, True), _dev(ctx, Pi1, True), T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+            T.sitetensor_solve_device(dP, dPi1, dT)
+            out[mask] = dT.to_host()
+    finally:
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
+    ref = O.sitetensor_solve(P, Pi1).reshape((R, r), order="F")
+    np.testing.assert_allclose(out[15], out[7], rtol=1e-11, atol=1e-13 * np.abs(ref).max())
+    np.testing.assert_allclose(out[15], ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("np_", [256, 1024])
 @pytest.mark.parametrize("leftorth", [True, False])
 def test_luci_factors_mfma(ctx, np_, leftorth):
