@@ -559,7 +559,11 @@ __device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
                     }
                 }
             }
-            const double d = S.prow[C];
+            // the pivot row: one LDS read per wave (lane cc holds column cc), then wave-uniform
+            // operands by readlane -- LDS broadcasts of every element cost LDS bandwidth per wave
+            const int lane = tid & 63;
+            const double pw = lane < NBP ? S.prow[lane < NBP ? lane : 0] : 0.0;
+            const double d = readlane_d(pw, C);
             S.bv = -1.0;
             S.bi = 0x7fffffff;
 #pragma unroll
@@ -569,7 +573,8 @@ __device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
                     const double l = S.v[u][C] / d;
                     S.v[u][C] = l;
 #pragma unroll
-                    for (int cc = C + 1; cc < NBP; ++cc) S.v[u][cc] = __dsub_rn(S.v[u][cc], __dmul_rn(l, S.prow[cc]));
+                    for (int cc = C + 1; cc < NBP; ++cc)
+                        S.v[u][cc] = __dsub_rn(S.v[u][cc], __dmul_rn(l, readlane_d(pw, cc)));
                     if constexpr (C + 1 < NBP) {
                         if (C + 1 < S.nbp) {
                             const double a = fabs(S.v[u][C + 1]);
@@ -648,8 +653,11 @@ __global__ __launch_bounds__(256) void k_getrf_swap(double* __restrict__ A, int 
         int pos0 = l < nbp ? jb + l : -1, src0 = pos0;
         int pos1 = -1, src1 = -1;
         int n = nbp;
+        // every interchange loaded at once (lane k holds piv[jb + k]), read back by readlane: a load
+        // per step inside the loop was a dependent round trip per interchange (~1 us each)
+        const int pl = l < nbp ? piv[jb + l] : 0;
         for (int k = 0; k < nbp; ++k) {
-            const int p = piv[jb + k];
+            const int p = __builtin_amdgcn_readlane(pl, k);
             const unsigned long long b0 = __ballot(pos0 == p), b1 = __ballot(pos1 == p);
             int qp;
             if (b0) qp = __ffsll((long long)b0) - 1;

@@ -1149,6 +1149,10 @@ static_assert(kMfBlk == 4, "a lane's 16 loaded rows are 4 blocks of 4");
 // fragments fit.
 constexpr int kMfMaxP = 15;
 constexpr int kMfExCap = 128;                         // deferred examinations per wave
+#ifndef TCI_EXB
+#define TCI_EXB 4
+#endif
+constexpr int kExB = TCI_EXB;  // final examinations with pending y's in memory: updates in flight
 static_assert(3 * kMfMaxP <= 64 && kMfMaxP < kMaxPend, "two MFMA K-steps per tile");
 
 template <int P, bool EXT = false>
@@ -1476,17 +1480,18 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             if (rp <= k) continue;
             if constexpr (decltype(fast)::value) {
                 if constexpr (Gm::ymem) {
-                    // x's and y's from memory, four pending updates in flight at a time
-                    for (int s0 = 0; s0 < PE - 1; s0 += 4) {
-                        double xv[4], yv[4];
+                    // x's and y's from memory, kExB pending updates in flight at a time (the
+                    // streaming registers are dead here): at PE = 30 two round trips, not eight
+                    for (int s0 = 0; s0 < PE - 1; s0 += kExB) {
+                        double xv[kExB], yv[kExB];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
+                        for (int i = 0; i < kExB; ++i)
                             if (s0 + i < PE - 1) {
                                 xv[i] = g.X[(int64_t)(s0 + i) * ldx + r];
                                 yv[i] = g.Y[(int64_t)(s0 + i) * ldy + j];
                             }
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
+                        for (int i = 0; i < kExB; ++i)
                             if (s0 + i < PE - 1) v = __dsub_rn(v, __dmul_rn(xv[i], yv[i]));
                     }
                 } else {
