@@ -559,11 +559,7 @@ __device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
                     }
                 }
             }
-            // the pivot row: one LDS read per wave (lane cc holds column cc), then wave-uniform
-            // operands by readlane -- LDS broadcasts of every element cost LDS bandwidth per wave
-            const int lane = tid & 63;
-            const double pw = lane < NBP ? S.prow[lane < NBP ? lane : 0] : 0.0;
-            const double d = readlane_d(pw, C);
+            const double d = S.prow[C];
             S.bv = -1.0;
             S.bi = 0x7fffffff;
 #pragma unroll
@@ -573,8 +569,7 @@ __device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
                     const double l = S.v[u][C] / d;
                     S.v[u][C] = l;
 #pragma unroll
-                    for (int cc = C + 1; cc < NBP; ++cc)
-                        S.v[u][cc] = __dsub_rn(S.v[u][cc], __dmul_rn(l, readlane_d(pw, cc)));
+                    for (int cc = C + 1; cc < NBP; ++cc) S.v[u][cc] = __dsub_rn(S.v[u][cc], __dmul_rn(l, S.prow[cc]));
                     if constexpr (C + 1 < NBP) {
                         if (C + 1 < S.nbp) {
                             const double a = fabs(S.v[u][C + 1]);
