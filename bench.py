@@ -96,8 +96,9 @@ def main():
     ap.add_argument("--nb", type=int, default=int(os.environ.get("TCI_RRLU_NB", "10")),
                     help="shadow epoch of the rrLU: pending updates before the shadow is rewritten "
                          "(results are identical for every nb)")
-    ap.add_argument("--epochs", type=int, default=int(os.environ.get("TCI_RRLU_EPOCHS", "3")),
-                    help="shadow epochs per fp64 write-back (two-level epoch; identical results)")
+    ap.add_argument("--epochs", type=int, default=int(os.environ.get("TCI_RRLU_EPOCHS", "0")),
+                    help="shadow epochs per fp64 write-back (two-level epoch; identical results; "
+                         "0 = the library's choice by shape)")
     ap.add_argument("--no-shadow", action="store_true",
                     help="exact fp64 read-only passes instead of the certified fp16 shadow search")
     args = ap.parse_args()
@@ -117,6 +118,7 @@ def main():
     ctx = T.context(int(os.environ.get("TCI_BENCH_DEVICE", local_rank)))
     ctx.check(ctx.lib.tci_set_rrlu_flush(ctx.h, args.nb))
     ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, args.epochs))
+    args.epochs = ctx.lib.tci_rrlu_epochs_for(ctx.h, args.m, args.n)  # the value the factorisation uses
     shadow = not args.no_shadow and os.environ.get("TCI_RRLU_SHADOW", "1") != "0"
     ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, int(shadow)))
     m, n, r = args.m, args.n, args.r

@@ -49,6 +49,9 @@ extern "C" {
 #define TCI_F_MPO 9      /* Contraction(A, B) of two 4-leg tensor trains (contraction.jl:60-575)  */
 #define TCI_F_HOST 10    /* the user's own f / BatchEvaluator, evaluated on the host by a callback
                             (tci_func_create_host; batcheval.jl:131-214, 247-308)               */
+#define TCI_F_C128 11    /* a ComplexF64 integrand as sums of real ones, Re f = sum of parts, Im f
+                            = sum of parts (tci_func_create_c128; Contraction{ComplexF64},
+                            contraction.jl:60-152)                                              */
 /* GAUSSMIX, CP and MPO are sums of K separable terms: Pi is assembled as a rank-K fp64 MFMA GEMM
  * (MPO: K = ra*rb at the cut, the factor rows are the left / right environments).
  * MPO params: [N, per site t (ra, d1, d2, ra', rb, d3, rb', offA, offB), cores]: A_t is
@@ -98,8 +101,10 @@ int tci_set_timing(tci_ctx* ctx, int enabled);
  * fp64 values. Results are bitwise identical for every nb and epochs. */
 int tci_set_rrlu_flush(tci_ctx* ctx, int nb);
 /* Shadow epochs per fp64 write-back (two-level epoch; 1..32 with nb * epochs <= 32;
- * default 3, env TCI_RRLU_EPOCHS; 1 = write back every nb pivots). */
+ * 1 = write back every nb pivots; 0, the default, = by shape: 3 on trailing blocks of >= 2.4e7
+ * elements, else 1; env TCI_RRLU_EPOCHS). tci_rrlu_epochs_for: the value an m x n rrLU will use. */
 int tci_set_rrlu_epochs(tci_ctx* ctx, int epochs);
+int tci_rrlu_epochs_for(tci_ctx* ctx, int64_t m, int64_t n);
 /* Matrices with m*n <= 16384 and m + n <= 4096 are factorised by one workgroup holding the whole
  * matrix in LDS (one launch instead of one per pivot); enabled = 0 forces the pass pipeline.
  * Both paths give bitwise identical results. Default on (env TCI_RRLU_SMALL=0: off). */
@@ -152,6 +157,16 @@ typedef int (*tci_host_fn)(void* user, const int32_t* I, int64_t m, int32_t nl, 
                            int64_t n, int32_t nr, int32_t M, double* out, int64_t ldo);
 int tci_func_create_host(tci_ctx* ctx, tci_host_fn fn, void* user, const int32_t* localdims,
                          int32_t L, tci_func** out);
+
+/* A ComplexF64 integrand from real ones: f(x) = sum_{i<nre} re[i](x) + im * sum_{i<nim} im[i](x)
+ * (the sums in part order). Used for Contraction{ComplexF64} (contraction.jl:60-152): with both
+ * complex MPOs realified (each entry a 2x2 real block, bonds doubled; A_re, A_im the real MPOs of
+ * Re A, Im A), Re(A B) = A_re B_re + A_im (-B_im) and Im(A B) = A_im B_re + A_re B_im: four real
+ * TCI_F_MPO parts, each an fp64 MFMA GEMM. The parts must outlive f and share its localdims. Only the ComplexF64
+ * entries accept it (tci_batcheval_c128_h, tci_update_pivots_c128_h; the real ones return
+ * TCI_ERR_ARG). */
+int tci_func_create_c128(tci_ctx* ctx, const tci_func* const* re, int32_t nre,
+                         const tci_func* const* im, int32_t nim, tci_func** out);
 
 /* ----------------------------------------------------------- batch eval
  * Replaces _batchevaluate_dispatch (batcheval.jl:131-175) plus maxabs (util.jl:34-43) as used by

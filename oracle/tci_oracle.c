@@ -275,11 +275,164 @@ double orc_feval(int kind, const double* p, i64 np, const i32* localdims, int L,
     return feval(&f, x);
 }
 
+#ifdef ORC_FAST
+/* ------------------------------------------------------------------ fast mode
+ * liboracle_fast.so (oracle/Makefile: -DORC_FAST -fopenmp, with cpu_rrlu_omp.c) exists for the
+ * one config whose loop-for-loop restatement would take the CPU many hours: config 5 as stated
+ * (12 legs of d = 32, CP rank 1024, maxbonddim 1024; Pi up to 32768^2). It changes three things
+ * and nothing else:
+ *  1. rrlu runs on cpu_rrlu_inplace_omp, bitwise equal to orc_rrlu_inplace
+ *     (tests/test_oracle_kats.py::test_omp_baseline_bitwise_equals_oracle);
+ *  2. the CP integrand is evaluated factorised at the bond: f(x) = sum_k EL[k, R] * ER[k, j] with
+ *     EL = prod of g over the row legs (and the centre leg) in leg order, ER the same over the
+ *     column legs, k ascending, one multiply and one add per term -- the same function, another
+ *     association of its product (the product path evaluates it the same way, EL^T ER on fp64
+ *     MFMA, so f is compared at tolerance, as for every transcendental/separable kind);
+ *  3. setsitetensor! fills Pi1 (it updates maxsample, tensorci2.jl:610) and checks the pivot
+ *     matrix is square, but skips the solve: in deterministic mode the solved tensors are never
+ *     read -- the final sweep1site!(updatetensors) overwrites every site tensor
+ *     (tensorci2.jl:683-716) before anything evaluates the tensor train.
+ * The MatrixLUCI factors run their rows / columns in parallel (each entry's arithmetic unchanged). */
+#include <omp.h>
+int cpu_rrlu_inplace_omp(double* A, i64 m, i64 n, i64 lda, i64 maxrank, double reltol,
+                         double abstol, int leftorth, i64* rowperm, i64* colperm, i64* npivot,
+                         double* err, i64 pivot_limit);
+
+typedef double v4d __attribute__((vector_size(32)));
+enum { CP_MR = 8, CP_NR = 4, CP_KC = 256 };
+
+/* E[k * ld + R] = prod of g[k][t0 + q][e_q - 1] over q (and the centre leg), in leg order */
+static void cp_factors(const orc_func* f, const i32* T, i64 cnt_rows, int cnt, int M, i64 D,
+                       int t0, double* E, i64 ld) {
+    const double* p = f->p;
+    const int L = f->L, K = (int)p[0], dmax = (int)p[1];
+    const double* g0 = p + 2;
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < K; ++k) {
+        const double* g = g0 + (i64)k * L * dmax;
+        for (i64 R = 0; R < cnt_rows * D; ++R) {
+            const i64 i = R % cnt_rows, c = R / cnt_rows;
+            const i32* e = T + i * cnt;
+            double prod = 1.0;
+            for (int q = 0; q < cnt; ++q) prod = prod * g[(i64)(t0 + q) * dmax + (e[q] - 1)];
+            if (M) prod = prod * g[(i64)(t0 + cnt) * dmax + c];
+            E[(i64)k * ld + R] = prod;
+        }
+        for (i64 R = cnt_rows * D; R < ld; ++R) E[(i64)k * ld + R] = 0.0;
+    }
+}
+
+/* out[R + mR j] = sum_k EL[k, R] ER[k, j], k ascending: a packed register-tile GEMM (CP_MR rows x
+ * CP_NR columns per tile, all K terms of a tile summed in one pass in k order) */
+static void cp_gemm(const double* EL, i64 mR, const double* ER, i64 n, int K, double* out) {
+    const i64 nrb = (mR + CP_MR - 1) / CP_MR, ncb = (n + CP_NR - 1) / CP_NR;
+    /* pack: Ap[rb][k][CP_MR], Bp[cb][k][CP_NR] (zero-padded at the edges) */
+    double* Ap = (double*)aligned_alloc(64, sizeof(double) * (size_t)(nrb * K * CP_MR));
+    double* Bp = (double*)aligned_alloc(64, sizeof(double) * (size_t)(ncb * K * CP_NR));
+#pragma omp parallel for schedule(static)
+    for (i64 rb = 0; rb < nrb; ++rb)
+        for (int k = 0; k < K; ++k)
+            for (int r = 0; r < CP_MR; ++r) {
+                const i64 R = rb * CP_MR + r;
+                Ap[(rb * K + k) * CP_MR + r] = R < mR ? EL[(i64)k * mR + R] : 0.0;
+            }
+#pragma omp parallel for schedule(static)
+    for (i64 cb = 0; cb < ncb; ++cb)
+        for (int k = 0; k < K; ++k)
+            for (int c = 0; c < CP_NR; ++c) {
+                const i64 j = cb * CP_NR + c;
+                Bp[(cb * K + k) * CP_NR + c] = j < n ? ER[(i64)k * n + j] : 0.0;
+            }
+    /* a task = 16 column tiles; per row tile the K terms go in panels of CP_KC (the tile's A panel
+     * stays in L1 while the task's B panels stream from L2), the running sums of the 16 tiles
+     * carried in a small buffer between panels: every sum still adds its terms in k order */
+    const i64 cbs = 16, ntask = (ncb + cbs - 1) / cbs;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (i64 task = 0; task < ntask; ++task) {
+        const i64 cb0 = task * cbs, cb1 = cb0 + cbs < ncb ? cb0 + cbs : ncb;
+        v4d st[16][CP_NR][2];
+        for (i64 rb = 0; rb < nrb; ++rb) {
+            for (int kp = 0; kp < K; kp += CP_KC) {
+                const int kc = K - kp < CP_KC ? K - kp : CP_KC;
+                const double* a = Ap + (rb * K + kp) * CP_MR;
+                for (i64 cb = cb0; cb < cb1; ++cb) {
+                    const double* b = Bp + (cb * K + kp) * CP_NR;
+                    v4d acc[CP_NR][2];
+                    for (int c = 0; c < CP_NR; ++c) {
+                        acc[c][0] = kp ? st[cb - cb0][c][0] : (v4d){0.0, 0.0, 0.0, 0.0};
+                        acc[c][1] = kp ? st[cb - cb0][c][1] : (v4d){0.0, 0.0, 0.0, 0.0};
+                    }
+                    for (int k = 0; k < kc; ++k) {
+                        v4d a0, a1;
+                        memcpy(&a0, a + k * CP_MR, sizeof a0);
+                        memcpy(&a1, a + k * CP_MR + 4, sizeof a1);
+                        for (int c = 0; c < CP_NR; ++c) {
+                            const double bv = b[k * CP_NR + c];
+                            const v4d bb = {bv, bv, bv, bv};
+                            acc[c][0] = acc[c][0] + a0 * bb;
+                            acc[c][1] = acc[c][1] + a1 * bb;
+                        }
+                    }
+                    for (int c = 0; c < CP_NR; ++c) {
+                        st[cb - cb0][c][0] = acc[c][0];
+                        st[cb - cb0][c][1] = acc[c][1];
+                    }
+                }
+            }
+            for (i64 cb = cb0; cb < cb1; ++cb)
+                for (int c = 0; c < CP_NR; ++c) {
+                    const i64 j = cb * CP_NR + c;
+                    if (j >= n) break;
+                    double v[CP_MR];
+                    memcpy(v, &st[cb - cb0][c][0], sizeof(v4d));
+                    memcpy(v + 4, &st[cb - cb0][c][1], sizeof(v4d));
+                    for (int r = 0; r < CP_MR; ++r) {
+                        const i64 R = rb * CP_MR + r;
+                        if (R < mR) out[R + mR * j] = v[r];
+                    }
+                }
+        }
+    }
+    free(Ap);
+    free(Bp);
+}
+
+static void batcheval_cp_fast(const orc_func* f, const i32* I, i64 m, int nl, const i32* J, i64 n,
+                              int nr, int M, double* out) {
+    const int K = (int)f->p[0];
+    const i64 D = M ? f->localdims[nl] : 1, mR = m * D;
+    double* EL = (double*)malloc(sizeof(double) * (size_t)(K * mR + 1));
+    double* ER = (double*)malloc(sizeof(double) * (size_t)(K * n + 1));
+    double t0 = omp_get_wtime();
+    cp_factors(f, I, m, nl, M, D, 0, EL, mR);
+    cp_factors(f, J, n, nr, 0, 1, f->L - nr, ER, n);
+    double t1 = omp_get_wtime();
+    cp_gemm(EL, mR, ER, n, K, out);
+    if (getenv("ORC_FAST_PROF"))
+        fprintf(stderr, "cp %ld x %ld K=%d: factors %.3f s, gemm %.3f s\n", (long)mR, (long)n, K, t1 - t0,
+                omp_get_wtime() - t1);
+    free(EL);
+    free(ER);
+}
+#endif
+
 /* _batchevaluate_dispatch (batcheval.jl:131-175): result[i, c, j] = f([I_i..., c..., J_j...]),
  * loops i, c, j nested with j innermost. I: m x nl (row-major per entry), J: n x nr.
  * out is column-major (m, prod(d_c), n). Returns maxabs(init, out) via *maxabs (util.jl:34). */
 static void batcheval(const orc_func* f, const i32* I, i64 m, int nl, const i32* J, i64 n, int nr,
                       int M, double* out, double* maxabs) {
+#ifdef ORC_FAST
+    if (f->kind == F_CP && m > 0 && n > 0) {
+        batcheval_cp_fast(f, I, m, nl, J, n, nr, M, out);
+        if (maxabs) {
+            double mx = *maxabs;
+            const i64 tot = m * (M ? f->localdims[nl] : 1) * n;
+            for (i64 e = 0; e < tot; ++e) mx = jl_max(fabs(mx), fabs(out[e]));
+            *maxabs = mx;
+        }
+        return;
+    }
+#endif
     int L = nl + M + nr;
     i32 x[512];
     i64 D = 1;
@@ -468,10 +621,22 @@ static int rrlu_copy(const double* A, i64 m, i64 n, i64 maxrank, double reltol, 
     lu->rowperm = (i64*)malloc(sizeof(i64) * (size_t)(m > 0 ? m : 1));
     lu->colperm = (i64*)malloc(sizeof(i64) * (size_t)(n > 0 ? n : 1));
     if (!W || !lu->rowperm || !lu->colperm) return fail(ORC_ERR_ALLOC, "alloc");
+#ifdef ORC_FAST
+    /* first touch by the threads that update these columns (static contiguous column blocks, as
+     * in cpu_rrlu_inplace_omp): on a multi-socket host the pages land on their NUMA node */
+#pragma omp parallel for schedule(static)
+    for (i64 j = 0; j < n; ++j) memcpy(W + j * m, A + j * m, sizeof(double) * (size_t)m);
+#else
     memcpy(W, A, sizeof(double) * (size_t)(m * n));
+#endif
     lu->m = m; lu->n = n; lu->leftorth = leftorth;
+#ifdef ORC_FAST
+    cpu_rrlu_inplace_omp(W, m, n, m, maxrank, reltol, abstol, leftorth, lu->rowperm, lu->colperm,
+                         &lu->np, &lu->error, -1);
+#else
     orc_rrlu_inplace(W, m, n, m, maxrank, reltol, abstol, leftorth, lu->rowperm, lu->colperm,
                      &lu->np, &lu->error, -1);
+#endif
     lu->L = (double*)malloc(sizeof(double) * (size_t)(m * lu->np + 1));
     lu->U = (double*)malloc(sizeof(double) * (size_t)(lu->np * n + 1));
     int st = orc_rrlu_extract(W, m, n, m, lu->np, leftorth, lu->L, lu->U);
@@ -494,6 +659,9 @@ static void luci_left(const orc_lu* lu, double* out /* m x np */) {
         /* colstimespivotinv: [I; L21 / LowerTriangular(L11)] then result[rowperm,:] = result */
         double* res = (double*)calloc((size_t)(m * np + 1), sizeof(double));
         for (i64 i = 0; i < np; ++i) res[i + i * m] = 1.0;
+#ifdef ORC_FAST
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
         for (i64 i = np; i < m; ++i) {
             for (i64 j = np - 1; j >= 0; --j) {
                 double s = L[i + j * m];
@@ -507,6 +675,9 @@ static void luci_left(const orc_lu* lu, double* out /* m x np */) {
     } else {
         /* colmatrix: left(lu) * right(lu, permute=false)[:, 1:np] */
         const double* U = lu->U;
+#ifdef ORC_FAST
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
         for (i64 i = 0; i < m; ++i)
             for (i64 j = 0; j < np; ++j) {
                 double s = 0.0;
@@ -522,6 +693,9 @@ static void luci_right(const orc_lu* lu, double* out /* np x n */) {
     if (lu->leftorth) {
         /* rowmatrix: left(lu, permute=false)[1:np, :] * right(lu) */
         const double* L = lu->L;
+#ifdef ORC_FAST
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
         for (i64 j = 0; j < n; ++j)
             for (i64 a = 0; a < np; ++a) {
                 double s = 0.0;
@@ -532,6 +706,9 @@ static void luci_right(const orc_lu* lu, double* out /* np x n */) {
         /* pivotinvtimesrows: [I, UpperTriangular(U11) \ U12], result[:, colperm] = result */
         double* res = (double*)calloc((size_t)(np * n + 1), sizeof(double));
         for (i64 i = 0; i < np; ++i) res[i + i * np] = 1.0;
+#ifdef ORC_FAST
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
         for (i64 c = np; c < n; ++c) {
             for (i64 a = np - 1; a >= 0; --a) {
                 double s = U[a + c * np];
@@ -893,6 +1070,17 @@ static int tci_setsitetensor(orc_tci* t, int p) {
         return ORC_OK;
     }
     i64 r1 = t->I[p + 1].n;
+#ifdef ORC_FAST
+    /* fast mode: the solved tensor is never read in deterministic mode (see "fast mode") */
+    free(Pi1);
+    if (r1 != nJ) {
+        char msg[128];
+        snprintf(msg, sizeof msg, "Pivot matrix at bond %d is not square!", p + 1);
+        return fail(ORC_ERR_NONSQ, msg);
+    }
+    set_T(t, p, NULL, 0);
+    return ORC_OK;
+#endif
     double* P = filltensor(t, &t->I[p + 1], &t->J[p], 0);
     if (r1 != nJ) {
         free(P); free(Pi1);
@@ -1085,6 +1273,67 @@ int orc_tci_optimize(orc_tci* t, double tolerance, i64 maxbonddim, int maxiter, 
     for (int i = 0; i < it; ++i) errors[i] = errors[i] / errnorm;
     *niter = it;
     return ORC_OK;
+}
+
+/* ------------------------------------------------------------ checkpoints
+ * The state a warm restart needs (SURVEY 5 "Checkpoint / resume": the reference resumes from
+ * Iset/Jset, tensorci2.jl:123-137), plus what the next sweep2site! reads: the last history entry
+ * (extra sets, :1212-1217), pivoterrors, bonderrors and maxsamplevalue. Site tensors are not
+ * saved (every sweep recomputes them). Used to split long oracle runs (config 5 as stated). */
+static int wr_iset(FILE* fp, const iset_t* s) {
+    i64 h[2] = {s->n, s->w};
+    if (fwrite(h, sizeof h, 1, fp) != 1) return 1;
+    if (s->n * s->w > 0 && fwrite(s->d, sizeof(i32), (size_t)(s->n * s->w), fp) != (size_t)(s->n * s->w)) return 1;
+    return 0;
+}
+static int rd_iset(FILE* fp, iset_t* s) {
+    i64 h[2];
+    if (fread(h, sizeof h, 1, fp) != 1 || h[1] != s->w) return 1;
+    iset_free(s);
+    iset_init(s, (int)h[1]);
+    s->n = s->cap = h[0];
+    s->d = (i32*)malloc(sizeof(i32) * (size_t)(h[0] * h[1] + 1));
+    if (h[0] * h[1] > 0 && fread(s->d, sizeof(i32), (size_t)(h[0] * h[1]), fp) != (size_t)(h[0] * h[1])) return 1;
+    return 0;
+}
+
+int orc_tci_save(const orc_tci* t, const char* path) {
+    FILE* fp = fopen(path, "wb");
+    if (!fp) return fail(ORC_ERR_ARG, "cannot open checkpoint for writing");
+    int bad = 0;
+    i64 hdr[4] = {0x54434932, t->L, t->has_hist, t->npe};
+    bad |= fwrite(hdr, sizeof hdr, 1, fp) != 1;
+    bad |= fwrite(&t->maxsample, sizeof(double), 1, fp) != 1;
+    if (t->npe) bad |= fwrite(t->pe, sizeof(double), (size_t)t->npe, fp) != (size_t)t->npe;
+    bad |= fwrite(t->bonderr, sizeof(double), (size_t)(t->L - 1), fp) != (size_t)(t->L - 1);
+    for (int p = 0; p < t->L && !bad; ++p)
+        bad |= wr_iset(fp, &t->I[p]) | wr_iset(fp, &t->J[p]) | wr_iset(fp, &t->hI[p]) | wr_iset(fp, &t->hJ[p]);
+    bad |= fclose(fp) != 0;
+    return bad ? fail(ORC_ERR_ARG, "checkpoint write failed") : ORC_OK;
+}
+
+/* t must come from orc_tci_new with the same integrand and localdims */
+int orc_tci_load(orc_tci* t, const char* path) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return fail(ORC_ERR_ARG, "cannot open checkpoint");
+    int bad = 0;
+    i64 hdr[4];
+    bad |= fread(hdr, sizeof hdr, 1, fp) != 1;
+    if (!bad && (hdr[0] != 0x54434932 || hdr[1] != t->L)) bad = 1;
+    if (!bad) {
+        t->has_hist = (int)hdr[2];
+        free(t->pe);
+        t->npe = hdr[3];
+        t->pe = (double*)malloc(sizeof(double) * (size_t)(t->npe + 1));
+        bad |= fread(&t->maxsample, sizeof(double), 1, fp) != 1;
+        if (t->npe) bad |= fread(t->pe, sizeof(double), (size_t)t->npe, fp) != (size_t)t->npe;
+        bad |= fread(t->bonderr, sizeof(double), (size_t)(t->L - 1), fp) != (size_t)(t->L - 1);
+        for (int p = 0; p < t->L && !bad; ++p)
+            bad |= rd_iset(fp, &t->I[p]) | rd_iset(fp, &t->J[p]) | rd_iset(fp, &t->hI[p]) | rd_iset(fp, &t->hJ[p]);
+    }
+    fclose(fp);
+    tci_invalidate(t);
+    return bad ? fail(ORC_ERR_ARG, "checkpoint read failed") : ORC_OK;
 }
 
 /* -------------------------------------------------------------- accessors */

@@ -41,7 +41,7 @@ struct tci_ctx {
     double* ybuf = nullptr;
     size_t capY = 0;
     int flush_every = 10;  // deferred-update depth nb: the shadow epoch (1 = write back every pivot)
-    int epochs = 3;        // shadow epochs per fp64 write-back (two-level epoch; env TCI_RRLU_EPOCHS)
+    int epochs = 0;        // shadow epochs per fp64 write-back (two-level epoch; 0 = by shape; env TCI_RRLU_EPOCHS)
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
     int pass_gridx = 1;    // rrLU pass workgroups per CU (env TCI_PASS_GRIDX; 1 = all resident at once)
@@ -198,6 +198,8 @@ struct tci_func {
     int32_t mpoEnv = 0, mpoTmp = 0;
     tci_host_fn hostfn = nullptr;  // TCI_F_HOST: the user's f on the host (tci_func_create_host)
     void* hostuser = nullptr;
+    std::vector<const tci_func*> cparts;  // TCI_F_C128: real parts, then imaginary parts
+    int32_t cnre = 0;
     FuncDev view() const {
         FuncDev f;
         f.cpK = cpK;
@@ -405,6 +407,17 @@ struct StopPoll {
 // its trailing values are left stale). Leaves on the device: rowphys/colphys (= rowpermutation /
 // colpermutation, 0-based) in c->rowperm / c->colperm, pivot values in c->pivv, L columns in
 // physical row order in c->Lp (ld m) and U rows in physical column order in c->Up (ld mr).
+// Shadow epochs per fp64 write-back (two-level epoch). A later shadow epoch's read
+// passes pay the EXT prologue (exact pending chains up to nb * epochs - 1 long, ~5-10 us each), and
+// a refresh replaces a write-back (18 B/element) by the MFMA search's shadow store (4 B/element): the
+// trade pays where a write-back streams long, i.e. on large trailing blocks. Measured on MI355X
+// (profiles/r04_ab_epochs_shapes.jsonl, r = 256): 2048^2 / 4096^2 fastest at 1, 8192^2 / 16384^2 at
+// 3; the break-even (2 write-backs' 14 B/element saved ~ 20 EXT prologues) is near 2.4e7 elements.
+int rrlu_epochs(const tci_ctx* c, int64_t m, int64_t n) {
+    if (c->epochs > 0) return c->epochs;
+    return (double)m * (double)n >= 2.4e7 ? 3 : 1;
+}
+
 int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
                 double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out) {
     int st;
@@ -517,8 +530,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     // epoch ends with a write-back (round 2's scheme); the exact passes (shadow off) always do.
     // (the refresh is the MFMA search's: shadow epochs of 2 .. 15 pivots -- pass 0 writes the
     // shadow of A and cannot refresh, and the search has at most two K-steps)
-    const int epochs = (shadow && tci::shadow_elem_bytes() == 2 && nb >= 2 && nb <= 15)
-                           ? std::max(1, std::min(c->epochs, tci::kMaxPendR / nb)) : 1;
+    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15)
+                           ? std::max(1, std::min(rrlu_epochs(c, m, n), tci::kMaxPendR / nb)) : 1;
     const int nbx = nb * epochs;
     g.nbs = nb;
     g.pe = g.ps = 0;
@@ -668,6 +681,8 @@ int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
     const int D = M ? f->localdims[nl] : 1;
     if (ldo < m * D) return set_err(c, TCI_ERR_ARG, "ldo < m * prod(centre dims)");
     HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    if (f->kind == TCI_F_C128)
+        return set_err(c, TCI_ERR_ARG, "a ComplexF64 integrand needs the ComplexF64 entries (*_c128_*)");
     if (f->kind == TCI_F_HOST) return host_batcheval(c, f, dI, m, nl, dJ, n, nr, M, D, dout, ldo);
     if (m > 0 && n > 0) {
         FuncDev fv = f->view();
@@ -957,11 +972,13 @@ int tci_set_rrlu_flush(tci_ctx* c, int nb) {
 }
 
 int tci_set_rrlu_epochs(tci_ctx* c, int epochs) {
-    if (!c || epochs < 1 || epochs > tci::kMaxPendR)
-        return set_err(c, TCI_ERR_ARG, "epochs must be in 1.." + std::to_string(tci::kMaxPendR));
+    if (!c || epochs < 0 || epochs > tci::kMaxPendR)
+        return set_err(c, TCI_ERR_ARG, "epochs must be in 0 (by shape) .. " + std::to_string(tci::kMaxPendR));
     c->epochs = epochs;
     return TCI_OK;
 }
+
+int tci_rrlu_epochs_for(tci_ctx* c, int64_t m, int64_t n) { return c ? rrlu_epochs(c, m, n) : 0; }
 
 int tci_set_rrlu_small(tci_ctx* c, int enabled) {
     c->small_path = enabled != 0;
@@ -1119,6 +1136,28 @@ int tci_func_create_host(tci_ctx* c, tci_host_fn fn, void* user, const int32_t* 
         return set_err(c, TCI_ERR_NOMEM, "integrand allocation failed");
     }
     hipMemcpy(f->dld, localdims, L * sizeof(int32_t), hipMemcpyHostToDevice);
+    *out = f;
+    return TCI_OK;
+}
+
+int tci_func_create_c128(tci_ctx* c, const tci_func* const* re, int32_t nre, const tci_func* const* im,
+                         int32_t nim, tci_func** out) {
+    if (!c || !out || nre < 0 || nim < 0 || nre + nim < 1 || (nre && !re) || (nim && !im)) return TCI_ERR_ARG;
+    const tci_func* first = nre ? re[0] : im[0];
+    tci_func* f = new tci_func();
+    f->ctx = c;
+    f->kind = TCI_F_C128;
+    f->L = first->L;
+    f->localdims = first->localdims;
+    for (int i = 0; i < nre + nim; ++i) {
+        const tci_func* p = i < nre ? re[i] : im[i - nre];
+        if (!p || p->kind == TCI_F_C128 || p->L != f->L || p->localdims != f->localdims) {
+            delete f;
+            return set_err(c, TCI_ERR_ARG, "complex integrand: parts must be real integrands on the same localdims");
+        }
+        f->cparts.push_back(p);
+    }
+    f->cnre = nre;
     *out = f;
     return TCI_OK;
 }
@@ -1450,9 +1489,61 @@ int tci_luci_c128_h(tci_ctx* c, const double* A, int64_t m, int64_t n, int64_t l
                       right, npivot);
 }
 
+// TCI_F_C128: the complex Pi (interleaved, ld) in c->dA from the real parts (index tables uploaded
+// once, each part's real values into c->dRe and added into its component in part order), then
+// coeff * Pi and max|.| into c->maxbits. Launches only (the caller synchronises).
+static int c128_parts_assemble(tci_ctx* c, const tci_func* f, double cre, double cim, const int32_t* I,
+                               int64_t m, int32_t nl, const int32_t* J, int64_t n, int32_t nr, int32_t M,
+                               int64_t ld) {
+    const int64_t D = M ? f->localdims[nl] : 1, mR = m * D;
+    int st;
+    const size_t bi = (size_t)std::max<int64_t>(m * nl, 0) * 4, bj = (size_t)std::max<int64_t>(n * nr, 0) * 4;
+    if ((st = ensure(c, &c->dI, &c->capI, std::max<size_t>(bi / 4, 1)))) return st;
+    if ((st = ensure(c, &c->dJ, &c->capJ, std::max<size_t>(bj / 4, 1)))) return st;
+    if ((st = ensure_pinned(c, &c->hin, &c->capHin, bi + bj + 16))) return st;
+    if (bi) memcpy(c->hin, I, bi);
+    if (bj) memcpy(c->hin + bi, J, bj);
+    if (bi) HIPCHK(c, hipMemcpyAsync(c->dI, c->hin, bi, hipMemcpyHostToDevice, c->stream));
+    if (bj) HIPCHK(c, hipMemcpyAsync(c->dJ, c->hin + bi, bj, hipMemcpyHostToDevice, c->stream));
+    const int64_t ldr = round_up(std::max<int64_t>(mR, 1), 2);
+    if ((st = ensure(c, &c->dRe, &c->capRe, (size_t)(ldr * std::max<int64_t>(n, 1))))) return st;
+    if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * ld * std::max<int64_t>(n, 1))))) return st;
+    if (mR > 0 && n > 0) {
+        HIPCHK(c, hipMemsetAsync(c->dA, 0, (size_t)(2 * ld * n) * sizeof(double), c->stream));
+        for (size_t p = 0; p < f->cparts.size(); ++p) {
+            if ((st = batcheval_launch(c, f->cparts[p], c->dI, m, nl, c->dJ, n, nr, M, c->dRe, ldr))) return st;
+            tci::launch_c128_accum(c->stream, c->dRe, ldr, (int)mR, (int)n, (int)p >= f->cnre ? 1 : 0,
+                                   reinterpret_cast<double2*>(c->dA), ld);
+        }
+    }
+    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    if (mR > 0 && n > 0)
+        tci::launch_c128_finish(c->stream, (int)mR, (int)n, cre, cim, reinterpret_cast<double2*>(c->dA), ld,
+                                c->maxbits);
+    HIPCHK(c, hipGetLastError());
+    return TCI_OK;
+}
+
 int tci_batcheval_c128_h(tci_ctx* c, const tci_func* f, double cre, double cim,
                          const int32_t* I, int64_t m, int32_t nl, const int32_t* J, int64_t n,
                          int32_t nr, int32_t M, double* out, double* maxabs) {
+    if (c && f && maxabs && f->kind == TCI_F_C128) {
+        if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
+        if (M < 0 || M > 1) return set_err(c, TCI_ERR_ARG, "only M = 0 or M = 1 centre legs are supported");
+        const int64_t mR = m * (M ? f->localdims[nl] : 1), ld = std::max<int64_t>(mR, 1);
+        if (mR > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+        int st;
+        if ((st = c128_parts_assemble(c, f, cre, cim, I, m, nl, J, n, nr, M, ld))) return st;
+        if (out && mR > 0 && n > 0)
+            HIPCHK(c, hipMemcpyAsync(out, c->dA, mR * n * 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        double mx;
+        memcpy(&mx, c->hmaxbits, sizeof mx);
+        *maxabs = (mR > 0 && n > 0) ? mx : 0.0;
+        return TCI_OK;
+    }
     if (!c || !f || !maxabs) return TCI_ERR_ARG;
     if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
     const int64_t D = M ? f->localdims[nl] : 1;
@@ -1491,6 +1582,17 @@ int tci_update_pivots_c128_h(tci_ctx* c, const tci_func* f, double cre, double c
     if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
     const int64_t ld = std::max<int64_t>(m, 1);
     int st;
+    if (f->kind == TCI_F_C128) {  // Pi from the complex integrand's real parts
+        if ((st = c128_parts_assemble(c, f, cre, cim, rows, m, nl, cols, n, nr, 0, ld))) return st;
+        HIPCHK(c, hipMemcpyAsync(c->hmaxbits, c->maxbits, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        double mx;
+        memcpy(&mx, c->hmaxbits, sizeof mx);
+        *maxabs = (m > 0 && n > 0) ? mx : 0.0;
+        return cluci_core(c, m, n, maxrank, reltol, abstol, leftorth, rowidx, colidx, pivoterrors,
+                          want_factors ? left : nullptr, want_factors ? right : nullptr, npivot);
+    }
     // real values of f on the device, then Pi = coeff * f and max|Pi| (hypot) into c->dA
     if ((st = ensure(c, &c->dRe, &c->capRe, (size_t)(round_up(ld, 2) * std::max<int64_t>(n, 1)))))
         return st;

@@ -118,6 +118,7 @@ struct FuncDev {
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // bytes per element of the rrLU passes' shadow (2: fp16, scaled per epoch; 4: fp32)
 int shadow_elem_bytes();
+bool shadow_two_level();
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
 // One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).
@@ -187,6 +188,10 @@ void launch_crrlu_extract(hipStream_t s, const double2* A, int64_t ld, int m, in
 
 void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int n, double cre,
                        double cim, double2* out, int64_t ldo, unsigned long long* maxbits);
+void launch_c128_accum(hipStream_t s, const double* re, int64_t ldr, int m, int n, int comp, double2* out,
+                       int64_t ldo);
+void launch_c128_finish(hipStream_t s, int m, int n, double cre, double cim, double2* out, int64_t ldo,
+                        unsigned long long* maxbits);
 void launch_csitetensor_solve(hipStream_t s, const double2* P, int r, const double2* Pi1, int R,
                               double2* T, double2* work, int* piv);
 void launch_ctt_eval(hipStream_t s, const double2* cores, const int64_t* off, const int32_t* bd,

@@ -2015,6 +2015,9 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
 // column tiles (at least one; the host rejects tiles_r > kMaxPassGrid).
 int shadow_elem_bytes() { return kShHalf ? 2 : 4; }
+// the two-level epoch (refresh + EXT passes) exists only in the MFMA search (k_pass_mf): a build
+// without it (TCI_SH_MFMA=0) must write back after every shadow epoch
+bool shadow_two_level() { return kShHalf && TCI_SH_MFMA; }
 
 int argmax_grid(int m, int n, int k, int cb, int max_grid) {
     (void)k;

@@ -476,6 +476,44 @@ __global__ void k_c128_scale(const double* __restrict__ re, int64_t ldr, int m, 
     if ((threadIdx.x & 63) == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
 }
 
+// A ComplexF64 integrand given as real parts (TCI_F_C128, tci_func_create_c128): the real value
+// of one part added into the real (comp 0) or imaginary (comp 1) component of the complex Pi ...
+__global__ void k_c128_accum(const double* __restrict__ re, int64_t ldr, int m, int n, int comp,
+                             double2* __restrict__ out, int64_t ldo) {
+    const int64_t tot = (int64_t)m * n;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(e % m), j = (int)(e / m);
+        double2 z = out[i + (int64_t)j * ldo];
+        const double x = re[i + (int64_t)j * ldr];
+        if (comp) z.y = z.y + x;
+        else z.x = z.x + x;
+        out[i + (int64_t)j * ldo] = z;
+    }
+}
+
+// ... then the coefficient (complex multiply, no fma) and max|.| (abs = hypot, NaN-propagating)
+__global__ void k_c128_finish(int m, int n, double cre, double cim, double2* __restrict__ out,
+                              int64_t ldo, unsigned long long* maxbits) {
+    const int64_t tot = (int64_t)m * n;
+    double mx = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(e % m), j = (int)(e / m);
+        const double2 w = out[i + (int64_t)j * ldo];
+        const double2 z = make_double2(__dsub_rn(__dmul_rn(cre, w.x), __dmul_rn(cim, w.y)),
+                                       __dadd_rn(__dmul_rn(cre, w.y), __dmul_rn(cim, w.x)));
+        out[i + (int64_t)j * ldo] = z;
+        const double a = jl_hypot(z.x, z.y);
+        mx = (a != a || a > mx) ? a : mx;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double v = __shfl_xor(mx, o);
+        mx = (v != v || v > mx) ? v : mx;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
+}
+
 // T = Pi1 * P^-1 for ComplexF64 (setsitetensor!, tensorci2.jl:620-627: transpose(transpose(P) \
 // transpose(Pi1))): getrf of A = P^T with partial pivoting (LAPACK's pivot: first maximal
 // cabs1 = |re| + |im|), one 1024-thread workgroup, A in global memory (r x r).
@@ -1435,6 +1473,21 @@ void launch_c128_scale(hipStream_t s, const double* re, int64_t ldr, int m, int 
     if (grid < 1) grid = 1;
     if (grid > 8192) grid = 8192;
     k_c128_scale<<<grid, 256, 0, s>>>(re, ldr, m, n, cre, cim, out, ldo, maxbits);
+}
+
+static int c128_grid(int64_t tot) {
+    int64_t g = (tot + 255) / 256;
+    return (int)(g < 1 ? 1 : g > 8192 ? 8192 : g);
+}
+
+void launch_c128_accum(hipStream_t s, const double* re, int64_t ldr, int m, int n, int comp, double2* out,
+                       int64_t ldo) {
+    k_c128_accum<<<c128_grid((int64_t)m * n), 256, 0, s>>>(re, ldr, m, n, comp, out, ldo);
+}
+
+void launch_c128_finish(hipStream_t s, int m, int n, double cre, double cim, double2* out, int64_t ldo,
+                        unsigned long long* maxbits) {
+    k_c128_finish<<<c128_grid((int64_t)m * n), 256, 0, s>>>(m, n, cre, cim, out, ldo, maxbits);
 }
 
 void launch_csitetensor_solve(hipStream_t s, const double2* P, int r, const double2* Pi1, int R,

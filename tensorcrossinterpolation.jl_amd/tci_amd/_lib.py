@@ -54,6 +54,7 @@ SIGNATURES = {
     "tci_set_timing": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_epochs": ([vp, C.c_int], C.c_int),
+    "tci_rrlu_epochs_for": ([vp, i64, i64], C.c_int),
     "tci_set_rrlu_small": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_mid": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_shadow": ([vp, C.c_int], C.c_int),
@@ -63,6 +64,7 @@ SIGNATURES = {
     "tci_func_create": ([vp, C.c_int, vp, i64, i32p, i32, C.POINTER(vp)], C.c_int),
     "tci_func_destroy": ([vp], C.c_int),
     "tci_func_create_host": ([vp, vp, vp, i32p, i32, C.POINTER(vp)], C.c_int),
+    "tci_func_create_c128": ([vp, vp, i32, vp, i32, C.POINTER(vp)], C.c_int),
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_batcheval_d": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_rrlu_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, i64, pi64, pdbl],

@@ -47,13 +47,21 @@ class Comm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
-    def allreduce_maxabs(self, x):
-        """max over ranks with Julia's NaN propagation (any NaN -> NaN)."""
+    def allreduce_maxabs(self, x, error=None):
+        """max over ranks with Julia's NaN propagation (any NaN -> NaN). `error`: an exception this
+        rank's local work raised; the flag travels in the same reduction, so when any rank failed
+        EVERY rank raises here together (the failing one its own error) instead of the others
+        blocking in the next collective."""
         torch = self.torch
-        isn = math.isnan(x)
-        t = torch.tensor([-math.inf if isn else float(x), 1.0 if isn else 0.0], dtype=torch.float64,
+        isn = error is None and math.isnan(x)
+        val = -math.inf if (isn or error is not None) else float(x)
+        t = torch.tensor([val, 1.0 if isn else 0.0, 1.0 if error is not None else 0.0], dtype=torch.float64,
                          device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        if t[2].item() > 0:
+            if error is not None:
+                raise error
+            raise RuntimeError("batch evaluation failed on another rank")
         return math.nan if t[1].item() > 0 else float(t[0].item())
 
     def allgather_columns(self, block, blocks, rows):
@@ -158,14 +166,17 @@ class ShardedBatchEvaluator:
                 self._buf.free()
             self._buf = _DevBuf(ctx, int(need * 1.25) + 1024)
         view = _DevView(ctx, self._buf.ptr, rows, nloc + 1, ld)
-        mx = 0.0
+        mx, err = 0.0, None
         if nloc > 0 and rows > 0:
             Jl = np.ascontiguousarray(J[j0:j1])
             m_ = C.c_double()
-            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), nloc,
-                                              Jl.shape[1], M, view.ptr, ld, C.byref(m_)))
-            mx = m_.value
-        return view, (j0, j1), self.comm.allreduce_maxabs(mx)
+            try:
+                ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), nloc,
+                                                  Jl.shape[1], M, view.ptr, ld, C.byref(m_)))
+                mx = m_.value
+            except Exception as e:  # raised on every rank by the reduction (no rank left waiting)
+                err = e
+        return view, (j0, j1), self.comm.allreduce_maxabs(mx, err)
 
     @property
     def device_gather(self):
@@ -198,16 +209,22 @@ class ShardedBatchEvaluator:
             bufs[slot] = _DevBuf(ctx, int(need * 1.25) + 1024)
         base = bufs[slot].ptr.value
         j0, j1 = min(r * w, n), min((r + 1) * w, n)
-        mx = 0.0
+        mx, err = 0.0, None
         if j1 > j0 and rows > 0:
             Jl = np.ascontiguousarray(J[j0:j1])
             m_ = C.c_double()
-            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), j1 - j0, nr, M,
-                                              C.c_void_p(base + 8 * ld * w * r), ld, C.byref(m_)))
-            mx = m_.value
+            try:
+                ctx.check(ctx.lib.tci_batcheval_d(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), j1 - j0,
+                                                  nr, M, C.c_void_p(base + 8 * ld * w * r), ld, C.byref(m_)))
+                mx = m_.value
+            except Exception as e:  # e.g. a HostFunctionEvaluator's f raising on this rank only
+                err = e
+        # agree on success (and max|Pi|) over the host group BEFORE the RCCL all-gather, so a
+        # failure on one rank raises on every rank instead of leaving the others in ncclAllGather
+        gmx = self.comm.allreduce_maxabs(mx, err)
         if rows > 0:
             self.device_comm.allgather(C.c_void_p(base + 8 * ld * w * r), C.c_void_p(base), 8 * ld * w)
-        return _DevView(ctx, C.c_void_p(base), rows, n, ld), self.comm.allreduce_maxabs(mx)
+        return _DevView(ctx, C.c_void_p(base), rows, n, ld), gmx
 
     def update_pivots_gathered(self, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                want_left=True, want_right=True):
@@ -296,11 +313,13 @@ class ShardedBatchEvaluator:
         J = np.ascontiguousarray(np.asarray(J, np.int32))
         D = self.localdims[I.shape[1]] if M == 1 else 1
         j0, j1 = self.block(len(J))
+        blk, mx, err = np.zeros((I.shape[0] * D, 0), order="F"), 0.0, None
         if j1 > j0:
-            blk, mx = self.local.pi(I, J[j0:j1], M)
-        else:
-            blk, mx = np.zeros((I.shape[0] * D, 0), order="F"), 0.0
-        return (j0, j1), blk, self.comm.allreduce_maxabs(mx)
+            try:
+                blk, mx = self.local.pi(I, J[j0:j1], M)
+            except Exception as e:  # raised on every rank by the reduction below
+                err = e
+        return (j0, j1), blk, self.comm.allreduce_maxabs(mx, err)
 
     def pi(self, I, J, M=0):
         """Full (|I| * D) x |J| Pi on every rank, and max|Pi|."""

@@ -9,6 +9,7 @@ tci_sitetensor_h). Only index sets, pivot errors and site tensors cross PCIe.
 Conventions: sites/bonds are 1-based in this API like the reference (b in 1..L-1); index sets
 are (count, width) int32 arrays of 1-based local indices.
 """
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -380,6 +381,9 @@ class TensorCI2:
     def _native_handle(self, ctx):
         h = getattr(self, "_native_h", None)
         if h is None or getattr(self, "_native_ctx", None) is not ctx:
+            if h is not None and self._py_stale:
+                self._native_pull_sets()  # the newest sets live only in the old native object
+                self._native_dirty = True  # ... so the new one must receive them
             h = C.c_void_p()
             ctx.check(ctx.lib.tci_tci2_create(ctx.h, len(self), np.ascontiguousarray(self.localdims, np.int32),
                                               C.byref(h)))
@@ -399,10 +403,11 @@ class TensorCI2:
         tens = np.empty(max(cap, 1))
         offs = np.zeros(2 * n, np.int64)
         handled = C.c_int(0)
-        ctx.check(lib.tci_tci2_sweep1site(h, f.h, int(bool(fwd)), float(reltol), float(abstol),
-                                          int(min(maxbonddim, INT64_MAX)), int(bool(updatetensors)),
-                                          tens.ctypes.data_as(C.c_void_p), cap, offs.ctypes.data_as(C.c_void_p),
-                                          C.byref(handled)))
+        with self._native_failure_sync(ctx, h):
+            ctx.check(lib.tci_tci2_sweep1site(h, f.h, int(bool(fwd)), float(reltol), float(abstol),
+                                              int(min(maxbonddim, INT64_MAX)), int(bool(updatetensors)),
+                                              tens.ctypes.data_as(C.c_void_p), cap, offs.ctypes.data_as(C.c_void_p),
+                                              C.byref(handled)))
         if not handled.value:
             return False
         self._native_pull(ctx, h)  # sweep1site! leaves the history alone (so does the kernel)
@@ -423,19 +428,38 @@ class TensorCI2:
         self._native_push(ctx, h)
         strat = {"backandforth": 0, "forward": 1, "backward": 2}[sweepstrategy]
         handled = C.c_int(0)
-        if fill_maxsample and niter > 0:
-            ctx.check(lib.tci_tci2_sweep2site_fill(h, f.h, int(niter), int(iter1), float(abstol),
-                                                   int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested)),
-                                                   C.byref(handled)))
-        else:
-            ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol),
-                                              int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested))))
-            if fill_maxsample:
-                ctx.check(lib.tci_tci2_fill_maxsample(h, f.h, C.byref(handled)))
+        with self._native_failure_sync(ctx, h, hist=niter > 0):
+            if fill_maxsample and niter > 0:
+                ctx.check(lib.tci_tci2_sweep2site_fill(h, f.h, int(niter), int(iter1), float(abstol),
+                                                       int(min(maxbonddim, INT64_MAX)), strat,
+                                                       int(bool(strictlynested)), C.byref(handled)))
+            else:
+                ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol),
+                                                  int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested))))
+                if fill_maxsample:
+                    ctx.check(lib.tci_tci2_fill_maxsample(h, f.h, C.byref(handled)))
         if niter > 0:
             self._native_has_hist = True  # every iteration starts a history
         self._native_pull(ctx, h)
         return bool(handled.value)
+
+    @contextlib.contextmanager
+    def _native_failure_sync(self, ctx, h, hist=False):
+        """A native sweep that fails (a NaN, a host callback's error) has already updated the native
+        sets in place, as the reference's sweep leaves the TensorCI2 half-updated when it throws: the
+        Python mirror then follows the native state (pulled on first access) before re-raising, so
+        the next push cannot resume from the stale Python copy."""
+        try:
+            yield
+        except Exception:
+            if hist:
+                self._native_has_hist = True
+            try:
+                self._native_pull(ctx, h)
+            except Exception:  # the original error is the one to report
+                self._py_stale = True
+                self._native_dirty = False
+            raise
 
     def _native_counts(self, which):
         ctx = self._native_ctx
@@ -536,7 +560,11 @@ class TensorCI2:
                  checkbatchevaluatable=False, checkconvglobalpivot=True, rng=None):
         """optimize! (tensorci2.jl:1018-1172). Returns (ranks, errors ./ errornormalization)."""
         errors, ranks, nglobalpivots = [], [], []
-        if checkbatchevaluatable and not (isinstance(f, GPUBatchEvaluator) or getattr(f, "is_batch", False)):
+        # any BatchEvaluator is accepted (tensorci2.jl:1044): the device evaluators and every
+        # HostFunctionEvaluator (pointwise, threaded or batch: it always exposes the batch interface)
+        from .hostfunction import HostFunctionEvaluator
+        if checkbatchevaluatable and not (isinstance(f, (GPUBatchEvaluator, HostFunctionEvaluator))
+                                          or getattr(f, "is_batch", False)):
             raise RuntimeError("Function `f` is not batch evaluatable")
         if 0 < nsearchglobalpivot < maxnglobalpivot:
             raise RuntimeError("nsearchglobalpivot < maxnglobalpivot!")
@@ -680,6 +708,9 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
     An evaluator that is not a GPUBatchEvaluator (e.g. a ShardedBatchEvaluator) supplies Pi
     through its pi() method; the factorisation then runs on this process's GPU."""
     if getattr(f, "is_complex", False):
+        if getattr(f, "host_values", False):  # a complex batch computed on the host (pi())
+            return _update_pivots_generic(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
+                                          want_left, want_right)
         return _update_pivots_c128(f, rows, cols, maxrank, reltol, abstol, leftorth, want_factors,
                                    want_left, want_right)
     if getattr(f, "shard_rrlu", False) and not want_factors:

@@ -22,16 +22,26 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-_lib = None
+FAST_LIB_PATH = os.path.join(ROOT, "oracle", "liboracle_fast.so")
+_libs = {}
 
 
 def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+    return _bind(LIB_PATH)
+
+
+def lib_fast():
+    """The oracle's fast mode (tci_oracle.c "fast mode"; config 5 as stated): OpenMP rrLU (bitwise
+    the same), CP evaluated factorised at the bond, site-tensor solves skipped (never read)."""
+    return _bind(FAST_LIB_PATH)
+
+
+def _bind(path):
+    if path not in _libs:
+        if not os.path.exists(path):
             import subprocess
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         L.orc_last_error.restype = C.c_char_p
         L.orc_fill_uniform.argtypes = [f64p, C.c_int64, C.c_uint64, C.c_int64]
         L.orc_submatrixargmax.argtypes = [f64p, C.c_int64, C.c_int64, C.c_int64, i64p, C.c_int64,
@@ -83,13 +93,15 @@ def lib():
         L.orc_cdiv.argtypes = [C.c_double] * 4 + [C.POINTER(C.c_double)] * 2
         L.orc_hypot.argtypes = [C.c_double, C.c_double]
         L.orc_hypot.restype = C.c_double
-        _lib = L
-    return _lib
+        L.orc_tci_save.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_tci_load.argtypes = [C.c_void_p, C.c_char_p]
+        _libs[path] = L
+    return _libs[path]
 
 
-def _check(st):
+def _check(st, L=None):
     if st != 0:
-        raise OracleError(st, lib().orc_last_error().decode())
+        raise OracleError(st, (L or lib()).orc_last_error().decode())
 
 
 def fill_uniform(n, seed, offset=0):
@@ -299,7 +311,8 @@ INT64_MAX = np.iinfo(np.int64).max
 class OracleTCI2:
     """CPU restatement of TensorCI2 (tensorci2.jl:50-137) in deterministic mode."""
 
-    def __init__(self, kind, params, localdims, initialpivots=None):
+    def __init__(self, kind, params, localdims, initialpivots=None, fast=False):
+        self._L = lib_fast() if fast else lib()
         self.localdims = [int(d) for d in localdims]
         L = len(self.localdims)
         if initialpivots is None:
@@ -307,13 +320,23 @@ class OracleTCI2:
         piv = np.ascontiguousarray(np.asarray(initialpivots, np.int32).reshape(-1, L))
         params = np.ascontiguousarray(params if params is not None and len(params) else [0.0], np.float64)
         st = C.c_int(0)
-        self._h = lib().orc_tci_new(kind, params, len(params), np.ascontiguousarray(self.localdims, np.int32),
+        self._h = self._L.orc_tci_new(kind, params, len(params), np.ascontiguousarray(self.localdims, np.int32),
                                     L, piv, piv.shape[0], C.byref(st))
-        _check(st.value)
+        _check(st.value, self._L)
+
+    def _chk(self, st):
+        _check(st, self._L)
+
+    def save(self, path):
+        """Checkpoint (orc_tci_save): sets, history entry, errors, maxsample."""
+        self._chk(self._L.orc_tci_save(self._h, path.encode()))
+
+    def load(self, path):
+        self._chk(self._L.orc_tci_load(self._h, path.encode()))
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().orc_tci_free(self._h)
+            self._L.orc_tci_free(self._h)
             self._h = None
 
     @property
@@ -321,20 +344,22 @@ class OracleTCI2:
         return len(self.localdims)
 
     def updatepivots(self, b, leftorthogonal=True, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX):
-        _check(lib().orc_tci_updatepivots(self._h, b, int(leftorthogonal), reltol, abstol, maxbonddim))
+        self._chk(self._L.orc_tci_updatepivots(self._h, b, int(leftorthogonal), reltol, abstol, maxbonddim))
 
     def sweep1site(self, forward=True, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX, updatetensors=True):
-        _check(lib().orc_tci_sweep1site(self._h, int(forward), reltol, abstol, maxbonddim, int(updatetensors)))
+        self._chk(self._L.orc_tci_sweep1site(self._h, int(forward), reltol, abstol, maxbonddim, int(updatetensors)))
 
     def sweep2site(self, niter=2, abstol=1e-8, maxbonddim=INT64_MAX, sweepstrategy="backandforth",
-                   strictlynested=False, fillsitetensors=True):
-        _check(lib().orc_tci_sweep2site(self._h, niter, 1, abstol, maxbonddim,
+                   strictlynested=False, fillsitetensors=True, iter1=1):
+        """iter1: the number of the first half-sweep (odd = forward under :backandforth), so a
+        sweep2site! call can be split into half-sweeps with identical results."""
+        self._chk(self._L.orc_tci_sweep2site(self._h, niter, iter1, abstol, maxbonddim,
                                         0 if sweepstrategy == "backandforth" else 1, int(strictlynested),
                                         int(fillsitetensors)))
 
     def addglobalpivots(self, pivots):
         piv = np.ascontiguousarray(np.asarray(pivots, np.int32).reshape(-1, self.L))
-        _check(lib().orc_tci_addglobalpivots(self._h, piv, piv.shape[0]))
+        self._chk(self._L.orc_tci_addglobalpivots(self._h, piv, piv.shape[0]))
 
     def makecanonical(self, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX):
         self.sweep1site(True, 0.0, 0.0, INT64_MAX, False)
@@ -346,7 +371,7 @@ class OracleTCI2:
         ranks = np.zeros(maxiter, np.int64)
         errors = np.zeros(maxiter)
         nit = C.c_int(0)
-        _check(lib().orc_tci_optimize(self._h, tolerance, maxbonddim, maxiter,
+        self._chk(self._L.orc_tci_optimize(self._h, tolerance, maxbonddim, maxiter,
                                       0 if sweepstrategy == "backandforth" else 1, int(normalizeerror),
                                       ncheckhistory, int(strictlynested), int(checkconvglobalpivot), ranks,
                                       errors, C.byref(nit)))
@@ -354,58 +379,58 @@ class OracleTCI2:
         return ranks[:k].tolist(), errors[:k].tolist()
 
     def Iset(self, p):
-        n = lib().orc_tci_iset_size(self._h, p)
+        n = self._L.orc_tci_iset_size(self._h, p)
         out = np.zeros(max(n * p, 1), np.int32)
-        lib().orc_tci_iset_get(self._h, p, out)
+        self._L.orc_tci_iset_get(self._h, p, out)
         return out[: n * p].reshape(n, p)
 
     def Jset(self, p):
-        n = lib().orc_tci_jset_size(self._h, p)
+        n = self._L.orc_tci_jset_size(self._h, p)
         w = self.L - 1 - p
         out = np.zeros(max(n * w, 1), np.int32)
-        lib().orc_tci_jset_get(self._h, p, out)
+        self._L.orc_tci_jset_get(self._h, p, out)
         return out[: n * w].reshape(n, w)
 
     def linkdims(self):
-        return [int(lib().orc_tci_iset_size(self._h, p + 1)) for p in range(self.L - 1)]
+        return [int(self._L.orc_tci_iset_size(self._h, p + 1)) for p in range(self.L - 1)]
 
     def rank(self):
         return max(self.linkdims())
 
     @property
     def maxsamplevalue(self):
-        return lib().orc_tci_maxsample(self._h)
+        return self._L.orc_tci_maxsample(self._h)
 
     @property
     def pivoterrors(self):
         out = np.zeros(1 << 16)
-        n = lib().orc_tci_pivoterrors(self._h, out, len(out))
+        n = self._L.orc_tci_pivoterrors(self._h, out, len(out))
         return out[:n].copy()
 
     @property
     def bonderrors(self):
         out = np.zeros(self.L - 1)
-        lib().orc_tci_bonderrors(self._h, out)
+        self._L.orc_tci_bonderrors(self._h, out)
         return out
 
     def pivoterror(self):
         return float(np.max(self.bonderrors))
 
     def sitetensor(self, p):
-        n = lib().orc_tci_sitetensor_size(self._h, p)
+        n = self._L.orc_tci_sitetensor_size(self._h, p)
         out = np.zeros(max(n, 1))
-        lib().orc_tci_sitetensor(self._h, p, out)
-        a = lib().orc_tci_iset_size(self._h, p)
-        b = lib().orc_tci_jset_size(self._h, p)
+        self._L.orc_tci_sitetensor(self._h, p, out)
+        a = self._L.orc_tci_iset_size(self._h, p)
+        b = self._L.orc_tci_jset_size(self._h, p)
         return out[:n].reshape((a, self.localdims[p], b), order="F")
 
     def evaluate(self, idx):
         v = C.c_double()
-        _check(lib().orc_tci_evaluate(self._h, np.ascontiguousarray(idx, np.int32), C.byref(v)))
+        self._chk(self._L.orc_tci_evaluate(self._h, np.ascontiguousarray(idx, np.int32), C.byref(v)))
         return v.value
 
 
-def crossinterpolate2(kind, params, localdims, initialpivots=None, **kw):
-    t = OracleTCI2(kind, params, localdims, initialpivots)
+def crossinterpolate2(kind, params, localdims, initialpivots=None, fast=False, **kw):
+    t = OracleTCI2(kind, params, localdims, initialpivots, fast=fast)
     ranks, errors = t.optimize(**kw)
     return t, ranks, errors

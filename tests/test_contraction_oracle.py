@@ -3,7 +3,8 @@
 Pinned by the reference's own properties (test/test_contraction.jl): the contraction of two MPOs
 evaluates to the product of their matrices (`_tomat(ab) ≈ _tomat(a) * _tomat(b)`, :94), also for
 an MPO times an MPS (:175-176), on the reference's test shapes (N = 4, bonds [1,2,3,2,1], local
-dims 2 x 3 x 2). The reference draws complex random cores; Float64 cores here.
+dims 2 x 3 x 2). The reference draws complex random cores; the Float64 tests use real ones, the
+ComplexF64 ones at the end complex ones.
 """
 import itertools
 
@@ -121,3 +122,45 @@ def test_contract_zipup_svd_is_matrix_product():
     A, B = gen_tto_tto(seed=5)
     ab = contract_zipup(A, B, method="SVD")
     np.testing.assert_allclose(tomat(ab), tomat(A) @ tomat(B), rtol=1e-10, atol=1e-12)
+
+
+def gen_complex_tto_tto(seed=0, N=4, bonds=(1, 2, 3, 2, 1), d1=2, d2=3, d3=2):
+    """_gen_testdata_TTO_TTO (test_contraction.jl:31-50): rand(ComplexF64, ...) cores."""
+    rng = np.random.default_rng(seed)
+    c = lambda *s: rng.random(s) + 1j * rng.random(s)  # noqa: E731
+    A = [c(bonds[n], d1, d2, bonds[n + 1]) for n in range(N)]
+    B = [c(bonds[n], d2, d3, bonds[n + 1]) for n in range(N)]
+    return A, B
+
+
+def test_realified_complex_contraction_is_the_complex_product():
+    """The identity the device's Contraction{ComplexF64} rests on (tci_amd.contraction._realify):
+    with both operators realified (2x2 real blocks, bonds doubled; X_re, X_im real MPOs of Re X,
+    Im X), Re(A B) = A_re B_re - A_im B_im and Im(A B) = A_im B_re + A_re B_im, each a REAL MPO
+    contraction."""
+    from tci_amd.contraction import _realify
+    for N, bonds in ((4, (1, 2, 3, 2, 1)), (1, (1, 1)), (2, (1, 3, 1))):
+        A, B = gen_complex_tto_tto(seed=N, N=N, bonds=bonds)
+        ref = tomat(A) @ tomat(B)
+        Are, Aim = _realify(A)
+        Br, Bi = _realify(B)
+        np.testing.assert_allclose(tomat(Are) + 1j * tomat(Aim), tomat(A), rtol=1e-13, atol=1e-14)
+        re = tomat(Are) @ tomat(Br) - tomat(Aim) @ tomat(Bi)
+        im = tomat(Aim) @ tomat(Br) + tomat(Are) @ tomat(Bi)
+        np.testing.assert_allclose(re + 1j * im, ref, rtol=1e-13, atol=1e-13)
+        # ... and the oracle's real MPO evaluation of one part agrees with it
+        p = _mpo_params(Are, Br)
+        X = np.array(list(itertools.product(*[range(1, 5)] * N))[:40], np.int32)
+        vals = np.array([O.feval(F_MPO, p, [4] * N, x) for x in X])
+        want = np.array([fused_index_value(tomat(Are) @ tomat(Br), x, [2] * N, [2] * N) for x in X])
+        np.testing.assert_allclose(vals, want, rtol=1e-13, atol=1e-14)
+
+
+def test_complex_naive_and_zipup_svd():
+    """contract(...; :naive) and :zipup (:SVD) of ComplexF64 operands (test_contraction.jl:68-98,
+    185-195) are exact products on the host."""
+    A, B = gen_complex_tto_tto(seed=3)
+    ref = tomat(A) @ tomat(B)
+    np.testing.assert_allclose(tomat(contract_naive(A, B)), ref, rtol=1e-12)
+    from tci_amd.contraction import contract_zipup
+    np.testing.assert_allclose(tomat(contract_zipup(A, B, method="SVD")), ref, rtol=1e-10, atol=1e-12)

@@ -254,3 +254,59 @@ def test_sharded_global_search_gloo(tmp_path, world):
     for r in range(world):
         res = json.load(open(tmp_path / f"rank{r}.json"))
         assert all(res.values()), (r, res)
+
+
+class _RaisesOnLastRank(OracleEvaluator):
+    """Test-only evaluator whose f fails on the last rank's column block only (a user's f raising
+    for some inputs, as a HostFunctionEvaluator's callback may)."""
+
+    def __init__(self, rank, world, *a):
+        super().__init__(*a)
+        self.fail = rank == world - 1
+
+    def pi(self, I, J, M=0):
+        if self.fail:
+            raise ValueError("f failed on this rank's columns")
+        return super().pi(I, J, M)
+
+
+def _fail_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ld = [6] * 6
+        I = np.array([[1, 2]] * 5, np.int32)
+        J = np.array([[1, 2, 3, 4]] * 11, np.int32)
+        f = ShardedBatchEvaluator(_RaisesOnLastRank(rank, world, 1, [1.0], ld), Comm(device="cpu"))
+        res = {}
+        try:
+            f.pi(I, J, 0)
+            res["raised"] = None
+        except ValueError as e:
+            res["raised"] = "own:" + str(e)
+        except RuntimeError as e:
+            res["raised"] = "other:" + str(e)
+        # the group is still usable afterwards (nobody is left inside a collective)
+        ok = ShardedBatchEvaluator(OracleEvaluator(1, [1.0], ld), Comm(device="cpu"))
+        full, _ = ok.pi(I, J, 0)
+        res["after"] = bool(np.array_equal(full, OracleEvaluator(1, [1.0], ld).pi(I, J, 0)[0]))
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_failure_raises_on_every_rank(tmp_path, world):
+    """a batch evaluation failing on one rank only must raise on every rank (the flag
+    travels in the max|Pi| reduction before any data collective), not leave the others blocked."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        want = "own:" if r == world - 1 else "other:"
+        assert res["raised"] and res["raised"].startswith(want) and res["after"], (r, res)

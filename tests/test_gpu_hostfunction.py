@@ -209,3 +209,39 @@ def test_host_function_complex_scaled(ctx):
     assert r1 == r2 and e1 == e2
     for p in range(len(ld)):
         assert np.array_equal(t1.Iset[p], t2.Iset[p])
+
+
+def test_checkbatchevaluatable_accepts_every_host_evaluator(ctx):
+    """checkbatchevaluatable=true accepts any BatchEvaluator (tensorci2.jl:1044): the pointwise and
+    threaded HostFunctionEvaluator forms expose the batch interface too."""
+    ld = [6] * 4
+    ref = None
+    for kw in ({}, {"threads": 2}, {"vectorized": True}):
+        fn = lorentz_vec if kw.get("vectorized") else lorentz_point
+        f = T.HostFunctionEvaluator(fn, ld, ctx=ctx, **kw)
+        tci, ranks, errors = T.crossinterpolate2(f, tolerance=1e-10, maxiter=4, nsearchglobalpivot=0,
+                                                 checkbatchevaluatable=True)
+        ref = ref or (ranks, errors)
+        assert (ranks, errors) == ref
+
+
+def test_failed_native_sweep_leaves_mirror_on_native_state(ctx):
+    """when a native sweep fails part-way (here the host f raises in the second
+    iteration), the Python mirror must show the native object's half-updated sets -- as the
+    reference's TensorCI2 is left half-updated when a sweep throws -- not the stale copy."""
+    ld = [5] * 5
+    calls = [0]
+
+    def f(X):
+        calls[0] += 1
+        if calls[0] == 16:  # 1 (initial pivot) + 8 bonds + 5 Pi1 in iteration 1; then mid-sweep
+            raise KeyError("boom")
+        return lorentz_vec(X)
+
+    fh = T.HostFunctionEvaluator(f, ld, ctx=ctx, vectorized=True)
+    tci = T.TensorCI2.from_function(fh, ld, None)
+    with pytest.raises(KeyError):
+        tci.optimize(fh, tolerance=1e-12, maxiter=4, nsearchglobalpivot=0)
+    assert getattr(tci, "_native_h", None) is not None
+    native = [tci._native_counts(0)[p] for p in range(len(ld))]
+    assert [len(s) for s in tci.Iset] == native
