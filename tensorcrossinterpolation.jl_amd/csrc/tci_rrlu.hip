@@ -1699,6 +1699,9 @@ constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
 #ifndef TCI_XSTAGE
 #define TCI_XSTAGE 128
 #endif
+#ifndef TCI_PX_EXP
+#define TCI_PX_EXP 0  // A/B timing probes of the deep write-back's LDS traffic (1: x, 2: y, 3: both); 0 in builds
+#endif
 constexpr int kXStage = TCI_XSTAGE;  // staged columns per group
 constexpr int kXU = 4;        // columns per chunk (two chunks in flight per lane)
 constexpr int kXSlices = kXHalf / 128;
@@ -1855,9 +1858,17 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 }
                 if (!any) return;
                 for (int s = 0; s < P; ++s) {
+#if TCI_PX_EXP & 1  // timing experiment only (wrong values): no LDS read of the x's
+                    const double2 x = double2{1.0 + s, 0.5 * s};
+#else
                     const double2 x = *reinterpret_cast<const double2*>(&L.xs[s * kXHalf + lr]);
+#endif
+#if TCI_PX_EXP & 2  // timing experiment only: no LDS read of the y's
+                    const double2 y01 = double2{0.25 * s, 0.125 * s}, y23 = double2{0.75 * s, 0.375};
+#else
                     const double2 y01 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU]);
                     const double2 y23 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU + 2]);
+#endif
                     const double y[kXU] = {y01.x, y01.y, y23.x, y23.y};
 #pragma unroll
                     for (int u = 0; u < kXU; ++u) {
