@@ -265,6 +265,7 @@ def main():
 
     if not args.no_extras:
         sh = sharded_pi(T, ctx, dist, world, rank)
+        shq = sharded_pi(T, ctx, dist, world, rank, "quantics_osc")
         try:  # a failure of the multi-GPU extras must not cost the headline line
             shr = sharded_extras(T, ctx, dist, world, rank, dev_res if rank == 0 else None)
         except Exception as e:  # noqa: BLE001
@@ -273,6 +274,7 @@ def main():
         if rank == 0:
             out["extras"] = extras(T, ctx)
             out["extras"]["pi_lorentz_sharded"] = sh
+            out["extras"]["pi_quantics_sharded"] = shq
             out["extras"].update(shr)
             # the paths that shard, as strong-scaling lines next to the replica
             # headline: fixed total work over N ranks, max-over-ranks time
@@ -283,6 +285,8 @@ def main():
                     "pivots_equal_unsharded": rec.get("pivots_equal_unsharded")}
             lines["pi_lorentz_sharded_8192x8192"] = {"value": sh["pi_rows_per_s"], "unit": "Pi-rows/s",
                                                      "ms": sh["ms_per_pi"]}
+            lines["pi_quantics40_sharded_8192x8192"] = {"value": shq["pi_rows_per_s"], "unit": "Pi-rows/s",
+                                                        "ms": shq["ms_per_pi"]}
             if "pi_sharded_with_gather" in shr:
                 g = shr["pi_sharded_with_gather"]
                 lines["pi_lorentz_gathered_8192x8192"] = {"value": g["pi_rows_per_s"], "unit": "Pi-rows/s",
@@ -362,20 +366,24 @@ def sharded_extras(T, ctx, dist, world, rank, full_res):
         ctx.check(ctx.lib.tci_fill_uniform_block_d(ctx.h, A0.ptr, m, nloc, A0.ld, 0, m * j0))
         W = T.DeviceMatrix(m, nloc + 1, ctx=ctx)
         W.copy_from(A0)
-        out = rrlu_sharded(W, m, n, j0, nloc, comm=dcomm, maxrank=r)  # warm-up (+ pivots for parity)
+        # one rank has nothing to exchange: the sharded driver then commits in the pass tail
+        xc = dcomm if world > 1 else None
+        out = rrlu_sharded(W, m, n, j0, nloc, comm=xc, maxrank=r)  # warm-up (+ pivots for parity)
         times = []
         for _ in range(reps):
             W.copy_from(A0)
             barrier()
             t0 = time.perf_counter()
-            rrlu_sharded(W, m, n, j0, nloc, comm=dcomm, maxrank=r)
+            rrlu_sharded(W, m, n, j0, nloc, comm=xc, maxrank=r)
             barrier()
             times.append(time.perf_counter() - t0)
         dt = tmax(min(times))
         rec = {"m": m, "n": n, "r": r, "ranks": world, "npivot": out[0], "ms": round(dt * 1e3, 3),
                "GFLOPs": round(rrlu_flops(m, n, out[0]) / dt / 1e9, 1),
-               "exchange": "candidate first: all-gather of 32-B candidates, then the winning column from "
-                           "its owner by an element-wise uint64 max (DESIGN.md 7)",
+               "exchange": ("candidate first: all-gather of 32-B candidates, then the winning column from "
+                            "its owner by an element-wise uint64 max (DESIGN.md 7)") if world > 1 else
+                           "none (one rank: the pass tail commits, as unsharded)",
+               "epochs": ctx.lib.tci_rrlu_epochs_for(ctx.h, m, n),
                "exchange_bytes_per_pivot": {"allgather_candidates": 32 * world, "allreduce_column": 8 * (m + 32)}}
         A0.free()
         W.free()
@@ -430,27 +438,36 @@ def sharded_extras(T, ctx, dist, world, rank, full_res):
     return res
 
 
-def sharded_pi(T, ctx, dist, world, rank):
-    """Pi assembly of one 8192 x 8192 Lorentzian Pi (L = 20) split by column blocks over the
-    ranks: each rank evaluates its block on its own GPU, maxsample is all-reduced.
-    Strong scaling: Pi-rows/s = m / (max over ranks of the block time)."""
+def sharded_pi(T, ctx, dist, world, rank, kind="lorentz"):
+    """Pi assembly of one 8192 x 8192 Pi split by column blocks over the ranks: each
+    rank evaluates its block on its own GPU, maxsample is all-reduced. Strong scaling: Pi-rows/s =
+    m / (max over ranks of the block time). kind "lorentz": L = 20 legs of d = 10 (config 1's
+    integrand, HBM-write-bound); "quantics_osc": config 4's integrand, L = 40 legs of d = 2
+    (fp64-VALU-bound: the Pi that shards; config 4's own TCI2 Pi are <= 30^2 and run as replicas)."""
     import ctypes as C
 
     import torch
 
     m = n = 8192
     rng = np.random.default_rng(1)
-    I = rng.integers(1, 11, (m, 10)).astype(np.int32)
-    J = rng.integers(1, 11, (n, 10)).astype(np.int32)
+    if kind == "lorentz":
+        I = rng.integers(1, 11, (m, 10)).astype(np.int32)
+        J = rng.integers(1, 11, (n, 10)).astype(np.int32)
+        f = T.lorentz([10] * 20, ctx=ctx)
+    else:
+        rng.integers(1, 11, (m + n, 10))  # the draws of the Lorentzian inputs, as in extras()
+        I = rng.integers(1, 3, (m, 20)).astype(np.int32)
+        J = rng.integers(1, 3, (n, 20)).astype(np.int32)
+        f = T.GPUBatchEvaluator(5, T.batcheval.QOSC_PARAMS, [2] * 40, ctx=ctx)
+    nl, nr = I.shape[1], J.shape[1]
     j0, j1 = T.column_blocks(n, world)[rank]
     Jb = np.ascontiguousarray(J[j0:j1])
-    f = T.lorentz([10] * 20, ctx=ctx)
     dm = T.DeviceMatrix(m, max(j1 - j0, 1), ctx=ctx)
     mx = C.c_double()
 
     def run():
         if j1 > j0:
-            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(I), m, 10, T._lib.ptr(Jb), j1 - j0, 10,
+            ctx.check(ctx.lib.tci_batcheval_d(ctx.h, f.h, T._lib.ptr(I), m, nl, T._lib.ptr(Jb), j1 - j0, nr,
                                               0, dm.ptr, dm.ld, C.byref(mx)))
         else:
             mx.value = 0.0
@@ -470,7 +487,7 @@ def sharded_pi(T, ctx, dist, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, gmx = float(t[0]), float(t[1])
     dm.free()
-    return {"m": m, "n": n, "L": 20, "ranks": world, "pi_rows_per_s": round(m / dt, 1),
+    return {"m": m, "n": n, "L": nl + nr, "ranks": world, "pi_rows_per_s": round(m / dt, 1),
             "ms_per_pi": round(dt * 1e3, 4), "maxsample": gmx,
             "note": "column blocks per rank, allreduce(max) of maxsample, no gather (strong scaling)"}
 
@@ -797,7 +814,7 @@ def tci2_configs():
     cs = TC.configs()
     out = {}
     for name in ("C1_lorentz8d_parity", "C1_lorentz8d_default", "C3_gauss20d", "C3_gaussmix20d", "C4_qosc40",
-                 "C5_cp12d_K256"):
+                 "C5_cp12d_K256", "C5_cp12d_K1024"):
         rec = cs[name]()
         rec.pop("linkdims", None)
         out[name] = rec

@@ -109,9 +109,21 @@ def configs():
         tci, ranks, errors = T.crossinterpolate2(f, [d] * L, [p0], tolerance=1e-10, maxbonddim=1024,
                                                  maxiter=3, nsearchglobalpivot=0)
         wall = time.perf_counter() - t0
-        return {"config": "C5: 12d CP-rank-1024 synthetic d=32 tol=1e-10 maxbonddim=1024 maxiter=3",
-                "wall_s": round(wall, 3), "iterations": len(ranks), "ranks": ranks,
-                "final_error": errors[-1], "linkdims": tci.linkdims()}
+        res = {"config": "C5: 12d CP-rank-1024 synthetic d=32 tol=1e-10 maxbonddim=1024 maxiter=3",
+               "wall_s": round(wall, 3), "iterations": len(ranks), "ranks": ranks,
+               "final_error": errors[-1], "linkdims": tci.linkdims()}
+        gp = os.path.join(ROOT, "tests", "golden", "c5_golden.json")
+        if os.path.exists(gp):  # the committed oracle result (tests/golden/make_c5_golden.py)
+            import json as _json
+            g = _json.load(open(gp))
+            r = g["result"]
+            res["oracle_golden"] = {
+                "same_initial_pivot": [p0] == g["initialpivots"],
+                "ranks_equal": list(ranks) == r["ranks"], "linkdims_equal": tci.linkdims() == r["linkdims"],
+                "max_abs_error_diff": float(np.max(np.abs(np.asarray(errors) - np.asarray(r["errors"])))),
+                "identical_Isets": int(sum(tci.Iset[q].tolist() == r["Iset"][q] for q in range(L))),
+                "oracle": g.get("oracle")}
+        return res
     out["C5_cp12d_K1024"] = cp12_full
 
     def mpo_contract():

@@ -752,8 +752,14 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     if ((st = ensure(c, &c->colpos, &c->capColpos, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->colposL, &c->capColposL, (size_t)nloc + 2))) return st;
     if ((st = ensure(c, &c->cand, &c->capCand, (size_t)kMaxGrid + 8))) return st;  // + the XCD-class candidates
+    // one rank without a communicator: nothing to exchange -- the pass tail commits as in
+    // rrlu_device (no candidate record, no ghost column: the pivot column is this rank's own). With a
+    // communicator (even of one rank) every pivot goes through the exchange.
     const bool multi = nranks > 1 || comm || exch;
-    if (!multi && nranks != 1) return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
+    if (nranks < 1 || (nranks > 1 && !comm && !exch))
+        return set_err(c, TCI_ERR_ARG, "rrlu_sharded: more than one rank needs a comm or exchange");
+    if (!multi && (c0 != 0 || nloc != n))
+        return set_err(c, TCI_ERR_ARG, "rrlu_sharded: a single rank must hold every column");
     if ((st = ensure(c, &c->lout, &c->capLout, (size_t)nranks + 1))) return st;  // [own, all-gathered ...]
     const int64_t cw = tci::shard_col(m);
     if (multi) {
@@ -810,7 +816,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     g.abstol = abstol;
     g.ticket = c->ticket;
     g.selk = 0;
-    g.lout = c->lout;
+    g.lout = multi ? c->lout : nullptr;
     g.pc_off = c0;
     const bool shadow = c->shadow && lda % 4 == 0;
     g.S = nullptr;
@@ -827,35 +833,48 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     uint64_t* colsend = reinterpret_cast<uint64_t*>(c->shsend);
     uint64_t* colrecv = multi ? reinterpret_cast<uint64_t*>(c->shrecv) : nullptr;
     auto select = [&](int selk) -> int {
-        if (multi) {
+        if (!multi) return TCI_OK;  // committed by the pass tail
+        {
             int e = shard_exchange(c, comm, exch, user, 0, c->lout, recvC, 4);
             if (e) return e;
             tci::launch_shard_pick(c->stream, recvC, nranks, dA, lda, mi, c->ybuf, ldy, c0, (int)nloc, colsend);
             if ((e = shard_exchange(c, comm, exch, user, 1, colsend, colrecv, cw))) return e;
         }
-        tci::launch_shard_commit(c->stream, recvC, multi ? nranks : 1, colrecv, mi, selk, c->st, reltol, abstol,
+        tci::launch_shard_commit(c->stream, recvC, nranks, colrecv, mi, selk, c->st, reltol, abstol,
                                  c->rowpos, c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0, (int)nloc,
                                  dA, lda, c->ybuf, ldy);
         return TCI_OK;
     };
+    // the two-level epoch of rrlu_device, decided by the GLOBAL shape so that every
+    // rank runs the same schedule (the ghost column carries all kMaxPendR pending y's of the pivot)
+    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15)
+                           ? std::max(1, std::min(rrlu_epochs(c, m, n), tci::kMaxPendR / nb)) : 1;
+    const int nbx = nb * epochs;
+    g.nbs = nb;
+    g.pe = g.ps = 0;
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // local argmax of A
     if ((st = select(0))) return st;
-    int64_t k = 0, chunk = 2, t0 = 0;
+    int64_t k = 0, chunk = 2, te = 0, ts = 0;  // first pivot pending in fp64 / in the shadow
     StopPoll poll(c, c->st);
     while (k < mr) {
         const int64_t kend = std::min<int64_t>(k + chunk, mr);
         for (int64_t kk = k; kk < kend; ++kk) {
-            const int P = (int)(kk - t0) + 1;
-            const bool flush = (P >= nb) && (kk + 1 < mr);
+            const int PE = (int)(kk - te) + 1, PS = (int)(kk - ts) + 1;
+            const bool last = kk + 1 >= mr;
+            const bool flush = PE >= nbx && !last;
+            const bool refresh = !flush && epochs > 1 && PS >= nb && !last;
             g.k = (int)kk;
-            g.selk = (kk + 1 < mr) ? (int)(kk + 1) : -1;
+            g.pe = PE;
+            g.ps = PS;
+            g.selk = !last ? (int)(kk + 1) : -1;
             g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
             const bool sampled = kk % c->timing_stride == 0;
-            ev_begin(c, flush ? 0 : 2, sampled, flush ? -1 : 3 + P);
-            tci::launch_pass(c->stream, P, flush, shadow, g, grid);
+            ev_begin(c, flush ? 0 : refresh ? 23 : 2, sampled, flush || refresh ? -1 : (PE > PS ? 24 : 3) + PS);
+            tci::launch_pass(c->stream, PE, flush, shadow, g, grid, flush ? 1 : refresh ? 2 : 0);
             ev_end(c, sampled);
             if (g.selk >= 0 && (st = select(g.selk))) return st;
-            if (flush) t0 = kk + 1;
+            if (flush) te = ts = kk + 1;
+            if (refresh) ts = kk + 1;
         }
         k = kend;
         if (k >= mr) break;

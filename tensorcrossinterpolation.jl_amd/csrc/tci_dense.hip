@@ -648,8 +648,11 @@ __global__ __launch_bounds__(256) void k_getrf_swap(double* __restrict__ A, int 
         int pos0 = l < nbp ? jb + l : -1, src0 = pos0;
         int pos1 = -1, src1 = -1;
         int n = nbp;
+        // every interchange loaded at once (lane k holds piv[jb + k], nbp <= 64), read back by
+        // readlane: a load per step inside the loop was a dependent round trip per interchange
+        const int pl = l < nbp ? piv[jb + l] : 0;
         for (int k = 0; k < nbp; ++k) {
-            const int p = piv[jb + k];
+            const int p = __builtin_amdgcn_readlane(pl, k);
             const unsigned long long b0 = __ballot(pos0 == p), b1 = __ballot(pos1 == p);
             int qp;
             if (b0) qp = __ffsll((long long)b0) - 1;

@@ -1703,7 +1703,11 @@ constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
 #define TCI_PX_EXP 0  // A/B timing probes of the deep write-back's LDS traffic (1: x, 2: y, 3: both); 0 in builds
 #endif
 constexpr int kXStage = TCI_XSTAGE;  // staged columns per group
-constexpr int kXU = 4;        // columns per chunk (two chunks in flight per lane)
+#ifndef TCI_XU
+#define TCI_XU 4
+#endif
+constexpr int kXU = TCI_XU;   // columns per chunk (two chunks in flight per lane); 4 or 8
+static_assert(kXU == 4 || kXU == 8, "chunks of 4 or 8 columns (cb is a multiple of 8)");
 constexpr int kXSlices = kXHalf / 128;
 constexpr int kXReps = kP2Threads / 64 / kXSlices;
 struct PxLds {
@@ -1863,13 +1867,17 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
 #else
                     const double2 x = *reinterpret_cast<const double2*>(&L.xs[s * kXHalf + lr]);
 #endif
+                    double y[kXU];
+#pragma unroll
+                    for (int u = 0; u < kXU; u += 2) {
 #if TCI_PX_EXP & 2  // timing experiment only: no LDS read of the y's
-                    const double2 y01 = double2{0.25 * s, 0.125 * s}, y23 = double2{0.75 * s, 0.375};
+                        const double2 yy = double2{0.25 * s + u, 0.125 * s};
 #else
-                    const double2 y01 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU]);
-                    const double2 y23 = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU + 2]);
+                        const double2 yy = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU + u]);
 #endif
-                    const double y[kXU] = {y01.x, y01.y, y23.x, y23.y};
+                        y[u] = yy.x;
+                        y[u + 1] = yy.y;
+                    }
 #pragma unroll
                     for (int u = 0; u < kXU; ++u) {
                         v[u].x = __dsub_rn(v[u].x, __dmul_rn(x.x, y[u]));

@@ -79,26 +79,31 @@ def ctx():
 
 
 @pytest.mark.parametrize("name", list(_cases()))
-@pytest.mark.parametrize("shadow", [1, 0])
-def test_sharded_one_rank_bitwise(ctx, name, shadow):
+@pytest.mark.parametrize("shadow,epochs", [(1, 0), (0, 0), (1, 3)])
+def test_sharded_one_rank_bitwise(ctx, name, shadow, epochs):
+    """epochs 3: the two-level epoch (refresh passes, EXT passes, the deep write-back) in the
+    sharded driver; 0: the by-shape default (1 at these sizes)."""
     A, kw = _cases()[name]
     ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, shadow))
+    ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, epochs))
     try:
         out = _run_rank(ctx, A, 0, 1, kw)
         L, U = rrlu_sharded_factors(ctx, A.shape[0], A.shape[1], out[0])
     finally:
         ctx.check(ctx.lib.tci_set_rrlu_shadow(ctx.h, 1))
+        ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, 0))
     res = _check(A, kw, out, L, U)
     assert all(res.values()), res
 
 
-def _multi_worker(rank, world, port, outdir, mode):
+def _multi_worker(rank, world, port, outdir, mode, epochs=0):
     import torch.distributed as dist
 
     sys.path.insert(0, HERE)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         ctx = T.Context(0)
+        ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, epochs))
         host = Comm(device="cpu")
         comm = exchange = None
         if mode == "rccl":
@@ -120,11 +125,13 @@ def _multi_worker(rank, world, port, outdir, mode):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,mode", [(2, "host"), (3, "host"), (1, "rccl")])
-def test_sharded_multi_rank_bitwise(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,epochs", [(2, "host", 0), (3, "host", 0), (1, "rccl", 0), (2, "host", 3),
+                                               (1, "rccl", 3)])
+def test_sharded_multi_rank_bitwise(tmp_path, world, mode, epochs):
+    """epochs 3: the two-level epoch across ranks (the ghost column carries every exact-pending y)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_multi_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    mp.spawn(_multi_worker, args=(world, _free_port(), str(tmp_path), mode, epochs), nprocs=world, join=True)
     for r in range(world):
         res = json.load(open(tmp_path / f"rank{r}.json"))
         bad = {k: v for k, v in res.items() if not all(v.values())}
