@@ -122,7 +122,10 @@ def configs():
                 "ranks_equal": list(ranks) == r["ranks"], "linkdims_equal": tci.linkdims() == r["linkdims"],
                 "max_abs_error_diff": float(np.max(np.abs(np.asarray(errors) - np.asarray(r["errors"])))),
                 "identical_Isets": int(sum(tci.Iset[q].tolist() == r["Iset"][q] for q in range(L))),
-                "oracle": g.get("oracle")}
+                "oracle": g.get("oracle"),
+                # the fast oracle's own run (OpenMP rrLU, factorised CP) on the GPU box's host cores
+                "oracle_wall_s": round(sum(h.get("seconds", 0.0) + h.get("sweep1site_and_outputs_s", 0.0)
+                                           for h in g.get("half_sweep_log", [])), 1)}
         return res
     out["C5_cp12d_K1024"] = cp12_full
 
