@@ -530,7 +530,9 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     // epoch ends with a write-back (round 2's scheme); the exact passes (shadow off) always do.
     // (the refresh is the MFMA search's: shadow epochs of 2 .. 15 pivots -- pass 0 writes the
     // shadow of A and cannot refresh, and the search has at most two K-steps)
-    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15)
+    // (the refresh stores address the whole shadow through one 32-bit buffer offset: <= 4 GB)
+    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15 &&
+                        tci::refresh_fits(g.lds, n))
                            ? std::max(1, std::min(rrlu_epochs(c, m, n), tci::kMaxPendR / nb)) : 1;
     const int nbx = nb * epochs;
     g.nbs = nb;
@@ -847,7 +849,9 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     };
     // the two-level epoch of rrlu_device, decided by the GLOBAL shape so that every
     // rank runs the same schedule (the ghost column carries all kMaxPendR pending y's of the pivot)
-    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15)
+    // (the refresh stores' 32-bit buffer offsets: every rank's shadow <= 4 GB, or no rank refreshes)
+    const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15 &&
+                        tci::refresh_fits(round_up(m, 16), (n + nranks - 1) / nranks + 1))
                            ? std::max(1, std::min(rrlu_epochs(c, m, n), tci::kMaxPendR / nb)) : 1;
     const int nbx = nb * epochs;
     g.nbs = nb;

@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "tci_internal.h"
 
@@ -194,15 +195,30 @@ __global__ __launch_bounds__(64 * WM * WN) void k_dgemm(DgemmArgs g) {
 // of 32 x 32); every form stays within 256 registers per lane so that two waves share a SIMD --
 // the fp64 MFMA pipe needs two issuing waves per SIMD to reach its rate (tci_diag_mfma_f64_ex:
 // 33.5 TF with one wave per SIMD, 72.4 TF with two)
+// TCI_DGEMM_TILE (A/B only): 1 / 2 / 3 force 128 x 128 / 128 x 64 / 64 x 64
+static int dgemm_tile_override() {
+    static const int v = [] {
+        const char* e = getenv("TCI_DGEMM_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 template <bool TB>
 static void dgemm_go(hipStream_t s, DgemmArgs g) {
     const long long t128 = (long long)((g.m + 127) / 128) * ((g.n + 127) / 128);
     const long long t12864 = (long long)((g.m + 127) / 128) * ((g.n + 63) / 64);
-    if (t128 >= 256) {
+    const long long t64 = (long long)((g.m + 63) / 64) * ((g.n + 63) / 64);
+    int ov = dgemm_tile_override();
+    // K <= 32 (a Schur update of depth 32, the getrs / TRSM updates of 32-wide blocks): the C round
+    // trip dominates and four times as many 64 x 64 tiles keep more of it in flight (8192^2, nb 32:
+    // 0.268 vs 0.289 ms, profiles/r04_s6_k3_tile*.json)
+    if (ov == 0 && g.k <= 32 && t64 >= 1024) ov = 3;
+    if (ov == 1 || (ov == 0 && t128 >= 256)) {
         g.tm = (g.m + 127) / 128;
         g.tn = (g.n + 127) / 128;
         hipLaunchKernelGGL((k_dgemm<2, 4, 4, 2, TB>), dim3(g.tm * g.tn), dim3(512), 0, s, g);
-    } else if (t12864 >= 256) {
+    } else if (ov == 2 || (ov == 0 && t12864 >= 256)) {
         g.tm = (g.m + 127) / 128;
         g.tn = (g.n + 63) / 64;
         hipLaunchKernelGGL((k_dgemm<2, 2, 4, 2, TB>), dim3(g.tm * g.tn), dim3(256), 0, s, g);

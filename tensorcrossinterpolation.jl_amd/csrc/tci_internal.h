@@ -119,6 +119,9 @@ int argmax_grid(int m, int n, int k, int cb, int max_grid);
 // bytes per element of the rrLU passes' shadow (2: fp16, scaled per epoch; 4: fp32)
 int shadow_elem_bytes();
 bool shadow_two_level();
+// the MFMA search's refresh stores reach the whole fp16 shadow (lds x n) through one 32-bit buffer
+// offset: the two-level epoch needs lds * n * 2 <= 0xFFFFFFF0 bytes
+inline bool refresh_fits(int64_t lds, int64_t n) { return lds * n * 2 <= (int64_t)0xFFFFFFF0; }
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
 // One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).

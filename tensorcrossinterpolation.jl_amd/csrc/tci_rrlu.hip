@@ -219,7 +219,8 @@ __device__ __forceinline__ void block_reduce_cand(CandR& c) {
 // only there, after every other workgroup has finished reading them.
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
-                             double* pivvals, int64_t rk = -1, int64_t ck = -1);
+                             double* pivvals, int64_t rk = -1, int64_t ck = -1, bool has_mxe = false,
+                             double mxe = 0.0);
 
 __device__ __forceinline__ void store_cand_sc1(Cand* dst, const CandR& c) {
     uint64_t* d = reinterpret_cast<uint64_t*>(dst);
@@ -266,7 +267,7 @@ __device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
 // (sc1 stores + agent-scope ticket), which reduces all of them and commits pivot sel.selk.
 template <int NT>
 __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* __restrict__ cand,
-                                          unsigned long long (&pt)[6], int m, int P, int flush) {
+                                          unsigned long long (&pt)[8], int m, int P, int flush) {
     RrluState* st = sel.st;
     (void)m;
     (void)P;
@@ -323,9 +324,11 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
         if (!last_s) return;
     }
     int64_t rk = -1, ck = -1;
+    double mxe = 0.0;
     if (threadIdx.x == 0) {
         rk = sel.rowphys[sel.selk];
         ck = sel.colphys[sel.selk];
+        mxe = st->maxerror;
     }
     CandR w = threadIdx.x < ncls ? load_cand_sc1(cand + kMaxPassGrid + threadIdx.x) : cand_none();
     __syncthreads();
@@ -333,9 +336,10 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
 #else
     if (threadIdx.x == 0) {
 #if TCI_PASS_PROF
-        for (int i = 0; i < 4; ++i)
-            __hip_atomic_store(&g_pprof[blockIdx.x * 8 + i], pt[i], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < 8; ++i)
+            if (i < 4 || i >= 6)
+                __hip_atomic_store(&g_pprof[blockIdx.x * 8 + i], pt[i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
 #endif
         store_cand_sc1(cand + blockIdx.x, best);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -348,12 +352,14 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     if (!last_s) return;
     // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
     constexpr int CPT = kMaxPassGrid / NT;
-    // the physical row / column at position selk (swapped by the commit): requested with the
-    // candidates, not after them
+    // the physical row / column at position selk (swapped by the commit) and the running maximum
+    // pivot error (the stop test): requested with the candidates, not after them
     int64_t rk = -1, ck = -1;
+    double mxe = 0.0;
     if (threadIdx.x == 0) {
         rk = sel.rowphys[sel.selk];
         ck = sel.colphys[sel.selk];
+        mxe = st->maxerror;
     }
     CandR cs[CPT];
 #pragma unroll
@@ -374,7 +380,7 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
             return;
         }
         commit_pivot(sel.selk, w, st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
-                     sel.colphys, sel.pivvals, rk, ck);
+                     sel.colphys, sel.pivvals, rk, ck, true, mxe);
 #if TCI_PASS_PROF
         __threadfence();
         PPROF(5);
@@ -383,7 +389,7 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
         gp[kMaxPassGrid * 8] = pt[5];
         if (sel.selk == TCI_PASS_PROF || sel.selk == TCI_PASS_PROF + 1) {
             unsigned long long t0min = ~0ull, t0max = 0, t3max = 0, t3min = ~0ull;
-            double s01 = 0, s12 = 0, s23 = 0;
+            double s01 = 0, s12 = 0, s23 = 0, s06 = 0, s61 = 0, s17 = 0, s72 = 0;
             // stream-end times (from the first entry) averaged by XCD (blockIdx % 8) and by
             // dispatch round (blockIdx / 256)
             unsigned long long ex[8] = {}, eq[8] = {};
@@ -403,6 +409,14 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
                 s01 += (double)(t[1] - t[0]);
                 s12 += (double)(t[2] - t[1]);
                 s23 += (double)(t[3] - t[2]);
+                const unsigned long long t6 = __hip_atomic_load(&gp[i * 8 + 6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long t7 = __hip_atomic_load(&gp[i * 8 + 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (t6 && t7) {  // thread 0's sub-phases (k_pass_mf only)
+                    s06 += (double)(t6 - t[0]);
+                    s61 += (double)(t[1] - t6);
+                    s17 += (double)(t7 - t[1]);
+                    s72 += (double)(t[2] - t7);
+                }
             }
             const double us = 0.01, G = (double)gridDim.x;  // 100 MHz ticks
 
@@ -414,6 +428,8 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
                    (double)(t3min - t0min) * us, (double)(t3max - t0min) * us,
                    (double)(pt[4] - t3max) * us, (double)(pt[5] - pt[4]) * us,
                    (double)(pt[5] - t0min) * us);
+            printf("  [k=%d] thread 0: entry->pivot known %.2f | ->end of startup %.2f | ->y's staged %.2f | ->streaming %.2f\n",
+                   sel.selk, s06 / G * us, s61 / G * us, s17 / G * us, s72 / G * us);
             printf("  [k=%d] end by XCD: %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f | by round: %.1f %.1f %.1f %.1f\n",
                    sel.selk, (ex[0] / nx[0] - t0min) * us, (ex[1] / nx[1] - t0min) * us,
                    (ex[2] / nx[2] - t0min) * us, (ex[3] / nx[3] - t0min) * us,
@@ -486,13 +502,27 @@ struct P2Lds {
     double xk[kRowsPerTile];  // shadow search: x_k of the tile's rows (exact examinations)
 };
 
+// Raw buffer stores (the MFMA search's refresh stores): an out-of-range offset is dropped, so a
+// chunk issues a fixed number of stores with no branch around them. (Measured in round 4: the
+// same treatment of the write-back passes' loads and stores made their waits precise but did not
+// make them faster -- 325 us either way; their single-row 8-B stores issued unconditionally cost
+// 60 us per deep write-back -- so those keep their branches.)
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+constexpr int kBufOOB = 0x7ffffff0;  // a buffer offset past every num_records: dropped / reads 0
+// a raw buffer resource over `bytes` bytes at p (gfx9 dword 3: 0x00020000)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+
 // Body of the exact pass (k_pass2). SH: also store the fp32 shadow S of the values this pass
 // leaves as the new stale ones (write-back passes) or reads unmodified (the initial pass, P = 0).
 // Returns false when the factorisation has already stopped.
 template <int P, bool FLUSH, bool SH>
 __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                                            P2Lds<(P > 0 ? P : 1)>& L, CandR& best,
-                                           unsigned long long (&pt)[6]) {
+                                           unsigned long long (&pt)[8]) {
     RrluState* st = sel.st;
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
@@ -746,7 +776,7 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
 template <int P, bool FLUSH, bool SH>
 __global__ __launch_bounds__(kP2Threads) void k_pass2(PassK g, SelArgs sel) {
     __shared__ P2Lds<(P > 0 ? P : 1)> L;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
     CandR best = cand_none();
     if (!pass2_body<P, FLUSH, SH>(g, sel, L, best, pt)) return;
@@ -778,7 +808,7 @@ __global__ __launch_bounds__(kP2Threads) void k_pass2(PassK g, SelArgs sel) {
 template <int P>
 __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel, P2Lds<P>& L,
                                              CandR& best, float eps, double shs,
-                                             unsigned long long (&pt)[6]) {
+                                             unsigned long long (&pt)[8]) {
     RrluState* st = sel.st;
     const int32_t* colpos = sel.colpos;
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev;
@@ -1078,7 +1108,7 @@ __device__ __forceinline__ bool pass_sh_body(const PassK& g, const SelArgs& sel,
 template <int P>
 __global__ __launch_bounds__(kP2Threads) void k_pass_sh(PassK g, SelArgs sel) {
     __shared__ P2Lds<P> L;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
     // error bound of the fp32 search over pending pivots k-P+1 .. k (uniform)
     const double* pv = sel.pivvals;
@@ -1251,10 +1281,68 @@ __device__ __forceinline__ void f16_split(double v, _Float16& hi, _Float16& lo) 
 // them). RF -- a refresh: the pass also writes the shadow of the values it computes (W, updated
 // through pivot k, scaled for the epoch that starts at k + 1; rows outside the trailing block 0),
 // so the next shadow epoch starts without a write-back of the fp64 values.
+// The certificate of a shadow-search pass after pivot k (DESIGN.md K2, two-level epoch): the
+// current shadow epoch started at t0 = k - PS + 1, the exact epoch at te = k - PE + 1, and every
+// shadow epoch in [te, t0) (nbs pivots each) ended with a refresh. In absolute units, with
+// |v| <= Mf the epoch's stale bound, d the error of its shadow against the exact stale values
+// (0 after a write-back or an exact refresh, else the bound of the refresh pass's W) and
+// sumM = sum |pivot_s| over its pending updates:
+//   d + 2^-11 (1 + 2^-9) (Mf + d) + 2^-25 / s     fp16 storage (s the epoch's scale)
+//     + 2^-19 sumM + P 2^-24 / s                   f16 splits, dropped xl yl
+//     + (3P + 4) 2^-23 (Mf + d + 2 sumM)           fp32 accumulation
+// The search runs while that is below 2^-TCI_SH_TIGHT |pivot k| (else the exact body, uniform).
+// Each pass re-derives the decisions of the refreshes before it from the pivot values with this
+// same function, so every pass agrees with what they did.
+struct ShCert {
+    double eps;  // scaled units of the current epoch
+    double shs;  // the current epoch's scale
+    bool ok;
+};
+// the pivot values pv[te - 1 .. k] (PE + 1 <= 33 of them), one load per lane (read back with
+// readlane: a loop of dependent scalar loads cost ~5 us at PE ~ 26, phase profile of round 3); a
+// separate step so that the load goes out first and sh_cert's wait counts only the loads after it
+__device__ __forceinline__ double sh_cert_load(const double* pv, int k, int PE) {
+    const int lane = threadIdx.x & 63, ix = k - PE + lane;
+    const double v = pv[min(max(ix, 0), k)];  // unconditional: no branch around the load
+    return lane <= PE && ix >= 0 ? v : 0.0;
+}
+__device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int nbs) {
+    const int te = k - PE + 1, t0 = k - PS + 1;
+    auto at = [&](int t) { return readlane_dbl(w, t - te + 1); };
+    double d = 0.0;
+    ShCert c{0.0, 0.0, false};
+    for (int e = te;; e += nbs) {
+        const bool cur = e >= t0;
+        const int ke = cur ? k : e + nbs - 1;  // the pass whose certificate this is
+        const int P = ke - e + 1;
+        double sumM = 0.0, maxM = 0.0;
+        for (int t = e; t <= ke; ++t) {
+            sumM += fabs(at(t));
+            maxM = fmax(maxM, fabs(at(t)));
+        }
+        const double s = sh_scale(e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1)));  // sh_bound(pv, e)
+        const double Mfd = fabs(at(e)) + d;
+        const double mag = Mfd + 2.0 * sumM;
+        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 / s + 0x1p-19 * sumM +
+                                        (double)P * 0x1p-24 / s + (double)(3 * P + 4) * 0x1p-23 * mag
+                                  : 0.0;
+        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -TCI_SH_TIGHT);
+        if (cur) {
+            c.eps = ea * s;
+            c.shs = s;
+            return c;
+        }
+        d = c.ok ? ea : 0.0;  // a refresh that could not certify its bound wrote exact values
+    }
+}
+
+// Returns 0 when the factorisation has stopped, 1 after the pass, 2 when the certificate fails
+// (nothing done: the caller runs the exact body). The certificate is derived after the
+// pivot-independent loads are issued, so its pivot-value round trip overlaps theirs.
+constexpr int kMfStop = 0, kMfDone = 1, kMfExact = 2;
 template <int P, bool EXT = false, bool RF = false>
-__device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P, EXT>& L,
-                                             CandR& best, float eps, double shs,
-                                             unsigned long long (&pt)[6]) {
+__device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P, EXT>& L,
+                                            CandR& best, unsigned long long (&pt)[8]) {
     static_assert(P >= 1 && P <= kMfMaxP, "at most two MFMA K-steps per tile");
     using Gm = MfGeom<P, EXT>;
     const int PE = EXT ? g.pe : P;  // exact pending updates; the shadow's are slots off .. PE - 1
@@ -1267,6 +1355,17 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
     const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy, lds = g.lds;
     const int t0 = k - P + 1;
+    // the pivot the previous pass committed, requested before anything else: every chain of this
+    // pass starts from it, and the certificate's pivot values and the prefetches below overlap its
+    // round trip (read after the certificate it was a second round trip on the critical path)
+    // (vector loads: as scalar loads they were waited for by the first kernel-argument reload,
+    // lgkmcnt(0), right after being issued; vmcnt counts in order, so a vector load is waited for
+    // only where it is used)
+    const double certw = sh_cert_load(pv, k, PE);
+    const int st_done = __hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int a = (int)__hip_atomic_load(&st->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int bq = (int)__hip_atomic_load(&st->q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double piv = __hip_atomic_load(&st->pval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slice = wave % kMfSlices, rep = wave / kMfSlices;
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
@@ -1288,17 +1387,15 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         const int it = g0 + (lc >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
     };
+    // Every chunk load is issued unconditionally (a lane past the last column reads the last one,
+    // a lane past the last row tile row 0: approx() masks both), so that a fixed number of memory
+    // instructions follows each chunk's loads and the compiler waits for that chunk alone.
     auto load_chunk = [&](int g0, int gcols, int h, h8v (&v)[2]) {
         const int lc = h * 16 + lcol;
         const int j = lc < gcols ? col_of(g0, lc) : n;
-        if (rload && j < n) {
-            const h8v* p = reinterpret_cast<const h8v*>(sbase + (int64_t)j * lds);
-            v[0] = p[0];
-            v[1] = p[1];
-        } else {
-            v[0] = h8v{};
-            v[1] = h8v{};
-        }
+        const h8v* p = reinterpret_cast<const h8v*>(sbase + (int64_t)(j < n ? j : n - 1) * lds);
+        v[0] = p[0];
+        v[1] = p[1];
     };
     // staging: threads 0 .. 511 (one staged column each); the tile's rows: threads 512 .. 1023
     const bool stager = threadIdx.x < kP2StageCols;
@@ -1308,31 +1405,45 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         if (!stager || lc >= gn * cb) return -1;
         return col_of(g0, lc);
     };
+    // Map loads: every one issued unconditionally at a clamped index and tested afterwards -- with
+    // the test folded into the load's condition (r < m && rowpos[r] > k) each became a branch
+    // with its own wait, four (a refresh: twenty) dependent round trips before the pivot read.
     // wave activity from the rows of its slice (lanes 0..15 x 4: every row once)
-    bool act = false;
+    int rpa[kMfBlk];
 #pragma unroll
-    for (int b = 0; b < kMfBlk; ++b) {
-        const int r = sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3);
-        act |= (r < m && rowpos[r] > k);
-    }
+    for (int b = 0; b < kMfBlk; ++b) rpa[b] = rowpos[min(sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3), m - 1)];
     // refresh: which of the lane's 16 loaded rows are trailing (the others get shadow 0)
-    [[maybe_unused]] unsigned tmask = 0;
+    [[maybe_unused]] int rpt[RF ? 16 : 1];
     if constexpr (RF) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) tmask |= (rl + i < m && rowpos[rl + i] > k ? 1u : 0u) << i;
+        for (int i = 0; i < 16; ++i) rpt[i] = rowpos[min(rl + i, m - 1)];
     }
-    [[maybe_unused]] const float rscale =
-        RF ? (float)(sh_scale(sh_bound(pv, k + 1)) / shs) : 1.0f;  // a power of two: exact
+    // refresh stores: the shadow as one buffer (the host keeps it below 4 GB for refreshes), the
+    // second 16 B of a lane's 32 through a resource 16 B further on (an out-of-range offset stays so)
+    [[maybe_unused]] const int shb = (int)(unsigned)min((int64_t)lds * n * 2, (int64_t)0xFFFFFFF0);
+    [[maybe_unused]] const auto rsS0 = buf_rsrc(g.S, shb);
+    [[maybe_unused]] const auto rsS1 = buf_rsrc(reinterpret_cast<const char*>(g.S) + 16, shb - 16);
     int jst = ntc > 0 ? stage_col(0) : -1;
-    int cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+    const int cpl = colpos[min(max(jst, 0), n - 1)];
     const int prow = threadIdx.x - kP2StageCols;  // this thread's tile row (row threads)
     const int rrow = tb + (prow >= 0 ? prow : 0);
-    const int rpos = (!stager && rrow < m) ? rowpos[rrow] : -1;
+    const int rpl = rowpos[min(rrow, m - 1)];
     h8v va[2], vb[2];
     const int gc0 = ntc > 0 ? min(G, ntc) * cb : 0;
     const int nch0 = (gc0 + 15) / 16;
-    if (rep < nch0) load_chunk(0, gc0, rep, va);
-    if (rep + kMfReps < nch0) load_chunk(0, gc0, rep + kMfReps, vb);
+    // unconditional (no columns: chunk 0 of an empty group reads column n - 1, never used)
+    load_chunk(0, gc0, max(min(rep, nch0 - 1), 0), va);
+    load_chunk(0, gc0, max(min(rep + kMfReps, nch0 - 1), 0), vb);
+    bool act = false;
+#pragma unroll
+    for (int b = 0; b < kMfBlk; ++b) act |= sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3) < m && rpa[b] > k;
+    [[maybe_unused]] unsigned tmask = 0;
+    if constexpr (RF) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmask |= (rl + i < m && rpt[i] > k ? 1u : 0u) << i;
+    }
+    int cpst = (jst >= 0 && jst < n) ? cpl : -1;
+    const int rpos = (!stager && rrow < m) ? rpl : -1;
     // EXT: the pivot-independent side of this thread's chain (row thread: X[s][row]; stager:
     // Y[s][column]), all PE - 1 of them requested before the pivot is read
     [[maybe_unused]] PendPre pre;
@@ -1342,9 +1453,14 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         else
             pend_pre(pre, g.Y + (jst >= 0 && jst < n ? jst : 0), ldy, PE - 1);
     }
-    if (st->done) return false;
-    const int a = (int)st->p, bq = (int)st->q;
-    const double piv = st->pval;
+    const ShCert cert = sh_cert(certw, k, P, PE, g.nbs > 0 ? g.nbs : P);
+    if (!cert.ok) return kMfExact;
+    const float eps = (float)(cert.eps * (1.0 + 0x1p-20));
+    const double shs = cert.shs;
+    [[maybe_unused]] const float rscale =
+        RF ? (float)(sh_scale(sh_bound(pv, k + 1)) / shs) : 1.0f;  // a power of two: exact
+    if (st_done) return kMfStop;
+    PPROF(6);
     // EXT: lane s of every wave holds the pivot's side, X[s][a] (stager waves) or Y[s][bq] (row
     // waves) -- one load per lane, no barrier. The chains that readlane it run on whole waves (the
     // stager / row split is by wave): a spilled upl reloaded under a partial exec mask would leave
@@ -1364,9 +1480,11 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         }
         double xk = g.A[rr + (int64_t)bq * lda];
         if constexpr (EXT) {  // all PE - 1 exact pending updates
-            xk = pend_chain(xk, pre, g.X + rr, ldx, upl, PE - 1);
+            // the shadow-pending x's first: pivot-independent, in flight with the chain's loads
+            // (requested after the chain they were one more round trip before the barrier)
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
+            xk = pend_chain(xk, pre, g.X + rr, ldx, upl, PE - 1);
         } else {
 #pragma unroll
             for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
@@ -1403,6 +1521,9 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
     // EXT: the first staged group's y_k chain here (whole stager waves; columns that are not
     // trailing compute a value nobody reads), so that pre is dead before the streaming loop
     [[maybe_unused]] double yk0 = 0.0;
+    // (Requesting the first group's shadow-pending y's here too, with the chain's loads, would save
+    // the staging's round trip for them, but holding them across the chain spills: 2 VGPRs at
+    // P = 3, 4, 10-14 at P = 9, 10.)
     if constexpr (EXT) {
         if (stager) {
             const int jj = jst >= 0 && jst < n ? jst : 0;
@@ -1431,6 +1552,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const h8v& hv = v[b >> 1];
             const int o = 4 * (b & 1);
             f4v acc = {(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
+            if (!rload) acc = f4v{0.0f, 0.0f, 0.0f, 0.0f};  // rows past the shadow: W = 0
 #pragma unroll
             for (int u = 0; u < KSt; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b][u], bf[u], acc, 0, 0, 0);
             mbs[b] = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
@@ -1442,13 +1564,11 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                     wout[b >> 1][o + t] = (tmask >> (4 * b + t)) & 1u ? (_Float16)(acc[t] * rscale) : (_Float16)0.0f;
             }
         }
-        if constexpr (RF) {
+        if constexpr (RF) {  // buffer stores, dropped out of range: a fixed count per chunk
             const int j = lc < gcols ? col_of(g0r, lc) : n;
-            if (rload && j < n && cp > k) {
-                h8v* p = reinterpret_cast<h8v*>(const_cast<_Float16*>(sbase) + (int64_t)j * lds);
-                p[0] = wout[0];
-                p[1] = wout[1];
-            }
+            const unsigned off = rload && j < n && cp > k ? (unsigned)(((int64_t)j * lds + rl) * 2) : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[0]), rsS0, (int)off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[1]), rsS1, (int)off, 0, 0);
         }
         if (cp <= k) {
 #pragma unroll
@@ -1477,6 +1597,9 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const int j = col_of(g0, lc);
             double v = g.A[r + (int64_t)j * lda];
             const int rp = rowpos[r];
+            // take v now: a load left in flight by the continue below (into a register the
+            // streaming loop reuses) would cost a wait for every load at the loop's head
+            asm volatile("" : "+v"(v));
             if (rp <= k) continue;
             if constexpr (decltype(fast)::value) {
                 if constexpr (Gm::ymem) {
@@ -1550,10 +1673,10 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         if (g0 > 0) {
             jst = stage_col(g0);
             cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
-            if (wact) {
-                if (rep < nch) load_chunk(g0, gcols, rep, va);
-                if (rep + kMfReps < nch) load_chunk(g0, gcols, rep + kMfReps, vb);
-            }
+            // unconditional (an inactive wave loads two chunks it never reads): loads skipped on
+            // some paths into the loop would make its head wait for every load in flight
+            load_chunk(g0, gcols, min(rep, nch - 1), va);
+            load_chunk(g0, gcols, min(rep + kMfReps, nch - 1), vb);
             __syncthreads();
         }
         [[maybe_unused]] double ykg = yk0;  // EXT: this group's y_k chain (whole stager waves)
@@ -1607,6 +1730,7 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
                 }
             }
         }
+        if (g0 == 0) PPROF(7);
         if (threadIdx.x < kMfSlices) L.cnt[threadIdx.x] = 2 * kMfReps;
         if (g0 == 0 && threadIdx.x == 0) L.tau = 0u;
         __syncthreads();
@@ -1620,10 +1744,10 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             }
             PPROF(2);
         }
-        auto grab = [&]() -> int {
+        auto grab = [&]() -> int {  // wave-uniform (an SGPR): the loop's branches stay scalar
             int h = 0;
             if (lane == 0) h = atomicAdd(&L.cnt[slice], 1);
-            return __shfl(h, 0);
+            return __builtin_amdgcn_readfirstlane(h);
         };
         int h0 = rep, h1 = rep + kMfReps;
         float mb0[kMfBlk], mb1[kMfBlk];
@@ -1633,17 +1757,17 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
             const int e0 = h0, e1 = h1;
 #pragma unroll
             for (int b = 0; b < kMfBlk; ++b) mb0[b] = mb1[b] = -1.0f;
+            // approx() of a chunk past the group is inert (-1, no stores). The grabs and loads run
+            // in inactive waves too (a slice's waves share its rows, so they are all inactive and
+            // take nothing from an active one): loads skipped on the way into the loop below would
+            // make its head wait for every load in flight.
+            if (wact) c0 = approx(h0, gcols, va, mb0);
+            h0 = grab();
+            load_chunk(g0, gcols, min(h0, nch - 1), va);
+            if (wact && (RF || EXT || h1 < nch)) c1 = approx(h1, gcols, vb, mb1);
+            h1 = grab();
+            load_chunk(g0, gcols, min(h1, nch - 1), vb);
             if (wact) {
-                if (h0 < nch) {
-                    c0 = approx(h0, gcols, va, mb0);
-                    h0 = grab();
-                    if (h0 < nch) load_chunk(g0, gcols, h0, va);
-                }
-                if (h1 < nch) {
-                    c1 = approx(h1, gcols, vb, mb1);
-                    h1 = grab();
-                    if (h1 < nch) load_chunk(g0, gcols, h1, vb);
-                }
                 float lb = fmaxf(fmaxf(c0, c1) - eps, 0.0f);
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) lb = fmaxf(lb, __shfl_xor(lb, off));
@@ -1658,30 +1782,40 @@ __device__ __forceinline__ bool pass_mf_body(const PassK& g, const SelArgs& sel,
         } else if (!wact) {
             continue;
         }
-        // h0's values in va, h1's in vb; every grab returns a larger index than both
+        // h0's values in va, h1's in vb; every grab returns a larger index than both, so h1 >= nch
+        // only in the last trip. Both halves issue their loads unconditionally: a fixed number of
+        // loads per trip lets each chunk's wait count the other chunk's loads (a skipped half
+        // would force a wait for every outstanding load). The last trip's h1 >= nch skips its
+        // approx() (no loads) in the first-epoch passes: at small sizes (where those are the only
+        // read-only passes) a wave streams one or two chunks, and the dead half would double its
+        // work. A refresh keeps it, inert, for its fixed count of stores, and the EXT passes too
+        // (skipping it there changes their register allocation: prologue spills).
         while (h0 < nch) {
             {
                 const float c = approx(h0, gcols, va, mb0);
                 const int e = h0;
                 h0 = grab();
-                if (h0 < nch) load_chunk(g0, gcols, h0, va);
+                load_chunk(g0, gcols, min(h0, nch - 1), va);
                 test(c);
                 append(g0, e, mb0, tau - tau * margin);
             }
-            if (h1 < nch) {
-                const float c = approx(h1, gcols, vb, mb1);
+            {
                 const int e = h1;
+                float c = -1.0f;
+                if (RF || EXT || e < nch) c = approx(e, gcols, vb, mb1);
                 h1 = grab();
-                if (h1 < nch) load_chunk(g0, gcols, h1, vb);
-                test(c);
-                append(g0, e, mb1, tau - tau * margin);
+                load_chunk(g0, gcols, min(h1, nch - 1), vb);
+                if (RF || EXT || e < nch) {  // (inert past the group: c and mb1 are -1)
+                    test(c);
+                    append(g0, e, mb1, tau - tau * margin);
+                }
             }
         }
         // the latest bound of the workgroup prunes the list
         tau = fmaxf(tau, __uint_as_float(__hip_atomic_load(&L.tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
         flush(g0, std::true_type{});
     }
-    return true;
+    return kMfDone;
 }
 
 // ------------------------------------------------------------------ deep exact pass (two-level epoch)
@@ -1721,7 +1855,7 @@ struct PxLds {
 
 template <int MODE>
 __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, PxLds& L, CandR& best,
-                                           unsigned long long (&pt)[6]) {
+                                           unsigned long long (&pt)[8]) {
     RrluState* st = sel.st;
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
@@ -1762,9 +1896,11 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
             constexpr int kPer = kMaxPendR * kXHalf / kP2Threads;  // 8
             double v[kPer];
 #pragma unroll
-            for (int u = 0; u < kPer; ++u) {
+            for (int u = 0; u < kPer; ++u) {  // unconditional loads (slot < kMaxPendR, row clamped),
+                // masked after: a load inside the condition became a branch + wait each (serial)
                 const int e = threadIdx.x + u * kP2Threads, s = e / kXHalf, rr = e - s * kXHalf;
-                v[u] = (s < P - 1 && hb + rr < m) ? g.X[(int64_t)s * ldx + hb + rr] : 0.0;
+                v[u] = g.X[(int64_t)s * ldx + min(hb + rr, m - 1)];
+                if (!(s < P - 1 && hb + rr < m)) v[u] = 0.0;
             }
 #pragma unroll
             for (int u = 0; u < kPer; ++u) {
@@ -1807,9 +1943,10 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 const int j = lc < gcols ? col_of(g0, lc) : 0;
                 double v[kPer];
 #pragma unroll
-                for (int u = 0; u < kPer; ++u) {
+                for (int u = 0; u < kPer; ++u) {  // unconditional (slot < kMaxPendR), masked after
                     const int s = s0 + u * (kP2Threads / kXStage);
-                    v[u] = (s < P - 1 && lc < gcols) ? g.Y[(int64_t)s * ldy + j] : 0.0;
+                    v[u] = g.Y[(int64_t)s * ldy + j];
+                    if (!(s < P - 1 && lc < gcols)) v[u] = 0.0;
                 }
 #pragma unroll
                 for (int u = 0; u < kPer; ++u) {
@@ -1947,63 +2084,12 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
 template <int MODE>
 __global__ __launch_bounds__(kP2Threads) void k_pass_x(PassK g, SelArgs sel) {
     __shared__ PxLds L;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
     CandR best = cand_none();
     if (!passx_body<MODE>(g, sel, L, best, pt)) return;
     PPROF(3);
     pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, g.pe, MODE);
-}
-
-// The certificate of a shadow-search pass after pivot k (DESIGN.md K2, two-level epoch): the
-// current shadow epoch started at t0 = k - PS + 1, the exact epoch at te = k - PE + 1, and every
-// shadow epoch in [te, t0) (nbs pivots each) ended with a refresh. In absolute units, with
-// |v| <= Mf the epoch's stale bound, d the error of its shadow against the exact stale values
-// (0 after a write-back or an exact refresh, else the bound of the refresh pass's W) and
-// sumM = sum |pivot_s| over its pending updates:
-//   d + 2^-11 (1 + 2^-9) (Mf + d) + 2^-25 / s     fp16 storage (s the epoch's scale)
-//     + 2^-19 sumM + P 2^-24 / s                   f16 splits, dropped xl yl
-//     + (3P + 4) 2^-23 (Mf + d + 2 sumM)           fp32 accumulation
-// The search runs while that is below 2^-TCI_SH_TIGHT |pivot k| (else the exact body, uniform).
-// Each pass re-derives the decisions of the refreshes before it from the pivot values with this
-// same function, so every pass agrees with what they did.
-struct ShCert {
-    double eps;  // scaled units of the current epoch
-    double shs;  // the current epoch's scale
-    bool ok;
-};
-__device__ __forceinline__ ShCert sh_cert(const double* pv, int k, int PS, int PE, int nbs) {
-    const int te = k - PE + 1, t0 = k - PS + 1;
-    // the pivot values pv[te - 1 .. k] (PE + 1 <= 33 of them), one load per lane, read back with
-    // readlane: a loop of dependent scalar loads cost ~5 us at PE ~ 26 (phase profile, round 3)
-    const int lane = threadIdx.x & 63, ix = te - 1 + lane;
-    const double w = (lane <= PE && ix >= 0) ? pv[ix] : 0.0;
-    auto at = [&](int t) { return readlane_dbl(w, t - te + 1); };
-    double d = 0.0;
-    ShCert c{0.0, 0.0, false};
-    for (int e = te;; e += nbs) {
-        const bool cur = e >= t0;
-        const int ke = cur ? k : e + nbs - 1;  // the pass whose certificate this is
-        const int P = ke - e + 1;
-        double sumM = 0.0, maxM = 0.0;
-        for (int t = e; t <= ke; ++t) {
-            sumM += fabs(at(t));
-            maxM = fmax(maxM, fabs(at(t)));
-        }
-        const double s = sh_scale(e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1)));  // sh_bound(pv, e)
-        const double Mfd = fabs(at(e)) + d;
-        const double mag = Mfd + 2.0 * sumM;
-        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 / s + 0x1p-19 * sumM +
-                                        (double)P * 0x1p-24 / s + (double)(3 * P + 4) * 0x1p-23 * mag
-                                  : 0.0;
-        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -TCI_SH_TIGHT);
-        if (cur) {
-            c.eps = ea * s;
-            c.shs = s;
-            return c;
-        }
-        d = c.ok ? ea : 0.0;  // a refresh that could not certify its bound wrote exact values
-    }
 }
 
 template <int P, bool EXT, bool RF>
@@ -2013,19 +2099,19 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
         P2MfLds<P, EXT> f;
         typename std::conditional<(EXT || RF), PxLds, char>::type px;
     } L;
-    [[maybe_unused]] unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
-    const ShCert c = sh_cert(sel.pivvals, g.k, P, EXT ? g.pe : P, g.nbs > 0 ? g.nbs : P);
     CandR best = cand_none();
-    bool go;
-    if (c.ok)
-        go = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, (float)(c.eps * (1.0 + 0x1p-20)), c.shs, pt);
-    else if constexpr (RF)
-        go = passx_body<2>(g, sel, L.px, best, pt);
-    else if constexpr (EXT)
-        go = passx_body<0>(g, sel, L.px, best, pt);
-    else
-        go = pass2_body<P, false, false>(g, sel, L.x, best, pt);
+    const int r = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, pt);
+    bool go = r == kMfDone;
+    if (r == kMfExact) {  // uniform: every workgroup derives the same certificate
+        if constexpr (RF)
+            go = passx_body<2>(g, sel, L.px, best, pt);
+        else if constexpr (EXT)
+            go = passx_body<0>(g, sel, L.px, best, pt);
+        else
+            go = pass2_body<P, false, false>(g, sel, L.x, best, pt);
+    }
     if (!go) return;
     PPROF(3);
     pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, RF ? 2 : 0);
@@ -2131,7 +2217,7 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
 // the columns at k and q (swapcol!, :269-275). One thread.
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
-                             double* pivvals, int64_t rk, int64_t ck) {
+                             double* pivvals, int64_t rk, int64_t ck, bool has_mxe, double mxe) {
     int pr = best.pr, pc = best.pc, rp = best.rpos, cp = best.cpos;
     double val = best.val;
     if (!(best.v >= 0.0)) {
@@ -2145,11 +2231,12 @@ __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double rel
     }
     const double err = fabs(val);
     st->error = err;
-    if (((fabs(err) < reltol * st->maxerror) || (fabs(err) < abstol)) && k > 0) {
+    const double maxerror = has_mxe ? mxe : st->maxerror;  // mxe: requested with the candidates
+    if (((fabs(err) < reltol * maxerror) || (fabs(err) < abstol)) && k > 0) {
         st->done = 1;
         return;
     }
-    st->maxerror = jl_max(st->maxerror, err);
+    st->maxerror = jl_max(maxerror, err);
     st->p = pr;
     st->q = pc;
     st->pval = val;
