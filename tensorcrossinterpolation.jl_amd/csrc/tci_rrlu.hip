@@ -254,6 +254,7 @@ __device__ __forceinline__ CandR load_cand_sc1(const Cand* src) {
 #endif
 #if TCI_PASS_PROF
 __device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
+__shared__ unsigned g_exam_lds;  // exact examinations of this workgroup (k_pass_mf)
 #define PPROF(i) (pt[i] = wall_clock64())
 #else
 #define PPROF(i) ((void)pt)
@@ -340,6 +341,9 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
             if (i < 4 || i >= 6)
                 __hip_atomic_store(&g_pprof[blockIdx.x * 8 + i], pt[i], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g_pprof[blockIdx.x * 8 + 5], (unsigned long long)g_exam_lds, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        g_exam_lds = 0;
 #endif
         store_cand_sc1(cand + blockIdx.x, best);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -428,6 +432,30 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
                    (double)(t3min - t0min) * us, (double)(t3max - t0min) * us,
                    (double)(pt[4] - t3max) * us, (double)(pt[5] - pt[4]) * us,
                    (double)(pt[5] - t0min) * us);
+            {  // the four workgroups that ended streaming last: id, row tile, stream end, examinations
+                int top[4] = {-1, -1, -1, -1};
+                for (int z = 0; z < 4; ++z) {
+                    unsigned long long bestt = 0;
+                    for (int i = 0; i < (int)gridDim.x; ++i) {
+                        if (i == top[0] || i == top[1] || i == top[2]) continue;
+                        const unsigned long long t3 = __hip_atomic_load(&gp[i * 8 + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (t3 >= bestt) { bestt = t3; top[z] = i; }
+                    }
+                }
+                const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
+                for (int z = 0; z < 4; ++z) {
+                    const int i = top[z];
+                    const int wid = xcd_spread(i, (int)gridDim.x);
+                    printf("  [k=%d] late wg %d (row tile %d, q %d): stream end %.2f, staged at %.2f, %llu exact examinations\n",
+                           sel.selk, i, wid % tiles_r, wid / tiles_r,
+                           (double)(__hip_atomic_load(&gp[i * 8 + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0min) * us,
+                           (double)(__hip_atomic_load(&gp[i * 8 + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0min) * us,
+                           __hip_atomic_load(&gp[i * 8 + 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                }
+                unsigned long long tot = 0;
+                for (int i = 0; i < (int)gridDim.x; ++i) tot += __hip_atomic_load(&gp[i * 8 + 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                printf("  [k=%d] exact examinations over the grid: %llu\n", sel.selk, tot);
+            }
             printf("  [k=%d] thread 0: entry->pivot known %.2f | ->end of startup %.2f | ->y's staged %.2f | ->streaming %.2f\n",
                    sel.selk, s06 / G * us, s61 / G * us, s17 / G * us, s72 / G * us);
             printf("  [k=%d] end by XCD: %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f | by round: %.1f %.1f %.1f %.1f\n",
@@ -1226,9 +1254,15 @@ static_assert(kMaxPendR - 1 <= 2 * kPendPre, "two batches");
 struct PendPre {
     double v[kPendPre];
 };
+// Loads unconditional (slots < kMaxPendR always exist), masked after: a load inside `i < cnt`
+// became a branch each, and the other role's branch then began with a wait for all of them.
 __device__ __forceinline__ void pend_pre(PendPre& p, const double* __restrict__ xp, int64_t xst, int cnt) {
+    static_assert(kPendPre <= kMaxPendR, "prefetched slots exist");
 #pragma unroll
-    for (int i = 0; i < kPendPre; ++i) p.v[i] = i < cnt ? xp[(int64_t)i * xst] : 0.0;
+    for (int i = 0; i < kPendPre; ++i) p.v[i] = xp[(int64_t)i * xst];
+#pragma unroll
+    for (int i = 0; i < kPendPre; ++i)
+        if (i >= cnt) p.v[i] = 0.0;
 }
 __device__ __forceinline__ double pend_chain(double v, const PendPre& p, const double* __restrict__ xp,
                                              int64_t xst, double upl, int cnt) {
@@ -1238,8 +1272,7 @@ __device__ __forceinline__ double pend_chain(double v, const PendPre& p, const d
     if (cnt > kPendPre) {
         double r[kMaxPendR - 1 - kPendPre];
 #pragma unroll
-        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i)
-            r[i] = kPendPre + i < cnt ? xp[(int64_t)(kPendPre + i) * xst] : 0.0;
+        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i) r[i] = xp[(int64_t)(kPendPre + i) * xst];
 #pragma unroll
         for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i)
             if (kPendPre + i < cnt) v = __dsub_rn(v, __dmul_rn(r[i], readlane_dbl(upl, kPendPre + i)));
@@ -1303,8 +1336,10 @@ struct ShCert {
 // separate step so that the load goes out first and sh_cert's wait counts only the loads after it
 __device__ __forceinline__ double sh_cert_load(const double* pv, int k, int PE) {
     const int lane = threadIdx.x & 63, ix = k - PE + lane;
-    const double v = pv[min(max(ix, 0), k)];  // unconditional: no branch around the load
-    return lane <= PE && ix >= 0 ? v : 0.0;
+    // unconditional, unmasked: sh_cert reads lanes 0 .. PE only, and lane 0 (pivot te - 1) only
+    // when te >= 1 (for te = 0 it takes |pivot 0| instead), so the clamped lanes are never read
+    (void)lane;
+    return pv[min(max(ix, 0), k)];
 }
 __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int nbs) {
     const int te = k - PE + 1, t0 = k - PS + 1;
@@ -1355,12 +1390,14 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
     const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy, lds = g.lds;
     const int t0 = k - P + 1;
-    // the pivot the previous pass committed, requested before anything else: every chain of this
-    // pass starts from it, and the certificate's pivot values and the prefetches below overlap its
-    // round trip (read after the certificate it was a second round trip on the critical path)
-    // (vector loads: as scalar loads they were waited for by the first kernel-argument reload,
-    // lgkmcnt(0), right after being issued; vmcnt counts in order, so a vector load is waited for
-    // only where it is used)
+    // The certificate's pivot values and the pivot the previous pass committed: the pass's first
+    // loads. The compiler moves the pivot to scalar registers at once, i.e. waits for it right
+    // here -- one round trip, after which the prologue's pivot-independent loads (maps, first
+    // chunks, pending slots) go out together with the pivot-dependent ones. (Requested after the
+    // prefetches instead, that wait also covered the first shadow chunks of the whole grid: +0.2
+    // ms per step; read after the certificate and behind serial map loads, the pivot had been the
+    // third or fourth round trip.) Vector loads: as scalar loads they were waited for by the next
+    // kernel-argument reload (lgkmcnt(0)).
     const double certw = sh_cert_load(pv, k, PE);
     const int st_done = __hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int a = (int)__hip_atomic_load(&st->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1434,24 +1471,16 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // unconditional (no columns: chunk 0 of an empty group reads column n - 1, never used)
     load_chunk(0, gc0, max(min(rep, nch0 - 1), 0), va);
     load_chunk(0, gc0, max(min(rep + kMfReps, nch0 - 1), 0), vb);
-    bool act = false;
-#pragma unroll
-    for (int b = 0; b < kMfBlk; ++b) act |= sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3) < m && rpa[b] > k;
-    [[maybe_unused]] unsigned tmask = 0;
-    if constexpr (RF) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) tmask |= (rl + i < m && rpt[i] > k ? 1u : 0u) << i;
-    }
-    int cpst = (jst >= 0 && jst < n) ? cpl : -1;
-    const int rpos = (!stager && rrow < m) ? rpl : -1;
+    // (the map values are tested where they are first needed, after the pivot-dependent loads have
+    // gone out: tested here, their wait held those loads back by a round trip)
     // EXT: the pivot-independent side of this thread's chain (row thread: X[s][row]; stager:
     // Y[s][column]), all PE - 1 of them requested before the pivot is read
     [[maybe_unused]] PendPre pre;
     if constexpr (EXT) {
-        if (!stager)
-            pend_pre(pre, g.X + (rrow < m ? rrow : 0), ldx, PE - 1);
-        else
-            pend_pre(pre, g.Y + (jst >= 0 && jst < n ? jst : 0), ldy, PE - 1);
+        // one call for both roles (the row threads' x slots, the stagers' y slots): as two
+        // calls under the role's branch, the second began with a wait for the first's loads
+        pend_pre(pre, stager ? g.Y + (jst >= 0 && jst < n ? jst : 0) : g.X + (rrow < m ? rrow : 0),
+                 stager ? ldy : ldx, PE - 1);
     }
     const ShCert cert = sh_cert(certw, k, P, PE, g.nbs > 0 ? g.nbs : P);
     if (!cert.ok) return kMfExact;
@@ -1467,7 +1496,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // the inactive lanes' values undefined.
     [[maybe_unused]] double upl = 0.0;
     if constexpr (EXT) {
-        if (lane < PE - 1) upl = stager ? g.X[(int64_t)lane * ldx + a] : g.Y[(int64_t)lane * ldy + bq];
+        upl = (stager ? g.X + a : g.Y + bq)[(int64_t)min(lane, kMaxPendR - 1) * (stager ? ldx : ldy)];
     }
     if (!stager) {
         // row thread: x_k of its row (the reference's operation order), the split A fragment row
@@ -1491,6 +1520,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         }
         if (leftorth) xk = xk / piv;
         L.xk[prow] = xk;
+        const int rpos = rrow < m ? rpl : -1;  // (a row thread)
         if (q == 0 && rpos > k) {
             g.X[(int64_t)(PE - 1) * ldx + rrow] = xk;
             g.Lp[rrow + (int64_t)k * g.ldl] = xk;
@@ -1531,6 +1561,15 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         }
     }
     PPROF(1);
+    bool act = false;
+#pragma unroll
+    for (int b = 0; b < kMfBlk; ++b) act |= sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3) < m && rpa[b] > k;
+    [[maybe_unused]] unsigned tmask = 0;
+    if constexpr (RF) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmask |= (rl + i < m && rpt[i] > k ? 1u : 0u) << i;
+    }
+    int cpst = (jst >= 0 && jst < n) ? cpl : -1;
     const bool wact = RF || __any(act);  // a refresh rewrites every row's shadow (non-trailing: 0)
     const float margin = 0x1p-20f;
     float tau = 0.0f;
@@ -1633,6 +1672,9 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * Gm::YS + Gm::YS - 1]));
             const double a2 = __dmul_rn(v, v);
             if (a2 >= best.v) cand_take(best, CandR{a2, v, L.cpos[lc], rp, j, r});
+#if TCI_PASS_PROF
+            atomicAdd(&g_exam_lds, 1u);
+#endif
         }
         nex = 0;
     };
@@ -1696,6 +1738,8 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                 double ysv[P];
 #pragma unroll
                 for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)(off + s) * ldy + jst];
+                // (taking them from pre's registers -- they are slots off .. PE - 2 of the column
+                // pre holds -- by a select per slot spills 16-80 VGPRs: pre would stay live here)
                 double yk;
                 if constexpr (EXT) {
                     yk = ykg;
@@ -2101,6 +2145,9 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     } L;
     [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
+#if TCI_PASS_PROF
+    if (threadIdx.x == 0) g_exam_lds = 0;  // (read after the body's barriers)
+#endif
     CandR best = cand_none();
     const int r = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, pt);
     bool go = r == kMfDone;
