@@ -307,7 +307,7 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
 PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 3, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 
