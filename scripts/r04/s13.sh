@@ -1,0 +1,12 @@
+# round-4 call 13: the full -m gpu suite, smoke(), and the full bench line (extras, CPU baseline)
+# of the final build
+set -e
+mkdir -p gpurun_out
+T=r04s13
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gputest.txt 2>&1 || { echo "gputest rc=$?"; tail -30 gpurun_out/${T}_gputest.txt; exit 1; }
+tail -2 gpurun_out/${T}_gputest.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${T}_smoke.txt 2>&1 || { echo "smoke rc=$?"; tail -20 gpurun_out/${T}_smoke.txt; exit 1; }
+tail -1 gpurun_out/${T}_smoke.txt
+timeout -k 10 900 python -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo "bench rc=$?"; tail -20 gpurun_out/${T}_bench.err; exit 1; }
+python -c "import json;d=json.loads(open('gpurun_out/${T}_bench.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],json.dumps(d['roofline'])[:700]);print(json.dumps(d.get('cpu_baseline'))[:300])"
+echo done
