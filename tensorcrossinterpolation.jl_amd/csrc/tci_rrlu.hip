@@ -1881,6 +1881,9 @@ constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
 #define TCI_PX_EXP 0  // A/B timing probes of the deep write-back's LDS traffic (1: x, 2: y, 3: both); 0 in builds
 #endif
 constexpr int kXStage = TCI_XSTAGE;  // staged columns per group
+#ifndef TCI_PX_DRAIN
+#define TCI_PX_DRAIN 0  // deep write-back: explicit drain, then the next chunk's loads, then the arithmetic (A/B)
+#endif
 #ifndef TCI_XU
 #define TCI_XU 4
 #endif
@@ -2109,6 +2112,24 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
             };
             double2 va[kXU], vb[kXU];
             int h0 = rep, h1 = rep + kXReps;
+#if TCI_PX_DRAIN
+            // with the write-back's stores in flight the compiler cannot count loads precisely
+            // (loads and stores share vmcnt), so every use of a chunk waited for vmcnt(0) -- for the
+            // chunk just requested too. Drain explicitly first, then request the next chunk, then
+            // process this one: the request overlaps one chunk of arithmetic
+            if (h0 < nch) load_chunk(h0, va);
+            while (h0 < nch) {
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): va landed, earlier stores done
+                if (h1 < nch) load_chunk(h1, vb);
+                process(h0, va);
+                if (h1 >= nch) break;
+                h0 = grab();
+                __builtin_amdgcn_s_waitcnt(0x0f70);
+                if (h0 < nch) load_chunk(h0, va);
+                process(h1, vb);
+                h1 = grab();
+            }
+#else
             if (h0 < nch) load_chunk(h0, va);
             if (h1 < nch) load_chunk(h1, vb);
             while (h0 < nch) {
@@ -2120,6 +2141,7 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 h1 = grab();
                 if (h1 < nch) load_chunk(h1, vb);
             }
+#endif
         }
     }
     return true;
