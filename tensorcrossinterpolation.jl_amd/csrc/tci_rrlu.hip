@@ -1882,7 +1882,7 @@ constexpr int kXHalf = 256;   // rows whose x's are in LDS at a time
 #endif
 constexpr int kXStage = TCI_XSTAGE;  // staged columns per group
 #ifndef TCI_PX_DRAIN
-#define TCI_PX_DRAIN 0  // deep write-back: explicit drain, then the next chunk's loads, then the arithmetic (A/B)
+#define TCI_PX_DRAIN 1  // deep write-back: explicit drain, then the next chunk's loads, then the arithmetic (0: round-3 order)
 #endif
 #ifndef TCI_XU
 #define TCI_XU 4
