@@ -849,9 +849,12 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     };
     // the two-level epoch of rrlu_device, decided by the GLOBAL shape so that every
     // rank runs the same schedule (the ghost column carries all kMaxPendR pending y's of the pivot)
-    // (the refresh stores' 32-bit buffer offsets: every rank's shadow <= 4 GB, or no rank refreshes)
+    // (the refresh stores' 32-bit buffer offsets: every rank's shadow <= 4 GB, or no rank refreshes.
+    // The test uses the global width n + 1, which bounds every rank's nloc + 1 whatever the split:
+    // all ranks reach the same decision without an exchange, and an unbalanced column block cannot
+    // exceed it -- ADVICE r4)
     const int epochs = (shadow && tci::shadow_two_level() && nb >= 2 && nb <= 15 &&
-                        tci::refresh_fits(round_up(m, 16), (n + nranks - 1) / nranks + 1))
+                        tci::refresh_fits(round_up(m, 16), n + 1))
                            ? std::max(1, std::min(rrlu_epochs(c, m, n), tci::kMaxPendR / nb)) : 1;
     const int nbx = nb * epochs;
     g.nbs = nb;
@@ -913,7 +916,8 @@ int tci_ctx_create(int device, tci_ctx** out) {
     c->device = device;
     if (const char* e = getenv("TCI_RRLU_NB")) c->flush_every = std::max(1, std::min(atoi(e), tci::kMaxPend));
     if (const char* e = getenv("TCI_RRLU_SERP")) c->serpentine = atoi(e) != 0;
-    if (const char* e = getenv("TCI_RRLU_EPOCHS")) c->epochs = std::max(1, std::min(atoi(e), tci::kMaxPendR));
+    // 0 = by shape, as tci_set_rrlu_epochs(0)
+    if (const char* e = getenv("TCI_RRLU_EPOCHS")) c->epochs = std::max(0, std::min(atoi(e), tci::kMaxPendR));
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
@@ -1167,6 +1171,7 @@ int tci_func_create_c128(tci_ctx* c, const tci_func* const* re, int32_t nre, con
                          int32_t nim, tci_func** out) {
     if (!c || !out || nre < 0 || nim < 0 || nre + nim < 1 || (nre && !re) || (nim && !im)) return TCI_ERR_ARG;
     const tci_func* first = nre ? re[0] : im[0];
+    if (!first) return set_err(c, TCI_ERR_ARG, "complex integrand: parts must be real integrands on the same localdims");
     tci_func* f = new tci_func();
     f->ctx = c;
     f->kind = TCI_F_C128;

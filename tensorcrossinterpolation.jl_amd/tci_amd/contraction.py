@@ -91,12 +91,33 @@ def _elementwise(f, vals, dtype=np.float64):
     is a numpy-compatible elementwise function, else element by element."""
     scalar = float if dtype == np.float64 else complex
     try:
-        out = np.asarray(f(vals), dtype)
-        if out.shape == vals.shape:
-            return out
+        raw = np.asarray(f(vals))
     except Exception:
-        pass
-    return np.vectorize(lambda v: scalar(f(scalar(v))), otypes=[dtype])(vals)
+        raw = None
+    if raw is not None and raw.shape == vals.shape:
+        if dtype == np.float64 and np.iscomplexobj(raw):
+            # `res .= obj.f.(res)` into a Float64 array throws InexactError for a value with a
+            # nonzero imaginary part (contraction.jl:571); a silent cast would drop it
+            if np.any(raw.imag != 0):
+                raise InexactError("Contraction{Float64}: f returned a complex value with a nonzero "
+                                   "imaginary part")
+            raw = raw.real
+        return np.asarray(raw, dtype)
+
+    def one(v):
+        r = f(scalar(v))
+        if dtype == np.float64 and isinstance(r, complex):
+            if r.imag != 0:
+                raise InexactError("Contraction{Float64}: f returned a complex value with a nonzero "
+                                   "imaginary part")
+            r = r.real
+        return scalar(r)
+
+    return np.vectorize(one, otypes=[dtype])(vals)
+
+
+class InexactError(ValueError):
+    """Julia's InexactError: a value that cannot be represented in the destination type."""
 
 
 class Contraction(_FusedIdx, GPUBatchEvaluator):

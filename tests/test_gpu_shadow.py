@@ -15,7 +15,7 @@ import oracle_lib as O
 # the library's deferred-update depth (tci_abi.cpp tci_ctx::flush_every, env TCI_RRLU_NB), restored
 # after tests that change it
 LIB_DEFAULT_NB = int(os.environ.get("TCI_RRLU_NB", "10"))
-LIB_DEFAULT_EPOCHS = int(os.environ.get("TCI_RRLU_EPOCHS", "3"))
+LIB_DEFAULT_EPOCHS = int(os.environ.get("TCI_RRLU_EPOCHS", "0"))  # 0: by shape, the library default
 
 pytestmark = pytest.mark.gpu
 

@@ -134,3 +134,19 @@ def test_host_function_batch_layout_vs_oracle(mode, M):
     assert gmx == mx
     if ev._pool is not None:
         ev._pool.shutdown()
+
+
+def test_contraction_f_complex_into_real_raises():
+    """a Float64 Contraction whose f returns a complex value with a nonzero imaginary part
+    throws InexactError in the reference (`res .= obj.f.(res)` into a Float64 array,
+    contraction.jl:571); real-valued complex results and real f pass through."""
+    from tci_amd.contraction import InexactError, _elementwise
+    vals = np.linspace(0.1, 1.0, 6).reshape(2, 3)
+    with pytest.raises(InexactError):
+        _elementwise(lambda x: np.exp(1j * x), vals)
+    with pytest.raises(InexactError):  # the element-by-element path (f not vectorised)
+        _elementwise(lambda x: complex(x, 1.0) if isinstance(x, float) else None, vals)
+    assert np.array_equal(_elementwise(lambda x: x + 0j, vals), vals)
+    assert np.array_equal(_elementwise(lambda x: 2 * x, vals), 2 * vals)
+    c = _elementwise(lambda x: np.exp(1j * x), vals, np.complex128)
+    assert np.allclose(c, np.exp(1j * vals))
