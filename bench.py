@@ -29,7 +29,7 @@ def rrlu_flops(m, n, r):
     return float(np.sum(2.0 * (m - k) * (n - k)))
 
 
-def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1):
+def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1, pass0_apart=False):
     """Algorithmic HBM bytes of the rrLU passes after pivots k = 0..r-1 with k % stride == 0
     (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block, following the host
     schedule of tci_abi.cpp rrlu_device. Exact passes: a read-only pass reads 8 B/element, every
@@ -39,14 +39,15 @@ def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1):
     ends every shadow epoch of nb pivots with a refresh (the shadow read and rewritten: 2 + 2) and
     every epochs-th with a write-back (8 read + 8 + 2 written). The exact re-reads of candidate
     elements and the pending x / y vectors are data-dependent / small and not counted.
-    Returns (read_only, write_back, refresh) as (bytes, launches)."""
+    Returns (read_only, write_back, refresh) as (bytes, launches); with pass0_apart the exact pass 0
+    (fp16 shadow: 8 + 2 B/element) is left out of read_only and returned fourth."""
     if not (shadow and sh_bytes == 2 and 2 <= nb <= 15):
         epochs = 1
     epochs = max(1, min(epochs, 32 // nb))
     nbx = nb * epochs
     ro_per, wb_per = (float(sh_bytes), 16.0 + sh_bytes) if shadow else (8.0, 16.0)
-    ro_b = wb_b = rf_b = 0.0
-    ro_n = wb_n = rf_n = 0
+    ro_b = wb_b = rf_b = p0_b = 0.0
+    ro_n = wb_n = rf_n = p0_n = 0
     te = ts = 0
     for k in range(r):
         PE, PS = k - te + 1, k - ts + 1
@@ -66,9 +67,14 @@ def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1):
         elif refresh:
             rf_b += 2.0 * sh_bytes * elems
             rf_n += 1
+        elif shadow and sh_bytes == 2 and k == 0 and pass0_apart:
+            p0_b += (8.0 + sh_bytes) * elems
+            p0_n += 1
         else:
             ro_b += (8.0 + sh_bytes if (shadow and sh_bytes == 2 and k == 0) else ro_per) * elems
             ro_n += 1
+    if pass0_apart:
+        return (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n), (p0_b, p0_n)
     return (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n)
 
 
@@ -155,7 +161,14 @@ def main():
     dt = time.perf_counter() - t0
     assert np_ == min(r, m, n), np_
     wb_ms, wb_launches = ctx.kernel_stats(0)
-    ro_ms, ro_launches = ctx.kernel_stats(2)
+    # read-only passes: per-pass launches (family 2, pass 0 excluded: family 43) and the persistent
+    # shadow-epoch launches (41 first shadow epoch, 42 later ones; units = the passes they ran)
+    ro1_ms, ro1_launches = ctx.kernel_stats(2)
+    ep_ms, ep_launches, ep_passes = ctx.kernel_units(41)
+    epx_ms, epx_launches, epx_passes = ctx.kernel_units(42)
+    p0_ms, p0_launches = ctx.kernel_stats(43)
+    ro_ms = ro1_ms + ep_ms + epx_ms
+    ro_launches = ro1_launches + ep_passes + epx_passes  # passes, not launches
     rf_ms, rf_launches = ctx.kernel_stats(23)
     by_pending = {}  # read-only pass time by pending depth P (sub-families 3 + P)
     by_pending_ext = {}  # the same in the later shadow epochs of an exact epoch (EXT passes, 24 + P)
@@ -183,7 +196,10 @@ def main():
     value = flops * world * args.steps / dt / 1e9  # GFLOP/s, whole job
     nb = args.nb
     sh_bytes = int(ctx.lib.tci_rrlu_shadow_bytes())
-    (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n) = pass_bytes(m, n, r, nb, stride, shadow, sh_bytes, args.epochs)
+    # algorithmic bytes per pass from the whole schedule (every pass, stride 1): the sampled passes are
+    # a uniform spread of it (every stride-th per-pass launch, every third persistent launch)
+    (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n), (p0_b, p0_n) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes,
+                                                                       args.epochs, pass0_apart=True)
     # dominant kernel: the read-only pass when nb > 1, else the write-back pass
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
@@ -202,8 +218,7 @@ def main():
                                                        wb_b, wb_n)
     # whole-step context: every pass's algorithmic bytes (stride 1), the initial argmax pass (8 B)
     # and the copy rrlu makes (16 B per element), over the measured step time
-    (ro_all, _), (wb_all, _), (rf_all, _) = pass_bytes(m, n, r, nb, 1, shadow, sh_bytes, args.epochs)
-    step_bytes = ro_all + wb_all + rf_all + 24.0 * m * n
+    step_bytes = ro_b + wb_b + rf_b + p0_b + 24.0 * m * n
     avg_launch_ms = dom_ms / max(dom_launches, 1)
     bytes_per_launch = dom_bytes / max(dom_n, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -215,6 +230,17 @@ def main():
                                 if ro_launches else None,
                                 "avg_ms_by_pending_depth": by_pending,
                                 "avg_ms_by_pending_depth_ext": by_pending_ext},
+             "read_only_pass_split": {
+                 "per_pass_launches": {"passes": ro1_launches, "avg_ms": round(ro1_ms / max(ro1_launches, 1), 5)},
+                 "persistent_first_epoch": {"launches": ep_launches, "passes": ep_passes,
+                                            "avg_ms_per_pass": round(ep_ms / max(ep_passes, 1), 5)},
+                 "persistent_ext": {"launches": epx_launches, "passes": epx_passes,
+                                    "avg_ms_per_pass": round(epx_ms / max(epx_passes, 1), 5)}},
+             "pass0": {"launches": p0_launches, "avg_ms": round(p0_ms / max(p0_launches, 1), 5),
+                       "GBps": round(p0_b / max(p0_n, 1) / (p0_ms / max(p0_launches, 1) * 1e-3) / 1e9, 1)
+                       if p0_launches else None,
+                       "note": "the exact pass after pivot 0 (reads A, writes the fp16 shadow: 10 B/element); "
+                               "its own family, not in read_only_pass"},
              "refresh_pass": {"launches": rf_launches, "avg_ms": round(rf_ms / max(rf_launches, 1), 5),
                               "GBps": round(rf_b / max(rf_n, 1) / (rf_ms / max(rf_launches, 1) * 1e-3) / 1e9, 1)
                               if rf_launches else None},

@@ -92,6 +92,11 @@ int tci_ctx_synchronize(tci_ctx* ctx);
  * 21 = MatrixLUCI factors, 22 = K3 GEMMs issued through tci_dgemm_d / tci_schur_update_d, 23 =
  * rrLU refresh passes (read-only passes that also rewrite the fp16 shadow, two-level epoch). */
 int tci_last_kernel_stats(tci_ctx* ctx, int family, double* total_ms, int64_t* launches);
+/* The same with the passes the timed launches covered (units): 41 / 42 = persistent launches of a
+ * shadow epoch's read-only passes (first shadow epoch / later ones; tci_set_rrlu_persist), whose
+ * units are passes, 43 = pass 0 (the exact pass after pivot 0 that writes the shadow of A; not in
+ * family 2). Every other launch counts one unit. */
+int tci_last_kernel_units(tci_ctx* ctx, int family, double* total_ms, int64_t* launches, int64_t* units);
 /* enabled = 0: off; s >= 1: on, timing the rrLU pass of every s-th pivot (k % s == 0) and every
  * batch evaluation. Resets the statistics. */
 int tci_set_timing(tci_ctx* ctx, int enabled);
@@ -114,6 +119,19 @@ int tci_set_rrlu_small(tci_ctx* ctx, int enabled);
  * enabled = 0 forces the pass pipeline. Bitwise identical results. Default on (env
  * TCI_RRLU_MID=0: off). */
 int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
+/* The read-only passes of a shadow epoch (the passes between two refreshes / write-backs of the
+ * fp16 shadow; up to nb - 1 of them) run as ONE persistent launch whose resident grid hands each
+ * pivot's commit to the next pass in place of a kernel boundary -- the same pass bodies, results
+ * bitwise identical (replaces the per-pivot loop of _optimizerrlu!, matrixlu.jl:356-369). If the grid
+ * is found not co-resident (another process holds CUs) the launch gives up after 0.5 s, the
+ * factorisation resumes with per-pass launches and this context stops using the persistent form
+ * (tci_rrlu_persist_faulted). Default on (env TCI_RRLU_PERSIST=0: off); enabled resets the flag.
+ * enabled = 2 is a test mode: the persistent launch is used even where its grid exceeds one workgroup
+ * per CU (TCI_PASS_GRIDX > 1), i.e. where it is NOT co-resident, and gives up after 2 ms, so that the
+ * give-up-and-resume path runs. */
+int tci_set_rrlu_persist(tci_ctx* ctx, int enabled);
+/* 1 once a persistent launch of this context gave up (see tci_set_rrlu_persist), else 0. */
+int tci_rrlu_persist_faulted(tci_ctx* ctx);
 /* Certified shadow search in the read-only passes of the pass pipeline: the write-back passes also
  * keep a shadow of the stale values -- fp16 scaled per write-back epoch (2 B/element; fp32 in
  * the TCI_SH_HALF=0 build) -- and a read-only pass streams it instead of the fp64 values, applies

@@ -50,6 +50,10 @@ struct tci_ctx {
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int mid_faulted = 0;   // its grid barrier timed out once on this context: pass pipeline from then on
+    int persist = 1;       // read-only passes of a shadow epoch as one persistent launch (env TCI_RRLU_PERSIST=0)
+    int persist_faulted = 0;  // such a launch found its grid not co-resident: per-pass launches from then on
+    unsigned* esync = nullptr;  // their sync slots (tci_rrlu.hip k_pass_mf_epoch), one per launch
+    size_t capEsync = 0;
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
     int c128_nb = -1;            // ComplexF64 rrLU deferred-update depth (env TCI_C128_NB; 0: round 1;
                                  // -1: 11 with the shadow search, 6 without -- measured best)
@@ -150,13 +154,19 @@ struct tci_ctx {
     struct EvPair {
         int fam, sub;
         size_t idx;
+        int units;  // passes the timed launch covers (1, or a persistent epoch launch's count)
     };
     std::vector<EvPair> evpairs;
     // + 20 solve, 21 LUCI factors, 22 K3, 23 refresh, 24 + P read-only passes of a later shadow epoch
-    // (EXT: the exact epoch is longer; 3 + P: the first shadow epoch after a write-back)
-    static constexpr int kFams = 3 + tci::kMaxPend + 1 + 4 + tci::kMaxPend + 1;
+    // (EXT: the exact epoch is longer; 3 + P: the first shadow epoch after a write-back), 41 / 42
+    // persistent epoch launches (first shadow epoch / EXT; units = passes), 43 pass 0 (the exact pass
+    // after pivot 0 that writes the shadow of A)
+    static constexpr int kFamEpoch = 3 + tci::kMaxPend + 1 + 4 + tci::kMaxPend + 1;
+    static constexpr int kFamPass0 = kFamEpoch + 2;
+    static constexpr int kFams = kFamPass0 + 1;
     double fam_ms[kFams] = {};
     int64_t fam_n[kFams] = {};
+    int64_t fam_u[kFams] = {};
 };
 
 struct tci_comm {
@@ -320,7 +330,7 @@ int ensure_pinned(tci_ctx* c, char** p, size_t* cap, size_t bytes) {
     return TCI_OK;
 }
 
-void ev_begin(tci_ctx* c, int fam, bool sampled = true, int sub = -1) {
+void ev_begin(tci_ctx* c, int fam, bool sampled = true, int sub = -1, int units = 1) {
     if (!c->timing || !sampled) return;
     if (c->evused + 2 > c->evpool.size()) {
         size_t add = std::max<size_t>(64, c->evpool.size());
@@ -330,7 +340,7 @@ void ev_begin(tci_ctx* c, int fam, bool sampled = true, int sub = -1) {
             c->evpool.push_back(e);
         }
     }
-    c->evpairs.push_back({fam, sub, c->evused});
+    c->evpairs.push_back({fam, sub, c->evused, units});
     hipEventRecord(c->evpool[c->evused], c->stream);
     c->evused += 2;
 }
@@ -344,6 +354,7 @@ void ev_reset(tci_ctx* c) {
     for (int f = 0; f < tci_ctx::kFams; ++f) {
         c->fam_ms[f] = 0;
         c->fam_n[f] = 0;
+        c->fam_u[f] = 0;
     }
 }
 void ev_collect(tci_ctx* c) {
@@ -354,9 +365,11 @@ void ev_collect(tci_ctx* c) {
         hipEventElapsedTime(&ms, c->evpool[pr.idx], c->evpool[pr.idx + 1]);
         c->fam_ms[pr.fam] += ms;
         c->fam_n[pr.fam] += 1;
+        c->fam_u[pr.fam] += pr.units;
         if (pr.sub >= 0) {
             c->fam_ms[pr.sub] += ms;
             c->fam_n[pr.sub] += 1;
+            c->fam_u[pr.sub] += pr.units;
         }
     }
     c->evpairs.clear();
@@ -390,12 +403,14 @@ struct StopPoll {
     int cur = 0;
     bool pending = false;
     StopPoll(tci_ctx* ctx, const void* state) : c(ctx), dstate(state) {}
-    int after_chunk(bool* stopped) {
+    // done (optional): the state's done word as copied (1: stop test, 2: a persistent launch gave up)
+    int after_chunk(bool* stopped, int* done = nullptr) {
         HIPCHK(c, hipMemcpyAsync(&c->hpoll[cur], dstate, kPrefix, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->pollev[cur], c->stream));
         if (pending) {
             HIPCHK(c, hipEventSynchronize(c->pollev[cur ^ 1]));
             *stopped = c->hpoll[cur ^ 1].done != 0;
+            if (done) *done = c->hpoll[cur ^ 1].done;
         }
         pending = true;
         cur ^= 1;
@@ -538,40 +553,113 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     g.nbs = nb;
     g.pe = g.ps = 0;
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
-    int64_t k = 0, chunk = 2, te = 0, ts = 0;  // te / ts: first pivot whose update is pending in fp64 / the shadow
-    StopPoll poll(c, c->st);
-    while (k < mr) {
-        const int64_t kend = std::min<int64_t>(k + chunk, mr);
-        for (int64_t kk = k; kk < kend; ++kk) {
-            // pass k: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
-            // selects pivot k+1 from the updated block. After the last pivot only x_k / y_k are
-            // needed: no selection.
-            const int PE = (int)(kk - te) + 1, PS = (int)(kk - ts) + 1;
-            const bool last = kk + 1 >= mr;
-            const bool flush = PE >= nbx && !last;
-            const bool refresh = !flush && epochs > 1 && PS >= nb && !last;
-            g.k = (int)kk;
-            g.pe = PE;
-            g.ps = PS;
-            g.selk = !last ? (int)(kk + 1) : -1;
-            g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
-            const bool sampled = kk % c->timing_stride == 0;
-            ev_begin(c, flush ? 0 : refresh ? 23 : 2, sampled, flush || refresh ? -1 : (PE > PS ? 24 : 3) + PS);
-            tci::launch_pass(c->stream, PE, flush, shadow, g, grid, flush ? 1 : refresh ? 2 : 0);
-            ev_end(c, sampled);
-            if (flush) te = ts = kk + 1;
-            if (refresh) ts = kk + 1;
-        }
-        k = kend;
-        if (k >= mr) break;
-        bool stopped = false;
-        if ((st = poll.after_chunk(&stopped))) return st;
-        if (stopped) break;
-        chunk = std::min<int64_t>(chunk * 2, StopPoll::kMaxChunk);
+    // The pass schedule: pass kk applies PE exact / PS shadow pending updates and is a
+    // write-back (flush), a refresh, or read-only; te / ts: the first pivot whose update is pending in
+    // fp64 / in the shadow. A deterministic function of kk, so a resume can replay it.
+    struct Sched {
+        int PE, PS;
+        bool last, flush, refresh;
+    };
+    auto sched = [&](int64_t kk, int64_t te, int64_t ts) {
+        Sched s;
+        s.PE = (int)(kk - te) + 1;
+        s.PS = (int)(kk - ts) + 1;
+        s.last = kk + 1 >= mr;
+        s.flush = s.PE >= nbx && !s.last;
+        s.refresh = !s.flush && epochs > 1 && s.PS >= nb && !s.last;
+        return s;
+    };
+    // Persistent epoch launches (tci_rrlu.hip k_pass_mf_epoch): a run of >= 2 read-only MFMA-search
+    // passes in one launch, when the grid is one workgroup per CU (all co-resident on an idle device)
+    // (persist == 2, a test mode: also when the grid exceeds one workgroup per CU -- it is then NOT
+    // co-resident and the launch must give up, after 2 ms instead of 0.5 s, and resume)
+    bool persist = c->persist && !c->persist_faulted && shadow && tci::shadow_two_level() && c->ncu > 0 &&
+                   ((grid <= c->ncu && c->pass_gridx == 1) || c->persist == 2);
+    const long long ptimeout = c->persist == 2 ? 200000 : 50000000;  // 100 MHz ticks
+    int64_t nlaunch = 0;  // persistent launches issued (their sync slots)
+    if (persist) {
+        const size_t slots = (size_t)mr / 2 + 2;
+        if ((st = ensure(c, &c->esync, &c->capEsync, slots * tci::kEpochSlot))) return st;
+        HIPCHK(c, hipMemsetAsync(c->esync, 0, slots * tci::kEpochSlot * sizeof(unsigned), c->stream));
     }
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int64_t k = 0, chunk = 2, te = 0, ts = 0;
+    StopPoll poll(c, c->st);
+    for (;;) {  // once, or again from a resume point after a persistent launch gave up
+        while (k < mr) {
+            const int64_t kend = std::min<int64_t>(k + chunk, mr);
+            int64_t kk = k;
+            while (kk < kend) {
+                // pass kk: derives x_k / y_k (L column / U row k), applies pending updates 0..P-1 and
+                // selects pivot k+1 from the updated block. After the last pivot only x_k / y_k are
+                // needed: no selection.
+                const Sched s = sched(kk, te, ts);
+                const bool ro = !s.flush && !s.refresh && !s.last;
+                if (persist && ro && kk >= 1 && s.PS <= tci::kEpochMaxP) {
+                    int np = 1;  // the run of read-only passes that follows (te, ts do not move in it)
+                    for (;; ++np) {
+                        const Sched t = sched(kk + np, te, ts);
+                        if (t.flush || t.refresh || t.last || t.PS > tci::kEpochMaxP) break;
+                    }
+                    if (np >= 2) {
+                        g.k = (int)kk;
+                        g.pe = s.PE;
+                        g.ps = s.PS;
+                        g.selk = (int)(kk + 1);
+                        const bool sampled = nlaunch % 3 == 0;
+                        ev_begin(c, s.PE > s.PS ? tci_ctx::kFamEpoch + 1 : tci_ctx::kFamEpoch, sampled, -1, np);
+                        tci::launch_pass_epoch(c->stream, g, grid, np, c->serpentine,
+                                               c->esync + (size_t)nlaunch * tci::kEpochSlot, ptimeout);
+                        ev_end(c, sampled);
+                        ++nlaunch;
+                        kk += np;
+                        continue;
+                    }
+                }
+                g.k = (int)kk;
+                g.pe = s.PE;
+                g.ps = s.PS;
+                g.selk = !s.last ? (int)(kk + 1) : -1;
+                g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
+                const bool sampled = kk % c->timing_stride == 0;
+                // pass 0 (shadow on: the exact pass that writes the shadow of A) is a family of its own
+                const bool pass0 = kk == 0 && shadow && tci::shadow_elem_bytes() == 2 && !s.flush;
+                ev_begin(c, s.flush ? 0 : s.refresh ? 23 : pass0 ? tci_ctx::kFamPass0 : 2, sampled,
+                         s.flush || s.refresh || pass0 ? -1 : (s.PE > s.PS ? 24 : 3) + s.PS);
+                tci::launch_pass(c->stream, s.PE, s.flush, shadow, g, grid, s.flush ? 1 : s.refresh ? 2 : 0);
+                ev_end(c, sampled);
+                if (s.flush) te = ts = kk + 1;
+                if (s.refresh) ts = kk + 1;
+                ++kk;
+            }
+            k = kk;
+            if (k >= mr) break;
+            bool stopped = false;
+            if ((st = poll.after_chunk(&stopped))) return st;
+            if (stopped) break;
+            chunk = std::min<int64_t>(chunk * 2, StopPoll::kMaxChunk);
+        }
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->hst->done != 2 && c->hst->done != 3) break;
+        // A persistent launch ended early: 2 -- it gave up waiting for its grid (another process
+        // holds CUs); 3 -- a pass's shadow certificate failed (a rapidly decaying block: the exact
+        // bodies are per-pass kernels). Nothing was committed for that pass, every launch after it
+        // returned at once, and every pass write is idempotent: resume with per-pass launches at the
+        // pass after the last commit (for the rest of this factorisation; after 2 for the context)
+        if (c->hst->done == 2) c->persist_faulted = 1;
+        persist = false;
+        k = c->hst->np - 1;
+        te = ts = 0;
+        for (int64_t q = 0; q < k; ++q) {  // replay the schedule up to pass k
+            const Sched s = sched(q, te, ts);
+            if (s.flush) te = ts = q + 1;
+            if (s.refresh) ts = q + 1;
+        }
+        HIPCHK(c, hipMemsetAsync(&c->st->done, 0, sizeof(int32_t), c->stream));
+        chunk = 2;
+        poll = StopPoll(c, c->st);
+    }
     int64_t np = c->hst->np;
     double err = c->hst->error;
     if (np >= std::min(m, n)) err = 0.0;  // matrixlu.jl:391-393
@@ -923,6 +1011,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = atoi(e) != 0;
     if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
     if (const char* e = getenv("TCI_C128_SH")) c->c128_sh = atoi(e) != 0;
     if (const char* e = getenv("TCI_DENSE_MFMA")) c->dense = std::max(0, std::min(atoi(e), (int)tci::kDenseAll));
@@ -961,7 +1050,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     auto fr = [](void* p) { if (p) hipFree(p); };
     fr(c->dA); fr(c->sbuf); fr(c->cand); fr(c->st); fr(c->rowperm); fr(c->colperm); fr(c->xbuf); fr(c->ybuf); fr(c->flag);
-    fr(c->ticket); fr(c->bar); fr(c->fault); fr(c->colbuf);
+    fr(c->ticket); fr(c->esync); fr(c->bar); fr(c->fault); fr(c->colbuf);
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
     fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
@@ -1042,6 +1131,16 @@ int tci_set_rrlu_mid(tci_ctx* c, int enabled) {
     return TCI_OK;
 }
 
+int tci_set_rrlu_persist(tci_ctx* c, int enabled) {
+    if (!c) return TCI_ERR_ARG;
+    if (enabled < 0 || enabled > 2) return set_err(c, TCI_ERR_ARG, "persist must be 0, 1 or 2 (test mode)");
+    c->persist = enabled;
+    c->persist_faulted = 0;
+    return TCI_OK;
+}
+
+int tci_rrlu_persist_faulted(tci_ctx* c) { return c ? c->persist_faulted : -1; }
+
 int tci_set_timing(tci_ctx* c, int enabled) {
     c->timing = enabled > 0;
     c->timing_stride = enabled > 0 ? enabled : 1;
@@ -1049,11 +1148,16 @@ int tci_set_timing(tci_ctx* c, int enabled) {
     return TCI_OK;
 }
 int tci_last_kernel_stats(tci_ctx* c, int family, double* total_ms, int64_t* launches) {
+    return tci_last_kernel_units(c, family, total_ms, launches, nullptr);
+}
+int tci_last_kernel_units(tci_ctx* c, int family, double* total_ms, int64_t* launches, int64_t* units) {
+    if (!c) return TCI_ERR_ARG;
     if (family < 0 || family >= tci_ctx::kFams)
         return set_err(c, TCI_ERR_ARG, "family must be in 0.." + std::to_string(tci_ctx::kFams - 1));
     ev_collect(c);
     if (total_ms) *total_ms = c->fam_ms[family];
     if (launches) *launches = c->fam_n[family];
+    if (units) *units = c->fam_u[family];
     return TCI_OK;
 }
 

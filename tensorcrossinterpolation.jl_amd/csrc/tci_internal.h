@@ -205,6 +205,14 @@ void launch_cluci_factors(hipStream_t s, const double2* L, const double2* U, int
 // kind: 0 read-only, 1 write-back (fp64 + shadow), 2 refresh (shadow only, from the MFMA search's
 // values or, when its bound is not tight, from the exact ones); P = g.pe
 void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& g, int grid, int kind = -1);
+// Persistent shadow epoch (k_pass_mf_epoch): the read-only passes k = g.k .. g.k + npass - 1 (shadow-
+// pending counts g.ps .. g.ps + npass - 1 <= kEpochMaxP, g.pe > g.ps: EXT) in one launch of `grid`
+// workgroups, which must all be resident at once (one per CU). sync: kEpochSlot zeroed words of this
+// launch's own. A launch that finds its grid not co-resident sets st->done = 2 (tci_abi.cpp resumes).
+constexpr int kEpochMaxP = 10;
+constexpr int kEpochSlot = 64;  // unsigned words per launch: ticket at 0, generation at 32
+void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
+                       long long timeout);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:

@@ -217,6 +217,7 @@ __device__ __forceinline__ void block_reduce_cand(CandR& c) {
 // MI355X_MICROARCH.md hand-off table, first row) and the one whose add comes last reduces them and
 // commits pivot sel.selk -- the selection needs no launch of its own. rowpos / colpos / st change
 // only there, after every other workgroup has finished reading them.
+template <bool COH = false>
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
                              double* pivvals, int64_t rk = -1, int64_t ck = -1, bool has_mxe = false,
@@ -544,10 +545,33 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int by
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
 
+// Loads and stores of the data one pass hands to the next (pending X / Y slots, the position maps,
+// the pivot values and the state). Between launches the kernel boundary makes them visible; inside
+// the persistent epoch kernel (k_pass_mf_epoch) they are handed over without fences, as
+// MI355X_MICROARCH.md's hand-off table, first row: every store of them `sc1`, drained before the
+// pass's ticket (or, for the commit, before the generation flag), and every load of them a
+// `global_load ... sc1` after the consumer's poll has matched. COH = false: plain accesses.
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <bool COH, typename T>
+__device__ __forceinline__ T ldc(const T* p) {
+    if constexpr (COH)
+        return __hip_atomic_load((gptr<T>)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return *p;
+}
+template <bool COH, typename T>
+__device__ __forceinline__ void stc(T* p, T v) {
+    if constexpr (COH)
+        __hip_atomic_store((gptr<T>)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 // Body of the exact pass (k_pass2). SH: also store the fp32 shadow S of the values this pass
 // leaves as the new stale ones (write-back passes) or reads unmodified (the initial pass, P = 0).
 // Returns false when the factorisation has already stopped.
-template <int P, bool FLUSH, bool SH>
+template <int P, bool FLUSH, bool SH, bool COH = false>
 __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                                            P2Lds<(P > 0 ? P : 1)>& L, CandR& best,
                                            unsigned long long (&pt)[8]) {
@@ -656,11 +680,11 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
         if (q == 0 && rep == 0) {
             double* xs = X + (int64_t)(P - 1) * ldx;
             if (in0) {
-                xs[r0] = xk0;
+                stc<COH>(xs + r0, xk0);
                 g.Lp[r0 + (int64_t)k * g.ldl] = xk0;
             }
             if (in1) {
-                xs[r0 + 1] = xk1;
+                stc<COH>(xs + r0 + 1, xk1);
                 g.Lp[r0 + 1 + (int64_t)k * g.ldl] = xk1;
             }
         }
@@ -695,7 +719,7 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                 if (!leftorth) yk = yk / piv;
                 ys[lc * PP + P - 1] = yk;
                 if (tr == 0) {
-                    Y[(int64_t)(P - 1) * ldy + jst] = yk;
+                    stc<COH>(Y + (int64_t)(P - 1) * ldy + jst, yk);
                     g.Up[k + (int64_t)jst * g.ldu] = yk;
                 }
             }
@@ -1256,14 +1280,16 @@ struct PendPre {
 };
 // Loads unconditional (slots < kMaxPendR always exist), masked after: a load inside `i < cnt`
 // became a branch each, and the other role's branch then began with a wait for all of them.
+template <bool COH = false>
 __device__ __forceinline__ void pend_pre(PendPre& p, const double* __restrict__ xp, int64_t xst, int cnt) {
     static_assert(kPendPre <= kMaxPendR, "prefetched slots exist");
 #pragma unroll
-    for (int i = 0; i < kPendPre; ++i) p.v[i] = xp[(int64_t)i * xst];
+    for (int i = 0; i < kPendPre; ++i) p.v[i] = ldc<COH>(xp + (int64_t)i * xst);
 #pragma unroll
     for (int i = 0; i < kPendPre; ++i)
         if (i >= cnt) p.v[i] = 0.0;
 }
+template <bool COH = false>
 __device__ __forceinline__ double pend_chain(double v, const PendPre& p, const double* __restrict__ xp,
                                              int64_t xst, double upl, int cnt) {
 #pragma unroll
@@ -1272,7 +1298,7 @@ __device__ __forceinline__ double pend_chain(double v, const PendPre& p, const d
     if (cnt > kPendPre) {
         double r[kMaxPendR - 1 - kPendPre];
 #pragma unroll
-        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i) r[i] = xp[(int64_t)(kPendPre + i) * xst];
+        for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i) r[i] = ldc<COH>(xp + (int64_t)(kPendPre + i) * xst);
 #pragma unroll
         for (int i = 0; i < kMaxPendR - 1 - kPendPre; ++i)
             if (kPendPre + i < cnt) v = __dsub_rn(v, __dmul_rn(r[i], readlane_dbl(upl, kPendPre + i)));
@@ -1334,12 +1360,13 @@ struct ShCert {
 // the pivot values pv[te - 1 .. k] (PE + 1 <= 33 of them), one load per lane (read back with
 // readlane: a loop of dependent scalar loads cost ~5 us at PE ~ 26, phase profile of round 3); a
 // separate step so that the load goes out first and sh_cert's wait counts only the loads after it
+template <bool COH = false>
 __device__ __forceinline__ double sh_cert_load(const double* pv, int k, int PE) {
     const int lane = threadIdx.x & 63, ix = k - PE + lane;
     // unconditional, unmasked: sh_cert reads lanes 0 .. PE only, and lane 0 (pivot te - 1) only
     // when te >= 1 (for te = 0 it takes |pivot 0| instead), so the clamped lanes are never read
     (void)lane;
-    return pv[min(max(ix, 0), k)];
+    return ldc<COH>(pv + min(max(ix, 0), k));
 }
 __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int nbs) {
     const int te = k - PE + 1, t0 = k - PS + 1;
@@ -1375,13 +1402,15 @@ __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int n
 // (nothing done: the caller runs the exact body). The certificate is derived after the
 // pivot-independent loads are issued, so its pivot-value round trip overlaps theirs.
 constexpr int kMfStop = 0, kMfDone = 1, kMfExact = 2;
-template <int P, bool EXT = false, bool RF = false>
+template <int P, bool EXT = false, bool RF = false, bool COH = false>
 __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P, EXT>& L,
-                                            CandR& best, unsigned long long (&pt)[8]) {
+                                            CandR& best, unsigned long long (&pt)[8], const int Pr = P) {
     static_assert(P >= 1 && P <= kMfMaxP, "at most two MFMA K-steps per tile");
     using Gm = MfGeom<P, EXT>;
-    const int PE = EXT ? g.pe : P;  // exact pending updates; the shadow's are slots off .. PE - 1
-    const int off = PE - P;
+    // Pr: the shadow-pending count, P its compile-time bound (register arrays, LDS strides): equal in
+    // the per-pass kernels, P = kEpochMaxP in the persistent epoch kernel (one body for every depth)
+    const int PE = EXT ? g.pe : Pr;  // exact pending updates; the shadow's are slots off .. PE - 1
+    const int off = PE - Pr;
     constexpr int KS = Gm::KS, KSP = Gm::KSP, KSt = KS / 32;
     RrluState* st = sel.st;
     const int32_t* colpos = sel.colpos;
@@ -1389,7 +1418,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     const double* pv = sel.pivvals;
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
     const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy, lds = g.lds;
-    const int t0 = k - P + 1;
+    const int t0 = k - Pr + 1;
     // The certificate's pivot values and the pivot the previous pass committed: the pass's first
     // loads. The compiler moves the pivot to scalar registers at once, i.e. waits for it right
     // here -- one round trip, after which the prologue's pivot-independent loads (maps, first
@@ -1398,17 +1427,22 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // ms per step; read after the certificate and behind serial map loads, the pivot had been the
     // third or fourth round trip.) Vector loads: as scalar loads they were waited for by the next
     // kernel-argument reload (lgkmcnt(0)).
-    const double certw = sh_cert_load(pv, k, PE);
-    const int st_done = __hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int a = (int)__hip_atomic_load(&st->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int bq = (int)__hip_atomic_load(&st->q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double piv = __hip_atomic_load(&st->pval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double certw = sh_cert_load<COH>(pv, k, PE);
+    const int st_done = ldc<true>(&st->done);
+    const int a = (int)ldc<true>(&st->p);
+    const int bq = (int)ldc<true>(&st->q);
+    const double piv = ldc<true>(&st->pval);
+    // thread / workgroup indices: inside the persistent epoch kernel (COH) made opaque per pass, so
+    // that nothing derived from them is hoisted out of its pass loop (kept live across every pass,
+    // those values spilled the body's registers)
+    int tx = (int)threadIdx.x, bx = (int)blockIdx.x, gx = (int)gridDim.x;
+    if constexpr (COH) asm volatile("" : "+v"(tx), "+s"(bx), "+s"(gx));
+    const int lane = tx & 63, wave = tx >> 6;
     const int slice = wave % kMfSlices, rep = wave / kMfSlices;
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
-    const int nq = gridDim.x / tiles_r;
-    const int wid = xcd_spread(blockIdx.x, gridDim.x);
+    const int nq = gx / tiles_r;
+    const int wid = xcd_spread(bx, gx);
     const int tr = wid % tiles_r;
     const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
@@ -1435,10 +1469,10 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         v[1] = p[1];
     };
     // staging: threads 0 .. 511 (one staged column each); the tile's rows: threads 512 .. 1023
-    const bool stager = threadIdx.x < kP2StageCols;
+    const bool stager = tx < kP2StageCols;
     auto stage_col = [&](int g0) -> int {
         const int gn = min(G, ntc - g0);
-        const int lc = threadIdx.x;
+        const int lc = tx;
         if (!stager || lc >= gn * cb) return -1;
         return col_of(g0, lc);
     };
@@ -1448,12 +1482,12 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // wave activity from the rows of its slice (lanes 0..15 x 4: every row once)
     int rpa[kMfBlk];
 #pragma unroll
-    for (int b = 0; b < kMfBlk; ++b) rpa[b] = rowpos[min(sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3), m - 1)];
+    for (int b = 0; b < kMfBlk; ++b) rpa[b] = ldc<COH>(rowpos + min(sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3), m - 1));
     // refresh: which of the lane's 16 loaded rows are trailing (the others get shadow 0)
     [[maybe_unused]] int rpt[RF ? 16 : 1];
     if constexpr (RF) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) rpt[i] = rowpos[min(rl + i, m - 1)];
+        for (int i = 0; i < 16; ++i) rpt[i] = ldc<COH>(rowpos + min(rl + i, m - 1));
     }
     // refresh stores: the shadow as one buffer (the host keeps it below 4 GB for refreshes), the
     // second 16 B of a lane's 32 through a resource 16 B further on (an out-of-range offset stays so)
@@ -1461,10 +1495,10 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     [[maybe_unused]] const auto rsS0 = buf_rsrc(g.S, shb);
     [[maybe_unused]] const auto rsS1 = buf_rsrc(reinterpret_cast<const char*>(g.S) + 16, shb - 16);
     int jst = ntc > 0 ? stage_col(0) : -1;
-    const int cpl = colpos[min(max(jst, 0), n - 1)];
-    const int prow = threadIdx.x - kP2StageCols;  // this thread's tile row (row threads)
+    const int cpl = ldc<COH>(colpos + min(max(jst, 0), n - 1));
+    const int prow = tx - kP2StageCols;  // this thread's tile row (row threads)
     const int rrow = tb + (prow >= 0 ? prow : 0);
-    const int rpl = rowpos[min(rrow, m - 1)];
+    const int rpl = ldc<COH>(rowpos + min(rrow, m - 1));
     h8v va[2], vb[2];
     const int gc0 = ntc > 0 ? min(G, ntc) * cb : 0;
     const int nch0 = (gc0 + 15) / 16;
@@ -1479,10 +1513,10 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     if constexpr (EXT) {
         // one call for both roles (the row threads' x slots, the stagers' y slots): as two
         // calls under the role's branch, the second began with a wait for the first's loads
-        pend_pre(pre, stager ? g.Y + (jst >= 0 && jst < n ? jst : 0) : g.X + (rrow < m ? rrow : 0),
+        pend_pre<COH>(pre, stager ? g.Y + (jst >= 0 && jst < n ? jst : 0) : g.X + (rrow < m ? rrow : 0),
                  stager ? ldy : ldx, PE - 1);
     }
-    const ShCert cert = sh_cert(certw, k, P, PE, g.nbs > 0 ? g.nbs : P);
+    const ShCert cert = sh_cert(certw, k, Pr, PE, g.nbs > 0 ? g.nbs : Pr);
     if (!cert.ok) return kMfExact;
     const float eps = (float)(cert.eps * (1.0 + 0x1p-20));
     const double shs = cert.shs;
@@ -1496,7 +1530,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // the inactive lanes' values undefined.
     [[maybe_unused]] double upl = 0.0;
     if constexpr (EXT) {
-        upl = (stager ? g.X + a : g.Y + bq)[(int64_t)min(lane, kMaxPendR - 1) * (stager ? ldx : ldy)];
+        upl = ldc<COH>((stager ? g.X + a : g.Y + bq) + (int64_t)min(lane, kMaxPendR - 1) * (stager ? ldx : ldy));
     }
     if (!stager) {
         // row thread: x_k of its row (the reference's operation order), the split A fragment row
@@ -1505,35 +1539,41 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         double xs[P];
         if constexpr (!EXT) {
 #pragma unroll
-            for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
+            for (int s = 0; s < P - 1; ++s)
+                if (s < Pr - 1) xs[s] = ldc<COH>(g.X + (int64_t)(off + s) * ldx + rr);
         }
         double xk = g.A[rr + (int64_t)bq * lda];
         if constexpr (EXT) {  // all PE - 1 exact pending updates
             // the shadow-pending x's first: pivot-independent, in flight with the chain's loads
             // (requested after the chain they were one more round trip before the barrier)
 #pragma unroll
-            for (int s = 0; s < P - 1; ++s) xs[s] = g.X[(int64_t)(off + s) * ldx + rr];
-            xk = pend_chain(xk, pre, g.X + rr, ldx, upl, PE - 1);
+            for (int s = 0; s < P - 1; ++s)
+                if (s < Pr - 1) xs[s] = ldc<COH>(g.X + (int64_t)(off + s) * ldx + rr);
+            xk = pend_chain<COH>(xk, pre, g.X + rr, ldx, upl, PE - 1);
         } else {
 #pragma unroll
-            for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(xs[s], g.Y[(int64_t)s * ldy + bq]));
+            for (int s = 0; s < P - 1; ++s)
+                if (s < Pr - 1) xk = __dsub_rn(xk, __dmul_rn(xs[s], ldc<COH>(g.Y + (int64_t)s * ldy + bq)));
         }
         if (leftorth) xk = xk / piv;
         L.xk[prow] = xk;
         const int rpos = rrow < m ? rpl : -1;  // (a row thread)
         if (q == 0 && rpos > k) {
-            g.X[(int64_t)(PE - 1) * ldx + rrow] = xk;
+            stc<COH>(g.X + (int64_t)(PE - 1) * ldx + rrow, xk);
             g.Lp[rrow + (int64_t)k * g.ldl] = xk;
         }
-        xs[P - 1] = xk;
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+            if (s == Pr - 1) xs[s] = xk;
         // rows pivoted before this epoch (and rows past m): 0; pivoted at step rp of it: x_s for
         // s < rp - t0, then the pivot's own x (1, or the pivot when not leftorth), then 0
-        const int dd = rpos > k ? P : (rpos >= t0 ? rpos - t0 : -1);
-        const double own = leftorth ? 1.0 : (rpos >= t0 && rpos <= k ? pv[rpos] : 0.0);
+        const int dd = rpos > k ? Pr : (rpos >= t0 ? rpos - t0 : -1);
+        const double own = leftorth ? 1.0 : (rpos >= t0 && rpos <= k ? ldc<COH>(pv + rpos) : 0.0);
         _Float16 sl[KS];
 #pragma unroll
         for (int s = 0; s < P; ++s) {
             double x = s < dd ? xs[s] : (s == dd ? own : 0.0);
+            if (s >= Pr) x = 0.0;  // (no-op for Pr == P)
             x = -(leftorth ? x : x * shs);
             f16_split(x, sl[3 * s], sl[3 * s + 2]);
             sl[3 * s + 1] = sl[3 * s];
@@ -1557,7 +1597,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     if constexpr (EXT) {
         if (stager) {
             const int jj = jst >= 0 && jst < n ? jst : 0;
-            yk0 = pend_chain(g.A[a + (int64_t)jj * lda], pre, g.Y + jj, ldy, upl, PE - 1);
+            yk0 = pend_chain<COH>(g.A[a + (int64_t)jj * lda], pre, g.Y + jj, ldy, upl, PE - 1);
         }
     }
     PPROF(1);
@@ -1635,7 +1675,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             if (r >= m) continue;
             const int j = col_of(g0, lc);
             double v = g.A[r + (int64_t)j * lda];
-            const int rp = rowpos[r];
+            const int rp = ldc<COH>(rowpos + r);
             // take v now: a load left in flight by the continue below (into a register the
             // streaming loop reuses) would cost a wait for every load at the loop's head
             asm volatile("" : "+v"(v));
@@ -1649,8 +1689,8 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
 #pragma unroll
                         for (int i = 0; i < kExB; ++i)
                             if (s0 + i < PE - 1) {
-                                xv[i] = g.X[(int64_t)(s0 + i) * ldx + r];
-                                yv[i] = g.Y[(int64_t)(s0 + i) * ldy + j];
+                                xv[i] = ldc<COH>(g.X + (int64_t)(s0 + i) * ldx + r);
+                                yv[i] = ldc<COH>(g.Y + (int64_t)(s0 + i) * ldy + j);
                             }
 #pragma unroll
                         for (int i = 0; i < kExB; ++i)
@@ -1659,15 +1699,17 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                 } else {
                     double xv[P];
 #pragma unroll
-                    for (int s = 0; s < P - 1; ++s) xv[s] = g.X[(int64_t)s * ldx + r];
+                    for (int s = 0; s < P - 1; ++s)
+                        if (s < Pr - 1) xv[s] = ldc<COH>(g.X + (int64_t)s * ldx + r);
 #pragma unroll
-                    for (int s = 0; s < P - 1; ++s) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
+                    for (int s = 0; s < P - 1; ++s)
+                        if (s < Pr - 1) v = __dsub_rn(v, __dmul_rn(xv[s], L.ys[lc * P + s]));
                 }
             } else {
 #pragma unroll 1
                 for (int s = 0; s < PE - 1; ++s)
-                    v = __dsub_rn(v, __dmul_rn(g.X[(int64_t)s * ldx + r],
-                                               Gm::ymem ? g.Y[(int64_t)s * ldy + j] : L.ys[lc * P + s]));
+                    v = __dsub_rn(v, __dmul_rn(ldc<COH>(g.X + (int64_t)s * ldx + r),
+                                               Gm::ymem ? ldc<COH>(g.Y + (int64_t)s * ldy + j) : L.ys[lc * P + s]));
             }
             v = __dsub_rn(v, __dmul_rn(L.xk[r - tb], L.ys[lc * Gm::YS + Gm::YS - 1]));
             const double a2 = __dmul_rn(v, v);
@@ -1714,7 +1756,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         g0r = g0;
         if (g0 > 0) {
             jst = stage_col(g0);
-            cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
+            cpst = (jst >= 0 && jst < n) ? ldc<COH>(colpos + jst) : -1;
             // unconditional (an inactive wave loads two chunks it never reads): loads skipped on
             // some paths into the loop would make its head wait for every load in flight
             load_chunk(g0, gcols, min(rep, nch - 1), va);
@@ -1726,18 +1768,19 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             if (g0 > 0 && stager) {
                 const int jj = jst >= 0 && jst < n ? jst : 0;
                 PendPre pg;
-                pend_pre(pg, g.Y + jj, ldy, PE - 1);
-                ykg = pend_chain(g.A[a + (int64_t)jj * lda], pg, g.Y + jj, ldy, upl, PE - 1);
+                pend_pre<COH>(pg, g.Y + jj, ldy, PE - 1);
+                ykg = pend_chain<COH>(g.A[a + (int64_t)jj * lda], pg, g.Y + jj, ldy, upl, PE - 1);
             }
         }
         if (jst >= 0) {
-            int lc = threadIdx.x;
+            int lc = tx;
             asm volatile("" : "+v"(lc));
             L.cpos[lc] = cpst;
             if (cpst > k) {
                 double ysv[P];
 #pragma unroll
-                for (int s = 0; s < P - 1; ++s) ysv[s] = g.Y[(int64_t)(off + s) * ldy + jst];
+                for (int s = 0; s < P - 1; ++s)
+                    if (s < Pr - 1) ysv[s] = ldc<COH>(g.Y + (int64_t)(off + s) * ldy + jst);
                 // (taking them from pre's registers -- they are slots off .. PE - 2 of the column
                 // pre holds -- by a select per slot spills 16-80 VGPRs: pre would stay live here)
                 double yk;
@@ -1746,12 +1789,15 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                 } else {
                     yk = g.A[a + (int64_t)jst * lda];
 #pragma unroll
-                    for (int s = 0; s < P - 1; ++s) yk = __dsub_rn(yk, __dmul_rn(g.X[(int64_t)s * ldx + a], ysv[s]));
+                    for (int s = 0; s < P - 1; ++s)
+                        if (s < Pr - 1) yk = __dsub_rn(yk, __dmul_rn(ldc<COH>(g.X + (int64_t)s * ldx + a), ysv[s]));
                 }
                 if (!leftorth) yk = yk / piv;
-                ysv[P - 1] = yk;
+#pragma unroll
+                for (int s = 0; s < P; ++s)
+                    if (s == Pr - 1) ysv[s] = yk;
                 if (tr == 0) {
-                    g.Y[(int64_t)(PE - 1) * ldy + jst] = yk;
+                    stc<COH>(g.Y + (int64_t)(PE - 1) * ldy + jst, yk);
                     g.Up[k + (int64_t)jst * g.ldu] = yk;
                 }
                 // B fragment: slots (yh_s, yl_s, yh_s) for s < P, zero after
@@ -1759,8 +1805,12 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                 L.ys[lc * Gm::YS + Gm::YS - 1] = yk;
 #pragma unroll
                 for (int s = 0; s < P; ++s) {
-                    if constexpr (!Gm::ymem) L.ys[lc * P + s] = ysv[s];
-                    f16_split(leftorth ? ysv[s] * shs : ysv[s], sl[3 * s], sl[3 * s + 1]);
+                    if (s < Pr) {
+                        if constexpr (!Gm::ymem) L.ys[lc * P + s] = ysv[s];
+                        f16_split(leftorth ? ysv[s] * shs : ysv[s], sl[3 * s], sl[3 * s + 1]);
+                    } else {  // (Pr < P: the persistent epoch kernel)
+                        sl[3 * s] = sl[3 * s + 1] = (_Float16)0.0f;
+                    }
                     sl[3 * s + 2] = sl[3 * s];
                 }
 #pragma unroll
@@ -1775,8 +1825,8 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             }
         }
         if (g0 == 0) PPROF(7);
-        if (threadIdx.x < kMfSlices) L.cnt[threadIdx.x] = 2 * kMfReps;
-        if (g0 == 0 && threadIdx.x == 0) L.tau = 0u;
+        if (tx < kMfSlices) L.cnt[tx] = 2 * kMfReps;
+        if (g0 == 0 && tx == 0) L.tau = 0u;
         __syncthreads();
         if (g0 == 0) {
 #pragma unroll
@@ -1900,7 +1950,7 @@ struct PxLds {
     int cnt[kXSlices];
 };
 
-template <int MODE>
+template <int MODE, bool COH = false>
 __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, PxLds& L, CandR& best,
                                            unsigned long long (&pt)[8]) {
     RrluState* st = sel.st;
@@ -1964,7 +2014,7 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 for (int s = 0; s < P - 1; ++s) xk = __dsub_rn(xk, __dmul_rn(L.xs[s * kXHalf + rr], L.yb[s]));
                 if (leftorth) xk = xk / piv;
                 if (q == 0 && rowpos[r] > k) {
-                    g.X[(int64_t)(P - 1) * ldx + r] = xk;
+                    stc<COH>(g.X + (int64_t)(P - 1) * ldx + r, xk);
                     g.Lp[r + (int64_t)k * g.ldl] = xk;
                 }
             }
@@ -2013,7 +2063,7 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                     if (!leftorth) yk = yk / piv;
                     L.ys[(P - 1) * kXStage + lcs] = yk;
                     if (tr == 0 && half == 0) {
-                        g.Y[(int64_t)(P - 1) * ldy + js] = yk;
+                        stc<COH>(g.Y + (int64_t)(P - 1) * ldy + js, yk);
                         g.Up[k + (int64_t)js * g.ldu] = yk;
                     }
                 }
@@ -2186,6 +2236,138 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, P, RF ? 2 : 0);
 }
 
+// ------------------------------------------------------------------ persistent shadow epoch
+// The read-only passes of one shadow epoch (pivots k0 .. k0 + npass - 1, shadow-pending counts
+// ps0 .. ps0 + npass - 1 <= kEpochMaxP) in ONE launch: the grid stays resident (one 1024-thread
+// workgroup per CU, as the per-pass launches) and hands each commit to the next pass in place of a
+// kernel boundary. Pass bodies are k_pass_mf's (pass_mf_body, COH: its loads and stores of the
+// handed-over data are `sc1`), the tail is pass_tail's ticket, monotonic over the launch:
+//   every wave drains its stores (X / Y slots), the workgroup publishes its candidate (sc1) and adds
+//   to the ticket; the add that completes pass i's count (i + 1) G commits pivot k + 1 with sc1
+//   stores, drains them and sets the generation word to i + 1 (sc1); every other workgroup polls it
+//   (sc1 loads, s_sleep) -- MI355X_MICROARCH.md's hand-off table, first row, both hops.
+// Co-residency is not assumed: a workgroup that waits longer than `timeout` ticks (100 MHz) marks
+// the ticket ABORT by a compare-and-swap that succeeds only while the count is short, so either
+// every workgroup sees the count complete or every one sees ABORT; the aborting one sets
+// st->done = 2 and every later pass launch returns at once. Nothing is committed for the aborted
+// pass, so the host resumes with per-pass launches at pass st->np - 1 (all pass writes are
+// idempotent) and stops using the persistent launch on that context.
+constexpr unsigned kEpochAbort = 0x80000000u;
+constexpr int kEpochGen = 32;  // the generation word's offset in a launch's sync slot (own 128-B line)
+static_assert(kEpochGen + 1 <= kEpochSlot, "sync slot");
+
+
+// thread 0 of a workgroup that is not the committer: wait for generation `want`. 1: go on, 0: abort
+__device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned* gen, unsigned want, unsigned target,
+                                          long long timeout, RrluState* st) {
+    long long t0 = (long long)wall_clock64();
+    for (;;) {
+        if (ldc<true>(gen) >= want) return 1;
+        unsigned tv = ldc<true>(ticket);
+        if (tv & kEpochAbort) return 0;
+        if ((long long)wall_clock64() - t0 > timeout) {
+            // a workgroup is missing (not co-resident) -- or slow: abort only while the count is short
+            while (!(tv & kEpochAbort) && tv < target) {
+                if (__hip_atomic_compare_exchange_strong((gptr<unsigned>)ticket, &tv, tv | kEpochAbort, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    stc<true>(&st->done, 2);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    return 0;
+                }
+            }
+            if (tv & kEpochAbort) return 0;
+            t0 = (long long)wall_clock64();  // every workgroup arrived: the commit is on its way
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+struct EpochArgs {
+    int npass;         // read-only passes in this launch (k = g.k .. g.k + npass - 1)
+    int serp;          // serpentine order: pass k walks backwards when (k + 1) is odd
+    unsigned* sync;    // this launch's words, zero at launch: [0] ticket, [kEpochGen] generation
+    long long timeout; // ticks a workgroup waits for the others before it gives up (abort)
+};
+
+template <bool EXT>
+__global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs sel0, EpochArgs e) {
+    __shared__ __attribute__((aligned(16))) char lds[sizeof(P2MfLds<kEpochMaxP, EXT>)];
+    __shared__ int s_go;
+    [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned G = gridDim.x;
+    unsigned* const ticket = e.sync;
+    unsigned* const gen = e.sync + kEpochGen;
+    for (int i = 0; i < e.npass; ++i) {
+        PassK g = g0;
+        SelArgs sel = sel0;
+        g.k = g0.k + i;
+        g.ps = g0.ps + i;
+        g.pe = g0.pe + i;
+        g.rev = e.serp ? ((g.k + 1) & 1) : 0;
+        sel.selk = g.k + 1;  // the host never puts the last pass in an epoch launch
+        CandR best = cand_none();
+        int r = pass_mf_body<kEpochMaxP, EXT, false, true>(g, sel, *reinterpret_cast<P2MfLds<kEpochMaxP, EXT>*>(lds),
+                                                             best, pt, g.ps);
+        if (r == kMfExact) {
+            // uniform (every workgroup derives the same certificate, before any store of the pass):
+            // the exact bodies are not in this kernel (their registers would spill its MFMA bodies),
+            // so the launch ends here and the host resumes at this pass with per-pass launches
+            // (st->done = 3, set by workgroup 0; nothing of the pass was written)
+            if (blockIdx.x == 0 && threadIdx.x == 0 && ldc<true>(&sel.st->done) == 0) {
+                stc<true>(&sel.st->done, 3);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            return;
+        }
+        if (r != kMfDone) return;  // the stop test fired: every workgroup read the same state
+        // ---- tail: every wave's X / Y slot stores drained before the workgroup's ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        block_reduce_cand<kP2Threads>(best);  // (its barrier orders the waves' drains before the add)
+        const unsigned target = (unsigned)(i + 1) * G;
+        if (threadIdx.x == 0) {
+            store_cand_sc1(g.cand + blockIdx.x, best);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned old = __hip_atomic_fetch_add((gptr<unsigned>)ticket, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            s_go = (old & kEpochAbort) ? 0
+                   : old + 1 == target ? 2
+                                        : epoch_wait(ticket, gen, (unsigned)(i + 1), target, e.timeout, sel.st);
+        }
+        __syncthreads();
+        const int go = s_go;
+        if (go == 0) return;
+        if (go == 2) {
+            // the last arrival: pass_tail's reduction and commit, then the generation word
+            int64_t rk = -1, ck = -1;
+            double mxe = 0.0;
+            if (threadIdx.x == 0) {
+                rk = ldc<true>(sel.rowphys + sel.selk);
+                ck = ldc<true>(sel.colphys + sel.selk);
+                mxe = ldc<true>(&sel.st->maxerror);
+            }
+            constexpr int CPT = kMaxPassGrid / kP2Threads;
+            CandR cs[CPT];
+#pragma unroll
+            for (int u = 0; u < CPT; ++u) {
+                const int c = threadIdx.x + u * kP2Threads;
+                cs[u] = c < (int)G ? load_cand_sc1(g.cand + c) : cand_none();
+            }
+            CandR w = cs[0];
+#pragma unroll
+            for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
+            __syncthreads();  // block_reduce_cand's LDS slots are reused
+            block_reduce_cand<kP2Threads>(w);
+            if (threadIdx.x == 0) {
+                commit_pivot<true>(sel.selk, w, sel.st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
+                                   sel.colphys, sel.pivvals, rk, ck, true, mxe);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                stc<true>(gen, (unsigned)(i + 1));
+            }
+        }
+        __syncthreads();  // s_go and the reduction's LDS are reused by the next pass
+    }
+}
+
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
 // column tiles (at least one; the host rejects tiles_r > kMaxPassGrid).
 int shadow_elem_bytes() { return kShHalf ? 2 : 4; }
@@ -2279,11 +2461,26 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
     }
 }
 
+void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
+                       long long timeout) {
+    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
+                      g.ticket, g.reltol, g.abstol,  g.selk,    nullptr, 0};
+    const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
+                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
+                  g.pe, g.ps, g.nbs};
+    const EpochArgs e{npass, serp, sync, timeout};
+    if (g.pe > g.ps)
+        hipLaunchKernelGGL((k_pass_mf_epoch<true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
+    else
+        hipLaunchKernelGGL((k_pass_mf_epoch<false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
+}
+
 // ---------------------------------------------------------------- select
 // Pivot k: given the winner over all candidates (its value is the current, pending-updated one),
 // the stop test of _optimizerrlu! (matrixlu.jl:359-368), and on acceptance addpivot!'s swaps as
 // map updates: the rows at positions k and p exchange positions (swaprow!, :254-262), likewise
 // the columns at k and q (swapcol!, :269-275). One thread.
+template <bool COH>
 __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double reltol, double abstol,
                              int32_t* rowpos, int32_t* colpos, int64_t* rowphys, int64_t* colphys,
                              double* pivvals, int64_t rk, int64_t ck, bool has_mxe, double mxe) {
@@ -2294,35 +2491,35 @@ __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double rel
         // whose current value is one of those NaNs
         rp = k;
         cp = k;
-        pr = (int)rowphys[k];
-        pc = (int)colphys[k];
+        pr = (int)ldc<COH>(rowphys + k);
+        pc = (int)ldc<COH>(colphys + k);
         val = __longlong_as_double(0x7ff8000000000000LL);
     }
     const double err = fabs(val);
-    st->error = err;
-    const double maxerror = has_mxe ? mxe : st->maxerror;  // mxe: requested with the candidates
+    stc<COH>(&st->error, err);
+    const double maxerror = has_mxe ? mxe : ldc<COH>(&st->maxerror);  // mxe: requested with the candidates
     if (((fabs(err) < reltol * maxerror) || (fabs(err) < abstol)) && k > 0) {
-        st->done = 1;
+        stc<COH>(&st->done, 1);
         return;
     }
-    st->maxerror = jl_max(maxerror, err);
-    st->p = pr;
-    st->q = pc;
-    st->pval = val;
-    st->np = k + 1;
-    pivvals[k] = val;
+    stc<COH>(&st->maxerror, jl_max(maxerror, err));
+    stc<COH>(&st->p, (int64_t)pr);
+    stc<COH>(&st->q, (int64_t)pc);
+    stc<COH>(&st->pval, val);
+    stc<COH>(&st->np, (int64_t)(k + 1));
+    stc<COH>(pivvals + k, val);
     // swaprow!(k, rp): the physical row at position k moves to position rp
-    if (rk < 0) rk = rowphys[k];
-    rowphys[k] = pr;
-    rowphys[rp] = rk;
-    rowpos[pr] = k;
-    rowpos[rk] = rp;
+    if (rk < 0) rk = ldc<COH>(rowphys + k);
+    stc<COH>(rowphys + k, (int64_t)pr);
+    stc<COH>(rowphys + rp, rk);
+    stc<COH>(rowpos + pr, (int32_t)k);
+    stc<COH>(rowpos + rk, (int32_t)rp);
     // swapcol!(k, cp)
-    if (ck < 0) ck = colphys[k];
-    colphys[k] = pc;
-    colphys[cp] = ck;
-    colpos[pc] = k;
-    colpos[ck] = cp;
+    if (ck < 0) ck = ldc<COH>(colphys + k);
+    stc<COH>(colphys + k, (int64_t)pc);
+    stc<COH>(colphys + cp, ck);
+    stc<COH>(colpos + pc, (int32_t)k);
+    stc<COH>(colpos + ck, (int32_t)cp);
 }
 
 __global__ void k_init_state(RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
@@ -2953,3 +3150,21 @@ void launch_shard_commit(hipStream_t s, const Cand* recv, int nranks, const uint
 }
 
 }  // namespace tci
+
+#ifdef TCI_EXPERIMENT_RT
+namespace tci {
+// register-pressure experiment: one pass with a runtime pending count, no persistent loop
+template <bool EXT, bool COH>
+__global__ __launch_bounds__(kP2Threads) void k_pass_mf_rt(PassK g, SelArgs sel) {
+    __shared__ P2MfLds<kEpochMaxP, EXT> L;
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    CandR best = cand_none();
+    const int r = pass_mf_body<kEpochMaxP, EXT, false, COH>(g, sel, L, best, pt, g.ps);
+    if (r != kMfDone) return;
+    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, 1, 0);
+}
+template __global__ void k_pass_mf_rt<false, false>(PassK, SelArgs);
+template __global__ void k_pass_mf_rt<false, true>(PassK, SelArgs);
+template __global__ void k_pass_mf_rt<true, true>(PassK, SelArgs);
+}  // namespace tci
+#endif

@@ -51,6 +51,9 @@ SIGNATURES = {
     "tci_ctx_stream": ([vp], vp),
     "tci_ctx_synchronize": ([vp], C.c_int),
     "tci_last_kernel_stats": ([vp, C.c_int, pdbl, pi64], C.c_int),
+    "tci_last_kernel_units": ([vp, C.c_int, pdbl, pi64, pi64], C.c_int),
+    "tci_set_rrlu_persist": ([vp, C.c_int], C.c_int),
+    "tci_rrlu_persist_faulted": ([vp], C.c_int),
     "tci_set_timing": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_epochs": ([vp, C.c_int], C.c_int),
@@ -292,6 +295,15 @@ class Context:
         n = C.c_int64()
         self.check(self.lib.tci_last_kernel_stats(self.h, family, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def kernel_units(self, family):
+        """(total ms, launches, units) of a timing family; units = passes for the persistent epoch
+        launches (families 41 / 42), launches otherwise."""
+        ms = C.c_double()
+        n = C.c_int64()
+        u = C.c_int64()
+        self.check(self.lib.tci_last_kernel_units(self.h, family, C.byref(ms), C.byref(n), C.byref(u)))
+        return ms.value, n.value, u.value
 
     @property
     def stream(self):
