@@ -574,7 +574,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     // (persist == 2, a test mode: also when the grid exceeds one workgroup per CU -- it is then NOT
     // co-resident and the launch must give up, after 2 ms instead of 0.5 s, and resume)
     bool persist = c->persist && !c->persist_faulted && shadow && tci::shadow_two_level() && c->ncu > 0 &&
-                   ((grid <= c->ncu && c->pass_gridx == 1) || c->persist == 2);
+                   ((grid <= c->ncu && c->pass_gridx == 1) || c->persist == 2) && tci::epoch_fits(mi, ni, g.cb, grid);
     const long long ptimeout = c->persist == 2 ? 200000 : 50000000;  // 100 MHz ticks
     int64_t nlaunch = 0;  // persistent launches issued (their sync slots)
     if (persist) {

@@ -210,9 +210,11 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
 // workgroups, which must all be resident at once (one per CU). sync: kEpochSlot zeroed words of this
 // launch's own. A launch that finds its grid not co-resident sets st->done = 2 (tci_abi.cpp resumes).
 constexpr int kEpochMaxP = 10;
-constexpr int kEpochSlot = 64;  // unsigned words per launch: ticket at 0, generation at 32
+constexpr int kEpochSlot = 64;  // unsigned words per launch (its ticket at 0; a 256-B line of its own)
 void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
                        long long timeout);
+// the persistent epoch launch's LDS maps hold this shape (n <= 32768, columns per workgroup bounded)
+bool epoch_fits(int m, int n, int cb, int grid);
 void launch_init_state(hipStream_t s, RrluState* st, int32_t* rowpos, int64_t* rowphys, int m,
                        int32_t* colpos, int64_t* colphys, int n);
 // small matrices: the whole rrLU in one workgroup's LDS (same outputs as the pass pipeline:

@@ -1402,9 +1402,24 @@ __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int n
 // (nothing done: the caller runs the exact body). The certificate is derived after the
 // pivot-independent loads are issued, so its pivot-value round trip overlaps theirs.
 constexpr int kMfStop = 0, kMfDone = 1, kMfExact = 2;
+// The persistent epoch kernel's per-pass inputs of pass_mf_body (COH): the pivot k the workgroup
+// selected itself (every workgroup reduces the previous pass's candidates), the positions of its rows
+// and columns (LDS copies, patched by every selection), and the pivot values selected inside the
+// launch (LDS; pivots <= k0 are in the global pivot values).
+struct EpochIn {
+    int a, b;             // pivot k: physical row / column
+    double piv;           // its value
+    const int32_t* lrow;  // LDS: position of tile row r at lrow[r - tile base]
+    const int16_t* lcol;  // LDS: position of the workgroup's column j at lcol[t cb + (j mod cb)], t its tile's
+                          // sequence number among the workgroup's tiles; -1 past n (n <= 32768)
+    const double* lpiv;   // LDS: pivot k0 + 1 + i at lpiv[i]
+    int k0;               // pivots <= k0 were committed before the launch
+    __device__ __forceinline__ double pivot(const double* pv, int t) const { return t > k0 ? lpiv[t - k0 - 1] : pv[t]; }
+};
 template <int P, bool EXT = false, bool RF = false, bool COH = false>
 __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, P2MfLds<P, EXT>& L,
-                                            CandR& best, unsigned long long (&pt)[8], const int Pr = P) {
+                                            CandR& best, unsigned long long (&pt)[8], const int Pr = P,
+                                            const EpochIn* ep = nullptr) {
     static_assert(P >= 1 && P <= kMfMaxP, "at most two MFMA K-steps per tile");
     using Gm = MfGeom<P, EXT>;
     // Pr: the shadow-pending count, P its compile-time bound (register arrays, LDS strides): equal in
@@ -1427,11 +1442,24 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // ms per step; read after the certificate and behind serial map loads, the pivot had been the
     // third or fourth round trip.) Vector loads: as scalar loads they were waited for by the next
     // kernel-argument reload (lgkmcnt(0)).
-    const double certw = sh_cert_load<COH>(pv, k, PE);
-    const int st_done = ldc<true>(&st->done);
-    const int a = (int)ldc<true>(&st->p);
-    const int bq = (int)ldc<true>(&st->q);
-    const double piv = ldc<true>(&st->pval);
+    // COH (the persistent epoch kernel): the pivot comes from the workgroup's own reduction of the
+    // previous pass's candidates, the maps from its LDS copies, the pivots of this launch from LDS
+    double certw;
+    int st_done, a, bq;
+    double piv;
+    if constexpr (COH) {
+        certw = ep->pivot(pv, min(max(k - PE + (int)(threadIdx.x & 63), 0), k));
+        st_done = 0;
+        a = ep->a;
+        bq = ep->b;
+        piv = ep->piv;
+    } else {
+        certw = sh_cert_load<COH>(pv, k, PE);
+        st_done = ldc<true>(&st->done);
+        a = (int)ldc<true>(&st->p);
+        bq = (int)ldc<true>(&st->q);
+        piv = ldc<true>(&st->pval);
+    }
     // thread / workgroup indices: inside the persistent epoch kernel (COH) made opaque per pass, so
     // that nothing derived from them is hoisted out of its pass loop (kept live across every pass,
     // those values spilled the body's registers)
@@ -1444,7 +1472,9 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     const int nq = gx / tiles_r;
     const int wid = xcd_spread(bx, gx);
     const int tr = wid % tiles_r;
-    const int q = rev ? nq - 1 - wid / tiles_r : wid / tiles_r;
+    // (COH: a workgroup keeps its column set in every pass -- its LDS map covers it; the serpentine
+    // order is kept by walking its tiles backwards, which walks the bands backwards as well)
+    const int q = (rev && !COH) ? nq - 1 - wid / tiles_r : wid / tiles_r;
     const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
     const int G = kP2StageCols / cb;
     const int cbs = __builtin_ctz(cb);  // cb is 8 or 16
@@ -1457,6 +1487,18 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     auto col_of = [&](int g0, int lc) -> int {  // global column of staged local column lc
         const int it = g0 + (lc >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
+    };
+    // COH: index of staged local column lc in the workgroup's LDS column map (by tile sequence)
+    [[maybe_unused]] auto lcol_of = [&](int g0, int lc) -> int {
+        const int it = g0 + (lc >> cbs);
+        return ((rev ? ntc - 1 - it : it) << cbs) + (lc & (cb - 1));
+    };
+    // positions of a row of the tile / a staged column: global maps, or (COH) the LDS copies
+    auto rowpos_of = [&](int r) -> int {
+        if constexpr (COH)
+            return ep->lrow[r - tb];
+        else
+            return rowpos[r];
     };
     // Every chunk load is issued unconditionally (a lane past the last column reads the last one,
     // a lane past the last row tile row 0: approx() masks both), so that a fixed number of memory
@@ -1482,12 +1524,12 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // wave activity from the rows of its slice (lanes 0..15 x 4: every row once)
     int rpa[kMfBlk];
 #pragma unroll
-    for (int b = 0; b < kMfBlk; ++b) rpa[b] = ldc<COH>(rowpos + min(sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3), m - 1));
+    for (int b = 0; b < kMfBlk; ++b) rpa[b] = rowpos_of(min(sb + 16 * (lcol >> 2) + 4 * b + (lcol & 3), m - 1));
     // refresh: which of the lane's 16 loaded rows are trailing (the others get shadow 0)
     [[maybe_unused]] int rpt[RF ? 16 : 1];
     if constexpr (RF) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) rpt[i] = ldc<COH>(rowpos + min(rl + i, m - 1));
+        for (int i = 0; i < 16; ++i) rpt[i] = rowpos_of(min(rl + i, m - 1));
     }
     // refresh stores: the shadow as one buffer (the host keeps it below 4 GB for refreshes), the
     // second 16 B of a lane's 32 through a resource 16 B further on (an out-of-range offset stays so)
@@ -1495,10 +1537,14 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     [[maybe_unused]] const auto rsS0 = buf_rsrc(g.S, shb);
     [[maybe_unused]] const auto rsS1 = buf_rsrc(reinterpret_cast<const char*>(g.S) + 16, shb - 16);
     int jst = ntc > 0 ? stage_col(0) : -1;
-    const int cpl = ldc<COH>(colpos + min(max(jst, 0), n - 1));
+    int cpl;
+    if constexpr (COH)
+        cpl = ep->lcol[jst >= 0 ? lcol_of(0, tx) : 0];
+    else
+        cpl = colpos[min(max(jst, 0), n - 1)];
     const int prow = tx - kP2StageCols;  // this thread's tile row (row threads)
     const int rrow = tb + (prow >= 0 ? prow : 0);
-    const int rpl = ldc<COH>(rowpos + min(rrow, m - 1));
+    const int rpl = rowpos_of(min(rrow, m - 1));
     h8v va[2], vb[2];
     const int gc0 = ntc > 0 ? min(G, ntc) * cb : 0;
     const int nch0 = (gc0 + 15) / 16;
@@ -1568,7 +1614,15 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         // rows pivoted before this epoch (and rows past m): 0; pivoted at step rp of it: x_s for
         // s < rp - t0, then the pivot's own x (1, or the pivot when not leftorth), then 0
         const int dd = rpos > k ? Pr : (rpos >= t0 ? rpos - t0 : -1);
-        const double own = leftorth ? 1.0 : (rpos >= t0 && rpos <= k ? ldc<COH>(pv + rpos) : 0.0);
+        double own = 0.0;
+        if (!leftorth) {
+            if constexpr (COH)
+                own = rpos >= t0 && rpos <= k ? ep->pivot(pv, rpos) : 0.0;
+            else
+                own = rpos >= t0 && rpos <= k ? pv[rpos] : 0.0;
+        } else {
+            own = 1.0;
+        }
         _Float16 sl[KS];
 #pragma unroll
         for (int s = 0; s < P; ++s) {
@@ -1675,7 +1729,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             if (r >= m) continue;
             const int j = col_of(g0, lc);
             double v = g.A[r + (int64_t)j * lda];
-            const int rp = ldc<COH>(rowpos + r);
+            const int rp = rowpos_of(r);
             // take v now: a load left in flight by the continue below (into a register the
             // streaming loop reuses) would cost a wait for every load at the loop's head
             asm volatile("" : "+v"(v));
@@ -1756,7 +1810,10 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         g0r = g0;
         if (g0 > 0) {
             jst = stage_col(g0);
-            cpst = (jst >= 0 && jst < n) ? ldc<COH>(colpos + jst) : -1;
+            if constexpr (COH)
+                cpst = jst >= 0 ? ep->lcol[lcol_of(g0, tx)] : -1;
+            else
+                cpst = (jst >= 0 && jst < n) ? colpos[jst] : -1;
             // unconditional (an inactive wave loads two chunks it never reads): loads skipped on
             // some paths into the loop would make its head wait for every load in flight
             load_chunk(g0, gcols, min(rep, nch - 1), va);
@@ -2237,34 +2294,38 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
 }
 
 // ------------------------------------------------------------------ persistent shadow epoch
-// The read-only passes of one shadow epoch (pivots k0 .. k0 + npass - 1, shadow-pending counts
+// The read-only passes of one shadow epoch (passes k0 .. k0 + npass - 1, shadow-pending counts
 // ps0 .. ps0 + npass - 1 <= kEpochMaxP) in ONE launch: the grid stays resident (one 1024-thread
-// workgroup per CU, as the per-pass launches) and hands each commit to the next pass in place of a
-// kernel boundary. Pass bodies are k_pass_mf's (pass_mf_body, COH: its loads and stores of the
-// handed-over data are `sc1`), the tail is pass_tail's ticket, monotonic over the launch:
-//   every wave drains its stores (X / Y slots), the workgroup publishes its candidate (sc1) and adds
-//   to the ticket; the add that completes pass i's count (i + 1) G commits pivot k + 1 with sc1
-//   stores, drains them and sets the generation word to i + 1 (sc1); every other workgroup polls it
-//   (sc1 loads, s_sleep) -- MI355X_MICROARCH.md's hand-off table, first row, both hops.
-// Co-residency is not assumed: a workgroup that waits longer than `timeout` ticks (100 MHz) marks
-// the ticket ABORT by a compare-and-swap that succeeds only while the count is short, so either
-// every workgroup sees the count complete or every one sees ABORT; the aborting one sets
-// st->done = 2 and every later pass launch returns at once. Nothing is committed for the aborted
-// pass, so the host resumes with per-pass launches at pass st->np - 1 (all pass writes are
-// idempotent) and stops using the persistent launch on that context.
+// workgroup per CU, as the per-pass launches) and no pass ends in a kernel boundary. The pass body is
+// k_pass_mf's (pass_mf_body, COH); between two passes (_optimizerrlu!'s loop, matrixlu.jl:356-369):
+//   * every wave drains its stores (the X / Y slots of x_k, y_k), the workgroup publishes its candidate
+//     (sc1) and adds to the launch's ticket (monotonic: pass i is complete at (i + 1) G);
+//   * EVERY workgroup polls the ticket until pass i is complete, reads all G candidates (sc1) and
+//     reduces them itself -- the same winner everywhere (cand_better is a strict total order) -- runs
+//     the stop test (matrixlu.jl:359-368) and applies the swaps (addpivot!'s swaprow! / swapcol!,
+//     :254-275) to its LDS copies of the positions of its rows and columns: no committing workgroup,
+//     no flag, no state read back (MI355X_MICROARCH.md hand-off table, first row: sc1 stores drained
+//     before the ticket add, sc1 loads after the poll);
+//   * the global state is written, stores only, by the workgroups that hold it: the row swap by the
+//     q = 0 workgroup of each row tile (the threads that own the two rows), the column swap by the
+//     tr = 0 workgroup owning each column, the pivot value and rrLU state by workgroup 0. Nothing in
+//     the launch reads them back; the next launch does.
+// Co-residency is not assumed: a workgroup that waits longer than `timeout` ticks (100 MHz) marks the
+// ticket ABORT by a compare-and-swap that succeeds only while the count is short, so either every
+// workgroup sees the count complete or every one sees ABORT; the aborting one sets st->done = 2 and
+// every later pass launch returns at once. Nothing is selected for the aborted pass, so the host
+// resumes with per-pass launches at pass st->np - 1 (every pass write is idempotent). A certificate
+// that fails (uniform) or an all-NaN trailing block ends the launch the same way with st->done = 3.
 constexpr unsigned kEpochAbort = 0x80000000u;
-constexpr int kEpochGen = 32;  // the generation word's offset in a launch's sync slot (own 128-B line)
-static_assert(kEpochGen + 1 <= kEpochSlot, "sync slot");
+constexpr int kEpochMaxCols = 15360;  // columns per workgroup the LDS column map holds (int16 positions)
 
-
-// thread 0 of a workgroup that is not the committer: wait for generation `want`. 1: go on, 0: abort
-__device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned* gen, unsigned want, unsigned target,
-                                          long long timeout, RrluState* st) {
+// thread 0: wait until `target` arrivals. 1: complete, 0: abort
+__device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned target, long long timeout, RrluState* st) {
     long long t0 = (long long)wall_clock64();
     for (;;) {
-        if (ldc<true>(gen) >= want) return 1;
         unsigned tv = ldc<true>(ticket);
         if (tv & kEpochAbort) return 0;
+        if (tv >= target) return 1;
         if ((long long)wall_clock64() - t0 > timeout) {
             // a workgroup is missing (not co-resident) -- or slow: abort only while the count is short
             while (!(tv & kEpochAbort) && tv < target) {
@@ -2275,8 +2336,7 @@ __device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned* gen, unsig
                     return 0;
                 }
             }
-            if (tv & kEpochAbort) return 0;
-            t0 = (long long)wall_clock64();  // every workgroup arrived: the commit is on its way
+            return (tv & kEpochAbort) ? 0 : 1;
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -2285,18 +2345,38 @@ __device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned* gen, unsig
 struct EpochArgs {
     int npass;         // read-only passes in this launch (k = g.k .. g.k + npass - 1)
     int serp;          // serpentine order: pass k walks backwards when (k + 1) is odd
-    unsigned* sync;    // this launch's words, zero at launch: [0] ticket, [kEpochGen] generation
+    unsigned* sync;    // this launch's ticket, zero at launch
     long long timeout; // ticks a workgroup waits for the others before it gives up (abort)
 };
 
 template <bool EXT>
 __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs sel0, EpochArgs e) {
     __shared__ __attribute__((aligned(16))) char lds[sizeof(P2MfLds<kEpochMaxP, EXT>)];
+    __shared__ int32_t lrow[kRowsPerTile];
+    __shared__ int16_t lcol[kEpochMaxCols];
+    __shared__ double lpiv[kEpochMaxP];
     __shared__ int s_go;
+    __shared__ CandR s_w;
     [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned G = gridDim.x;
-    unsigned* const ticket = e.sync;
-    unsigned* const gen = e.sync + kEpochGen;
+    RrluState* const st = sel0.st;
+    // geometry of the workgroup's rows and columns (the body's, with the column set fixed: q)
+    const int m = g0.m, n = g0.n, cb = g0.cb, cbs = __builtin_ctz(g0.cb);
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile, tiles_c = (n + cb - 1) / cb;
+    const int nq = (int)G / tiles_r;
+    const int wid = xcd_spread(blockIdx.x, G);
+    const int tr = wid % tiles_r, q = wid / tiles_r, tb = tr * kRowsPerTile;
+    const int ntc = q < tiles_c ? (tiles_c - 1 - q) / nq + 1 : 0;
+    const int ncols = ntc * cb;  // <= kEpochMaxCols (host)
+    // the maps as the previous launch left them (plain loads: written before this launch)
+    for (int t = threadIdx.x; t < kRowsPerTile; t += kP2Threads) lrow[t] = tb + t < m ? sel0.rowpos[tb + t] : -1;
+    for (int x = threadIdx.x; x < ncols; x += kP2Threads) {
+        const int j = ((q + (x >> cbs) * nq) << cbs) + (x & (cb - 1));
+        lcol[x] = (int16_t)(j < n ? sel0.colpos[j] : -1);
+    }
+    EpochIn ein{(int)st->p, (int)st->q, st->pval, lrow, lcol, lpiv, g0.k};
+    double maxerror = st->maxerror;
+    __syncthreads();
     for (int i = 0; i < e.npass; ++i) {
         PassK g = g0;
         SelArgs sel = sel0;
@@ -2304,68 +2384,125 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
         g.ps = g0.ps + i;
         g.pe = g0.pe + i;
         g.rev = e.serp ? ((g.k + 1) & 1) : 0;
-        sel.selk = g.k + 1;  // the host never puts the last pass in an epoch launch
+        const int K = g.k + 1;  // the pivot this pass selects (the host never puts the last pass here)
+        sel.selk = K;
         CandR best = cand_none();
-        int r = pass_mf_body<kEpochMaxP, EXT, false, true>(g, sel, *reinterpret_cast<P2MfLds<kEpochMaxP, EXT>*>(lds),
-                                                             best, pt, g.ps);
-        if (r == kMfExact) {
-            // uniform (every workgroup derives the same certificate, before any store of the pass):
-            // the exact bodies are not in this kernel (their registers would spill its MFMA bodies),
-            // so the launch ends here and the host resumes at this pass with per-pass launches
-            // (st->done = 3, set by workgroup 0; nothing of the pass was written)
-            if (blockIdx.x == 0 && threadIdx.x == 0 && ldc<true>(&sel.st->done) == 0) {
-                stc<true>(&sel.st->done, 3);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+        const int r = pass_mf_body<kEpochMaxP, EXT, false, true>(g, sel, *reinterpret_cast<P2MfLds<kEpochMaxP, EXT>*>(lds),
+                                                                 best, pt, g.ps, &ein);
+        if (r != kMfDone) {
+            // the certificate failed (uniform: every workgroup derives it from the same pivots),
+            // before any store of the pass: the host resumes here with the per-pass exact bodies
+            if (blockIdx.x == 0 && threadIdx.x == 0 && ldc<true>(&st->done) == 0) stc<true>(&st->done, 3);
             return;
         }
-        if (r != kMfDone) return;  // the stop test fired: every workgroup read the same state
-        // ---- tail: every wave's X / Y slot stores drained before the workgroup's ticket
+        // ---- every wave's X / Y slot stores drained before the workgroup's ticket
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         block_reduce_cand<kP2Threads>(best);  // (its barrier orders the waves' drains before the add)
         const unsigned target = (unsigned)(i + 1) * G;
         if (threadIdx.x == 0) {
             store_cand_sc1(g.cand + blockIdx.x, best);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned old = __hip_atomic_fetch_add((gptr<unsigned>)ticket, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            s_go = (old & kEpochAbort) ? 0
-                   : old + 1 == target ? 2
-                                        : epoch_wait(ticket, gen, (unsigned)(i + 1), target, e.timeout, sel.st);
+            const unsigned old =
+                __hip_atomic_fetch_add((gptr<unsigned>)e.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_go = (old & kEpochAbort) ? 0 : old + 1 == target ? 1 : epoch_wait(e.sync, target, e.timeout, st);
         }
         __syncthreads();
-        const int go = s_go;
-        if (go == 0) return;
-        if (go == 2) {
-            // the last arrival: pass_tail's reduction and commit, then the generation word
-            int64_t rk = -1, ck = -1;
-            double mxe = 0.0;
-            if (threadIdx.x == 0) {
-                rk = ldc<true>(sel.rowphys + sel.selk);
-                ck = ldc<true>(sel.colphys + sel.selk);
-                mxe = ldc<true>(&sel.st->maxerror);
+        if (!s_go) return;
+        // ---- every workgroup: the winner of all G candidates
+        CandR w = threadIdx.x < G ? load_cand_sc1(g.cand + threadIdx.x) : cand_none();
+        __syncthreads();  // block_reduce_cand's LDS slots are reused
+        block_reduce_cand<kP2Threads>(w);
+        if (threadIdx.x == 0) s_w = w;
+        __syncthreads();
+        w = s_w;
+        const double err = fabs(w.val);
+        if (!(w.v >= 0.0)) {  // every trailing value NaN: the per-pass path commits it (commit_pivot)
+            if (blockIdx.x == 0 && threadIdx.x == 0) stc<true>(&st->done, 3);
+            return;
+        }
+        if ((err < sel.reltol * maxerror) || (err < sel.abstol)) {  // the stop test (K >= 1)
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                st->error = err;
+                st->done = 1;
             }
-            constexpr int CPT = kMaxPassGrid / kP2Threads;
-            CandR cs[CPT];
-#pragma unroll
-            for (int u = 0; u < CPT; ++u) {
-                const int c = threadIdx.x + u * kP2Threads;
-                cs[u] = c < (int)G ? load_cand_sc1(g.cand + c) : cand_none();
-            }
-            CandR w = cs[0];
-#pragma unroll
-            for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
-            __syncthreads();  // block_reduce_cand's LDS slots are reused
-            block_reduce_cand<kP2Threads>(w);
-            if (threadIdx.x == 0) {
-                commit_pivot<true>(sel.selk, w, sel.st, sel.reltol, sel.abstol, sel.rowpos, sel.colpos, sel.rowphys,
-                                   sel.colphys, sel.pivvals, rk, ck, true, mxe);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stc<true>(gen, (unsigned)(i + 1));
+            return;
+        }
+        const int rp = w.rpos, cp = w.cpos, pr = w.pr, pc = w.pc;
+        // swaprow!(K, rp) / swapcol!(K, cp) on the LDS maps; the owners store the global maps
+        for (int t = threadIdx.x; t < kRowsPerTile; t += kP2Threads) {
+            const int pos = lrow[t];
+            if (pos == rp) {  // row pr: to position K
+                lrow[t] = K;
+                if (q == 0) {
+                    sel.rowphys[K] = pr;
+                    sel.rowpos[pr] = K;
+                }
+            } else if (pos == K) {  // the row at position K: to rp
+                lrow[t] = rp;
+                if (q == 0) {
+                    sel.rowphys[rp] = tb + t;
+                    sel.rowpos[tb + t] = rp;
+                }
             }
         }
-        __syncthreads();  // s_go and the reduction's LDS are reused by the next pass
+        for (int x = threadIdx.x; x < ncols; x += kP2Threads) {
+            const int pos = lcol[x];
+            if (pos == cp || pos == K) {
+                const int j = ((q + (x >> cbs) * nq) << cbs) + (x & (cb - 1));
+                if (pos == cp) {
+                    lcol[x] = (int16_t)K;
+                    if (tr == 0) {
+                        sel.colphys[K] = pc;
+                        sel.colpos[pc] = K;
+                    }
+                } else {
+                    lcol[x] = (int16_t)cp;
+                    if (tr == 0) {
+                        sel.colphys[cp] = j;
+                        sel.colpos[j] = cp;
+                    }
+                }
+            }
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->error = err;
+            st->maxerror = jl_max(maxerror, err);
+            st->p = pr;
+            st->q = pc;
+            st->pval = w.val;
+            st->np = K + 1;
+            sel.pivvals[K] = w.val;
+        }
+        if (threadIdx.x == 0) lpiv[i] = w.val;
+        maxerror = jl_max(maxerror, err);
+        ein.a = pr;
+        ein.b = pc;
+        ein.piv = w.val;
+        __syncthreads();  // the maps, lpiv, s_go and the reduction's LDS before the next pass
     }
+}
+
+void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
+                       long long timeout) {
+    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
+                      g.ticket, g.reltol, g.abstol,  g.selk,    nullptr, 0};
+    const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
+                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
+                  g.pe, g.ps, g.nbs};
+    const EpochArgs e{npass, serp, sync, timeout};
+    if (g.pe > g.ps)
+        hipLaunchKernelGGL((k_pass_mf_epoch<true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
+    else
+        hipLaunchKernelGGL((k_pass_mf_epoch<false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
+}
+
+// whether the persistent epoch launch takes this shape: its LDS column map holds int16 positions of
+// at most kEpochMaxCols columns per workgroup
+bool epoch_fits(int m, int n, int cb, int grid) {
+    const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile, tiles_c = (n + cb - 1) / cb;
+    const int nq = grid / tiles_r;
+    if (nq < 1 || n > 32768) return false;
+    return (int64_t)((tiles_c + nq - 1) / nq) * cb <= kEpochMaxCols;
 }
 
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
@@ -2459,20 +2596,6 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
 #undef TCI_PASS_CASE
     default: break;
     }
-}
-
-void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
-                       long long timeout) {
-    const SelArgs sel{g.rowpos, g.colpos, g.rowphys, g.colphys, g.pivvals, g.st,
-                      g.ticket, g.reltol, g.abstol,  g.selk,    nullptr, 0};
-    const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
-                  g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
-                  g.pe, g.ps, g.nbs};
-    const EpochArgs e{npass, serp, sync, timeout};
-    if (g.pe > g.ps)
-        hipLaunchKernelGGL((k_pass_mf_epoch<true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
-    else
-        hipLaunchKernelGGL((k_pass_mf_epoch<false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
 }
 
 // ---------------------------------------------------------------- select
