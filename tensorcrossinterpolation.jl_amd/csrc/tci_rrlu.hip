@@ -2399,8 +2399,12 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         block_reduce_cand<kP2Threads>(best);  // (its barrier orders the waves' drains before the add)
         const unsigned target = (unsigned)(i + 1) * G;
+        // candidates double-buffered by pass parity: a workgroup that has finished pass i's reduction
+        // may publish pass i + 1's candidate while another still reads pass i's (it cannot get two
+        // passes ahead: pass i + 1 completes only once every workgroup has read pass i's records)
+        Cand* const cbuf = g.cand + (i & 1) * G;
         if (threadIdx.x == 0) {
-            store_cand_sc1(g.cand + blockIdx.x, best);
+            store_cand_sc1(cbuf + blockIdx.x, best);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned old =
                 __hip_atomic_fetch_add((gptr<unsigned>)e.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2409,7 +2413,7 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
         __syncthreads();
         if (!s_go) return;
         // ---- every workgroup: the winner of all G candidates
-        CandR w = threadIdx.x < G ? load_cand_sc1(g.cand + threadIdx.x) : cand_none();
+        CandR w = threadIdx.x < G ? load_cand_sc1(cbuf + threadIdx.x) : cand_none();
         __syncthreads();  // block_reduce_cand's LDS slots are reused
         block_reduce_cand<kP2Threads>(w);
         if (threadIdx.x == 0) s_w = w;
