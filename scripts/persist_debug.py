@@ -28,4 +28,6 @@ for persist in (0, 1):
     print(f"persist={persist} kinds={os.environ.get('TCI_EPOCH_KINDS', '3')} npivot {lu.npivot}/{ref.npivot} "
           f"first bad pivot {bad[:5]} L cols differ {list(Ld)[:8]} U rows differ {list(Ud)[:8]} "
           f"faulted={c.lib.tci_rrlu_persist_faulted(c.h)}")
+    print("   rows", list(rp[:8]), "cols", list(cp[:8]), "piv", [float(x) for x in np.diag(lu.U)[:5]] if hasattr(lu, 'U') else '')
+    print("   ref  ", list(ref.rowpermutation[:8]), "cols", list(ref.colpermutation[:8]))
     c.close()

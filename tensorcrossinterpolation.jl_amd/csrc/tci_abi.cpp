@@ -53,6 +53,7 @@ struct tci_ctx {
     int persist = 1;       // read-only passes of a shadow epoch as one persistent launch (env TCI_RRLU_PERSIST=0)
     int persist_faulted = 0;  // such a launch found its grid not co-resident: per-pass launches from then on
     int persist_kinds = 3;    // diagnostic (env TCI_EPOCH_KINDS): bit 0 first shadow epochs, bit 1 later ones (EXT)
+    int persist_maxpass = 1 << 30;  // diagnostic (env TCI_EPOCH_MAXPASS): passes per persistent launch at most
     unsigned* esync = nullptr;  // their sync slots (tci_rrlu.hip k_pass_mf_epoch), one per launch
     size_t capEsync = 0;
     int dense = tci::kDenseAll;  // fp64 MFMA forms of the factors / solve (env TCI_DENSE_MFMA mask)
@@ -597,7 +598,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
                 const bool ro = !s.flush && !s.refresh && !s.last;
                 if (persist && ro && kk >= 1 && s.PS <= tci::kEpochMaxP && (c->persist_kinds & (s.PE > s.PS ? 2 : 1))) {
                     int np = 1;  // the run of read-only passes that follows (te, ts do not move in it)
-                    for (;; ++np) {
+                    for (; np < c->persist_maxpass; ++np) {
                         const Sched t = sched(kk + np, te, ts);
                         if (t.flush || t.refresh || t.last || t.PS > tci::kEpochMaxP) break;
                     }
@@ -1014,6 +1015,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = atoi(e) != 0;
     if (const char* e = getenv("TCI_EPOCH_KINDS")) c->persist_kinds = atoi(e);
+    if (const char* e = getenv("TCI_EPOCH_MAXPASS")) c->persist_maxpass = std::max(1, atoi(e));
     if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
     if (const char* e = getenv("TCI_C128_SH")) c->c128_sh = atoi(e) != 0;
     if (const char* e = getenv("TCI_DENSE_MFMA")) c->dense = std::max(0, std::min(atoi(e), (int)tci::kDenseAll));

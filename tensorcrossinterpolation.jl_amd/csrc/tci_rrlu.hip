@@ -2309,7 +2309,9 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
 //   * the global state is written, stores only, by the workgroups that hold it: the row swap by the
 //     q = 0 workgroup of each row tile (the threads that own the two rows), the column swap by the
 //     tr = 0 workgroup owning each column, the pivot value and rrLU state by workgroup 0. Nothing in
-//     the launch reads them back; the next launch does.
+//     the launch reads them back; the next launch does. They are sc1 (write-through) stores: a
+//     position's entry (rowphys[K]) is written by different workgroups in different passes, and
+//     plain stores would reach memory in the order the XCD L2s write back at the kernel's end.
 // Co-residency is not assumed: a workgroup that waits longer than `timeout` ticks (100 MHz) marks the
 // ticket ABORT by a compare-and-swap that succeeds only while the count is short, so either every
 // workgroup sees the count complete or every one sees ABORT; the aborting one sets st->done = 2 and
@@ -2426,8 +2428,8 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
         }
         if ((err < sel.reltol * maxerror) || (err < sel.abstol)) {  // the stop test (K >= 1)
             if (blockIdx.x == 0 && threadIdx.x == 0) {
-                st->error = err;
-                st->done = 1;
+                stc<true>(&st->error, err);
+                stc<true>(&st->done, 1);
             }
             return;
         }
@@ -2438,14 +2440,14 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
             if (pos == rp) {  // row pr: to position K
                 lrow[t] = K;
                 if (q == 0) {
-                    sel.rowphys[K] = pr;
-                    sel.rowpos[pr] = K;
+                    stc<true>(sel.rowphys + K, (int64_t)pr);
+                    stc<true>(sel.rowpos + pr, (int32_t)K);
                 }
             } else if (pos == K) {  // the row at position K: to rp
                 lrow[t] = rp;
                 if (q == 0) {
-                    sel.rowphys[rp] = tb + t;
-                    sel.rowpos[tb + t] = rp;
+                    stc<true>(sel.rowphys + rp, (int64_t)(tb + t));
+                    stc<true>(sel.rowpos + tb + t, (int32_t)rp);
                 }
             }
         }
@@ -2456,26 +2458,26 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
                 if (pos == cp) {
                     lcol[x] = (int16_t)K;
                     if (tr == 0) {
-                        sel.colphys[K] = pc;
-                        sel.colpos[pc] = K;
+                        stc<true>(sel.colphys + K, (int64_t)pc);
+                        stc<true>(sel.colpos + pc, (int32_t)K);
                     }
                 } else {
                     lcol[x] = (int16_t)cp;
                     if (tr == 0) {
-                        sel.colphys[cp] = j;
-                        sel.colpos[j] = cp;
+                        stc<true>(sel.colphys + cp, (int64_t)j);
+                        stc<true>(sel.colpos + j, (int32_t)cp);
                     }
                 }
             }
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->error = err;
-            st->maxerror = jl_max(maxerror, err);
-            st->p = pr;
-            st->q = pc;
-            st->pval = w.val;
-            st->np = K + 1;
-            sel.pivvals[K] = w.val;
+            stc<true>(&st->error, err);
+            stc<true>(&st->maxerror, jl_max(maxerror, err));
+            stc<true>(&st->p, (int64_t)pr);
+            stc<true>(&st->q, (int64_t)pc);
+            stc<true>(&st->pval, w.val);
+            stc<true>(&st->np, (int64_t)(K + 1));
+            stc<true>(sel.pivvals + K, w.val);
         }
         if (threadIdx.x == 0) lpiv[i] = w.val;
         maxerror = jl_max(maxerror, err);
