@@ -186,6 +186,17 @@ int tci_func_create_host(tci_ctx* ctx, tci_host_fn fn, void* user, const int32_t
 int tci_func_create_c128(tci_ctx* ctx, const tci_func* const* re, int32_t nre,
                          const tci_func* const* im, int32_t nim, tci_func** out);
 
+/* Batch evaluation with DEVICE-RESIDENT index tables and no host synchronisation (the column-sharded
+ * evaluation's per-rank block): I (m x nl) and J (n x nr) device int32 tables (row-major
+ * entries, 1-based), Pi into d_out (device, ld ldo) as tci_batcheval_d; the batch's max |value| is
+ * folded into *d_maxbits, a device uint64 holding the bits of a running maximum (atomic max of the
+ * non-negative doubles' bit patterns: NaN is the largest, as Julia's max propagates it) that the caller
+ * zeroes when a maximum starts -- updatemaxsample! (tensorci2.jl:636-638) over many batches, reduced
+ * over the ranks once with tci_comm_allreduce_max_u64_d. Stream-ordered on the context stream; catalog
+ * integrands only (not TCI_F_HOST, TCI_F_C128). Replaces _batchevaluate_dispatch
+ * (batcheval.jl:131-175) for a BatchEvaluator whose sets already live on the device. */
+int tci_batcheval_dd(tci_ctx* ctx, const tci_func* f, const int32_t* d_I, int64_t m, int32_t nl, const int32_t* d_J,
+                     int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo, uint64_t* d_maxbits);
 /* ----------------------------------------------------------- batch eval
  * Replaces _batchevaluate_dispatch (batcheval.jl:131-175) plus maxabs (util.jl:34-43) as used by
  * updatemaxsample! (tensorci2.jl:636-638).

@@ -2,5 +2,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for mp in 2 3 9; do TCI_EPOCH_MAXPASS=$mp timeout -k 10 120 python -u scripts/persist_debug.py 2100 1900 40 10 1 || exit 1; done
-TCI_RRLU_SERP=0 timeout -k 10 120 python -u scripts/persist_debug.py 2100 1900 40 10 1 || exit 1
+for ep in 3 1; do timeout -k 10 120 python -u scripts/persist_debug.py 2100 1900 150 10 $ep || exit 1; done

@@ -766,13 +766,21 @@ int host_batcheval(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, 
 
 // batch evaluation into a device buffer (column-major, ld ldo). *maxabs = max|out|.
 // batch evaluation launches only (no synchronisation); c->maxbits receives max|out| bits
+// maxbits: where the batch's max |value| bits are folded (atomic max); null = the context's word,
+// zeroed first (a running maximum passed in is not)
 int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl,
-                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo) {
+                     const int32_t* dJ, int64_t n, int32_t nr, int32_t M, double* dout, int64_t ldo,
+                     unsigned long long* maxbits = nullptr) {
     if (nl + M + nr != f->L) return set_err(c, TCI_ERR_ARG, "Invalid number of central indices");
     if (M < 0 || M > 1) return set_err(c, TCI_ERR_ARG, "only M = 0 or M = 1 centre legs are supported");
     const int D = M ? f->localdims[nl] : 1;
     if (ldo < m * D) return set_err(c, TCI_ERR_ARG, "ldo < m * prod(centre dims)");
-    HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    if (maxbits && f->kind == TCI_F_HOST)
+        return set_err(c, TCI_ERR_ARG, "a host integrand (TCI_F_HOST) needs tci_batcheval_d");
+    if (!maxbits) {
+        maxbits = c->maxbits;
+        HIPCHK(c, hipMemsetAsync(c->maxbits, 0, sizeof(unsigned long long), c->stream));
+    }
     if (f->kind == TCI_F_C128)
         return set_err(c, TCI_ERR_ARG, "a ComplexF64 integrand needs the ComplexF64 entries (*_c128_*)");
     if (f->kind == TCI_F_HOST) return host_batcheval(c, f, dI, m, nl, dJ, n, nr, M, D, dout, ldo);
@@ -783,7 +791,7 @@ int batcheval_launch(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
         if (sb > 0 && (st = ensure(c, (char**)&c->scratch, &c->capScratch, (size_t)sb))) return st;
         ev_begin(c, 1);
         tci::launch_batcheval(c->stream, fv, dI, (int)m, nl, dJ, (int)n, nr, M, D, dout, ldo,
-                              c->maxbits, c->scratch);
+                              maxbits, c->scratch);
         ev_end(c);
         HIPCHK(c, hipGetLastError());
     }
@@ -1322,6 +1330,15 @@ int tci_batcheval_d(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, 
     if (bi) HIPCHK(c, hipMemcpyAsync(c->dI, c->hin, bi, hipMemcpyHostToDevice, c->stream));
     if (bj) HIPCHK(c, hipMemcpyAsync(c->dJ, c->hin + bi, bj, hipMemcpyHostToDevice, c->stream));
     return batcheval_device(c, f, c->dI, m, nl, c->dJ, n, nr, M, d_out, ldo, maxabs);
+}
+
+int tci_batcheval_dd(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m, int32_t nl, const int32_t* dJ,
+                     int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo, uint64_t* d_maxbits) {
+    if (!c || !f || !d_maxbits || (m > 0 && nl > 0 && !dI) || (n > 0 && nr > 0 && !dJ)) return TCI_ERR_ARG;
+    if (f->kind == TCI_F_C128)
+        return set_err(c, TCI_ERR_ARG, "a ComplexF64 integrand needs the ComplexF64 entries (*_c128_*)");
+    return batcheval_launch(c, f, dI, m, nl, dJ, n, nr, M, d_out, ldo,
+                            reinterpret_cast<unsigned long long*>(d_maxbits));
 }
 
 int tci_batcheval_h(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, int32_t nl,

@@ -64,7 +64,7 @@ static constexpr int32_t kBig = 0x7fffffff;
 
 // Shadow element: fp16 (2 B) or fp32 (4 B). The fp16 shadow holds s * v with a power-of-two scale
 // s per epoch (the pivots between two write-backs): the stale trailing values of an epoch are
-// bounded by B (below), and s = 2^(14 - ilogb B) maps them below 2^15 < 65504. The scale is a
+// bounded by B (below), and s = 2^(13 - ilogb B) maps them below 2^14 < 65504. The scale is a
 // pure function of the committed pivot values, so the pass that writes the shadow and the passes
 // that read it derive the same s. 0 (search off) when B is outside [2^-100, 2^100] or not finite.
 constexpr bool kShHalf = TCI_SH_HALF != 0;
@@ -74,10 +74,16 @@ typedef _Float16 shT;
 typedef float shT;
 #endif
 
+// s = 2^(13 - ilogb B) maps the stale values below 2^14 and leaves one bit of headroom for the
+// pending updates: the certificate needs max |pivot_s| s <= 2^15 (the y's are split into fp16), i.e.
+// pivots up to 2 B. (Round 4 used 2^(14 - ilogb B): the first shadow epoch after pass 0, where B is
+// |pivot 0| = max |A| and the Schur complement's pivots of a random matrix grow past it, then failed
+// its certificate at every pass and ran the exact body -- 8 of every factorisation's passes.)
+constexpr int kShExp = 13;
 __device__ __forceinline__ double sh_scale(double B) {
     if (!kShHalf) return 1.0;
     if (!(B >= 0x1p-100 && B <= 0x1p100)) return 0.0;
-    return ldexp(1.0, 14 - ilogb(B));
+    return ldexp(1.0, kShExp - ilogb(B));
 }
 
 // Bound on the stale trailing values of the epoch whose first pending pivot is t0. t0 = 0: the
@@ -1563,6 +1569,15 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                  stager ? ldy : ldx, PE - 1);
     }
     const ShCert cert = sh_cert(certw, k, Pr, PE, g.nbs > 0 ? g.nbs : Pr);
+#ifdef TCI_EPOCH_DEBUG
+    {
+        const double c0 = readlane_dbl(certw, 0), c1 = readlane_dbl(certw, 1), c2 = readlane_dbl(certw, 2),
+                     c3 = readlane_dbl(certw, 3), c4 = readlane_dbl(certw, 4);
+        if (tx == 0 && bx == 0 && k < 12)
+            printf("[%s k=%d Pr=%d PE=%d nbs=%d] cert ok=%d eps=%g shs=%g pv lanes %.17g %.17g %.17g %.17g %.17g\n",
+                   COH ? "epoch" : "pass", k, Pr, PE, g.nbs, (int)cert.ok, cert.eps, cert.shs, c0, c1, c2, c3, c4);
+    }
+#endif
     if (!cert.ok) return kMfExact;
     const float eps = (float)(cert.eps * (1.0 + 0x1p-20));
     const double shs = cert.shs;
@@ -2362,6 +2377,9 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
     [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned G = gridDim.x;
     RrluState* const st = sel0.st;
+    // a launch enqueued after the factorisation stopped (or after an earlier persistent launch ended
+    // early, st->done = 2 / 3: the host resumes before this launch's passes) does nothing
+    if (st->done) return;
     // geometry of the workgroup's rows and columns (the body's, with the column set fixed: q)
     const int m = g0.m, n = g0.n, cb = g0.cb, cbs = __builtin_ctz(g0.cb);
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile, tiles_c = (n + cb - 1) / cb;
@@ -2434,6 +2452,10 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf_epoch(PassK g0, SelArgs 
             return;
         }
         const int rp = w.rpos, cp = w.cpos, pr = w.pr, pc = w.pc;
+#ifdef TCI_EPOCH_DEBUG
+        if (threadIdx.x == 0 && blockIdx.x < 3 && K < 12)
+            printf("[epoch wg %d] K=%d pr=%d pc=%d rp=%d cp=%d val=%.17g a2=%.17g\n", (int)blockIdx.x, K, pr, pc, rp, cp, w.val, w.v);
+#endif
         // swaprow!(K, rp) / swapcol!(K, cp) on the LDS maps; the owners store the global maps
         for (int t = threadIdx.x; t < kRowsPerTile; t += kP2Threads) {
             const int pos = lrow[t];
@@ -2615,6 +2637,9 @@ __device__ void commit_pivot(int k, const CandR& best, RrluState* st, double rel
                              double* pivvals, int64_t rk, int64_t ck, bool has_mxe, double mxe) {
     int pr = best.pr, pc = best.pc, rp = best.rpos, cp = best.cpos;
     double val = best.val;
+#ifdef TCI_EPOCH_DEBUG
+    if (k < 12) printf("[pass] K=%d pr=%d pc=%d rp=%d cp=%d val=%.17g a2=%.17g\n", k, pr, pc, rp, cp, val, best.v);
+#endif
     if (!(best.v >= 0.0)) {
         // every trailing value is NaN: Julia keeps (first(rows), first(cols)) = positions (k, k),
         // whose current value is one of those NaNs

@@ -25,7 +25,7 @@ def split(v):
 def sh_scale(B):
     if not (2.0 ** -100 <= B <= 2.0 ** 100):
         return 0.0
-    return math.ldexp(1.0, 14 - (math.frexp(B)[1] - 1))
+    return math.ldexp(1.0, 13 - (math.frexp(B)[1] - 1))  # tci_rrlu.hip sh_scale (kShExp = 13)
 
 
 def lu_states(A, steps):
