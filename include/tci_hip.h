@@ -125,7 +125,8 @@ int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
  * bitwise identical (replaces the per-pivot loop of _optimizerrlu!, matrixlu.jl:356-369). If the grid
  * is found not co-resident (another process holds CUs) the launch gives up after 0.5 s, the
  * factorisation resumes with per-pass launches and this context stops using the persistent form
- * (tci_rrlu_persist_faulted). Default on (env TCI_RRLU_PERSIST=0: off); enabled resets the flag.
+ * (tci_rrlu_persist_faulted). Default OFF (measured slower than the per-pass launches, DESIGN.md K2;
+ * env TCI_RRLU_PERSIST=1: on); enabled resets the flag.
  * enabled = 2 is a test mode: the persistent launch is used even where its grid exceeds one workgroup
  * per CU (TCI_PASS_GRIDX > 1), i.e. where it is NOT co-resident, and gives up after 2 ms, so that the
  * give-up-and-resume path runs. */

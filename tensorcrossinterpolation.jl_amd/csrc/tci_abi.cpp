@@ -50,7 +50,8 @@ struct tci_ctx {
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
     int mid_path = 1;      // persistent LDS-resident rrLU for mid-size matrices (env TCI_RRLU_MID=0)
     int mid_faulted = 0;   // its grid barrier timed out once on this context: pass pipeline from then on
-    int persist = 1;       // read-only passes of a shadow epoch as one persistent launch (env TCI_RRLU_PERSIST=0)
+    int persist = 0;       // read-only passes of a shadow epoch as one persistent launch (env TCI_RRLU_PERSIST=1;
+                           // off by default: measured slower)
     int persist_faulted = 0;  // such a launch found its grid not co-resident: per-pass launches from then on
     int persist_kinds = 3;    // diagnostic (env TCI_EPOCH_KINDS): bit 0 first shadow epochs, bit 1 later ones (EXT)
     int persist_maxpass = 1 << 30;  // diagnostic (env TCI_EPOCH_MAXPASS): passes per persistent launch at most

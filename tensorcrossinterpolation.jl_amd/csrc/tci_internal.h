@@ -209,7 +209,10 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
 // pending counts g.ps .. g.ps + npass - 1 <= kEpochMaxP, g.pe > g.ps: EXT) in one launch of `grid`
 // workgroups, which must all be resident at once (one per CU). sync: kEpochSlot zeroed words of this
 // launch's own. A launch that finds its grid not co-resident sets st->done = 2 (tci_abi.cpp resumes).
-constexpr int kEpochMaxP = 10;
+#ifndef TCI_EPOCH_MAXP
+#define TCI_EPOCH_MAXP 10
+#endif
+constexpr int kEpochMaxP = TCI_EPOCH_MAXP;
 constexpr int kEpochSlot = 64;  // unsigned words per launch (its ticket at 0; a 256-B line of its own)
 void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
                        long long timeout);

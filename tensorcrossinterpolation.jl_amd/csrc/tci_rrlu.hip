@@ -2013,9 +2013,12 @@ constexpr int kXU = TCI_XU;   // columns per chunk (two chunks in flight per lan
 static_assert(kXU == 4 || kXU == 8, "chunks of 4 or 8 columns (cb is a multiple of 8)");
 constexpr int kXSlices = kXHalf / 128;
 constexpr int kXReps = kP2Threads / 64 / kXSlices;
-struct PxLds {
-    double xs[kMaxPendR * kXHalf];   // x_s of the half-tile's rows
-    double ys[kMaxPendR * kXStage];  // y_s of the staged columns
+// (16-B aligned: the update loop reads a lane's two x's and two y's with one ds_read_b128 each -- as
+// ds_read2_b64 pairs at a 16-B lane stride the x reads were 4-way bank conflicts, and the loop was
+// LDS-bound: round 4's 31.5 M conflict cycles per deep write-back)
+struct alignas(16) PxLds {
+    alignas(16) double xs[kMaxPendR * kXHalf];   // x_s of the half-tile's rows
+    alignas(16) double ys[kMaxPendR * kXStage];  // y_s of the staged columns
     double xa[kMaxPendR];            // X[s][a] (pivot row a)
     double yb[kMaxPendR];            // Y[s][b] (pivot column b)
     int cpos[kXStage];
@@ -2169,17 +2172,19 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 if (!any) return;
                 for (int s = 0; s < P; ++s) {
 #if TCI_PX_EXP & 1  // timing experiment only (wrong values): no LDS read of the x's
-                    const double2 x = double2{1.0 + s, 0.5 * s};
+                    const dv2 x = dv2{1.0 + s, 0.5 * s};
 #else
-                    const double2 x = *reinterpret_cast<const double2*>(&L.xs[s * kXHalf + lr]);
+                    const dv2 x = *reinterpret_cast<const dv2*>(
+                        __builtin_assume_aligned(&L.xs[s * kXHalf + lr], 16));
 #endif
                     double y[kXU];
 #pragma unroll
                     for (int u = 0; u < kXU; u += 2) {
 #if TCI_PX_EXP & 2  // timing experiment only: no LDS read of the y's
-                        const double2 yy = double2{0.25 * s + u, 0.125 * s};
+                        const dv2 yy = dv2{0.25 * s + u, 0.125 * s};
 #else
-                        const double2 yy = *reinterpret_cast<const double2*>(&L.ys[s * kXStage + h * kXU + u]);
+                        const dv2 yy = *reinterpret_cast<const dv2*>(
+                            __builtin_assume_aligned(&L.ys[s * kXStage + h * kXU + u], 16));
 #endif
                         y[u] = yy.x;
                         y[u + 1] = yy.y;
