@@ -405,6 +405,85 @@ __global__ __launch_bounds__(256) void k_assemble(FuncDev f, const St* __restric
     block_maxabs(mx, maxbits);
 }
 
+// The Lorentzian (README.md:21-29) at HBM write speed: out[R + ldo j] = tab[s_R + s_j], the
+// quotient table p0 / (s + 1) over every reachable integer sum of squares (bitwise the division,
+// DESIGN.md K1) staged in LDS when it fits (a gather from L1/L2 per element otherwise). A tile is
+// 512 rows (two per lane, one 16-B non-temporal store) x kLzCols columns, the column states read as
+// wave-uniform (scalar) loads, all the tile's table reads issued before its stores.
+constexpr int kLzCols = 16;
+constexpr int kLzTabLds = 8192;  // table entries staged in LDS (64 KiB)
+template <bool LDS>
+__global__ __launch_bounds__(256) void k_assemble_lorentz(const St* __restrict__ rs, const St* __restrict__ cs,
+                                                          int64_t mR, int n, double* __restrict__ out, int64_t ldo,
+                                                          unsigned long long* maxbits, const double* __restrict__ tab,
+                                                          int64_t ntab, double p0, int vec) {
+    __shared__ double ltab[LDS ? kLzTabLds : 1];
+    if constexpr (LDS) {
+        for (int64_t s = threadIdx.x; s < ntab; s += blockDim.x) ltab[s] = tab[s];
+        __syncthreads();
+    }
+    // s < ntab for every reachable sum: the table covers them (tci_func_create sizes it, and this
+    // kernel runs only with a table)
+    (void)p0;
+    auto q = [&](int64_t s) -> double {
+        if constexpr (LDS)
+            return ltab[s];
+        else
+            return tab[s];
+    };
+    double mx = 0.0;
+    auto upd = [&](double v) {
+        const double a = fabs(v);
+        mx = (isnan(a) || a > mx) ? a : mx;
+    };
+    const int64_t rtiles = (mR + 511) / 512;
+    const int64_t ctiles = (n + kLzCols - 1) / kLzCols;
+    const int64_t ntiles = rtiles * ctiles;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t R = (t % rtiles) * 512 + 2 * threadIdx.x;
+        const int j0 = (int)(t / rtiles) * kLzCols;
+        const bool h0 = R < mR, h1 = R + 1 < mR;
+        const int64_t s0 = h0 ? rs[R].i : 0, s1 = h1 ? rs[R + 1].i : 0;
+        if (j0 + kLzCols <= n && h1 && vec) {  // full tile: every load first, then the stores
+            double v0[kLzCols], v1[kLzCols];
+#pragma unroll
+            for (int u = 0; u < kLzCols; ++u) {
+                const int64_t c = cs[j0 + u].i;
+                v0[u] = q(s0 + c);
+                v1[u] = q(s1 + c);
+            }
+#pragma unroll
+            for (int u = 0; u < kLzCols; ++u) {
+                upd(v0[u]);
+                upd(v1[u]);
+                typedef double dv2 __attribute__((ext_vector_type(2)));
+                __builtin_nontemporal_store(dv2{v0[u], v1[u]}, reinterpret_cast<dv2*>(out + R + ldo * (j0 + u)));
+            }
+        } else if (h0) {
+            const int je = min(j0 + kLzCols, n);
+            for (int j = j0; j < je; ++j) {
+                const int64_t c = cs[j].i;
+                double* o = out + R + ldo * j;
+                const double v0 = q(s0 + c);
+                upd(v0);
+                if (h1) {
+                    const double v1 = q(s1 + c);
+                    upd(v1);
+                    if (vec) {
+                        *reinterpret_cast<double2*>(o) = double2{v0, v1};
+                    } else {
+                        o[0] = v0;
+                        o[1] = v1;
+                    }
+                } else {
+                    o[0] = v0;
+                }
+            }
+        }
+    }
+    block_maxabs(mx, maxbits);
+}
+
 // Direct per-element path (TCI_F_GAUSSMIX, TCI_F_TT): the reference's loop order of f itself.
 __device__ double feval_direct(const FuncDev& f, const int32_t* e, int nl, int c, int M,
                                const int32_t* g, int nr) {
@@ -887,6 +966,17 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
         const int64_t ntiles = ((mR + 511) / 512) * ((n + kAsmCols - 1) / kAsmCols);
         const int grid = (int)(ntiles < 4096 ? (ntiles > 0 ? ntiles : 1) : 4096);
         const int vec = (ldo % 2 == 0) && ((uintptr_t)out % 16 == 0);
+        if (f.kind == F_LORENTZ && ntab > 0) {
+            const int64_t lt = ((mR + 511) / 512) * ((n + kLzCols - 1) / kLzCols);
+            const int lg = (int)(lt < 2048 ? (lt > 0 ? lt : 1) : 2048);
+            if (ntab <= kLzTabLds)
+                hipLaunchKernelGGL(k_assemble_lorentz<true>, dim3(lg), dim3(256), 0, s, rs, cs, mR, n, out, ldo,
+                                   maxbits, tab, ntab, 0.0, vec);
+            else
+                hipLaunchKernelGGL(k_assemble_lorentz<false>, dim3(lg), dim3(256), 0, s, rs, cs, mR, n, out, ldo,
+                                   maxbits, tab, ntab, 0.0, vec);
+            return;
+        }
         switch (f.kind) {
 #define TCI_ASM(K)                                                                                  \
     case K:                                                                                         \

@@ -191,3 +191,39 @@ def test_sharded_device_gather_one_rccl_rank(tmp_path):
     mp.spawn(_gather_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
     res = json.load(open(tmp_path / "rank0.json"))
     assert all(res.values()), res
+
+
+def _metric_worker(rank, world, port, outdir):
+    """The metric matrix (8192^2 U[0,1), seed 0: bench.py's) column-sharded over `world` ranks with
+    the host exchange and the two-level epoch forced (epochs = 3: refreshes, EXT passes, the deep
+    write-back, the ghost column carrying every exact-pending y); rank 0 checks against the oracle."""
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ctx = T.Context(0)
+        ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, 3))
+        host = Comm(device="cpu")
+        m = n = 8192
+        A = O.fill_uniform(m * n, seed=0).reshape((m, n), order="F")
+        kw = dict(maxrank=256)
+        out = _run_rank(ctx, A, rank, world, kw, exchange=HostExchange(ctx, host))
+        L, U = rrlu_sharded_factors(ctx, m, n, out[0], host_comm=host)
+        res = _check(A, kw, out, L, U) if rank == 0 else {"skipped": True}
+        ctx.close()
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_sharded_two_ranks_metric_epochs3(tmp_path):
+    """two ranks (host exchange, sharing cuda:0) at the metric size 8192^2, r = 256, with
+    epochs = 3 -- bitwise the unsharded oracle (permutations, npivot, lu.error, pivot errors, L, U)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_metric_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    res = json.load(open(tmp_path / "rank0.json"))
+    assert all(res.values()), res
