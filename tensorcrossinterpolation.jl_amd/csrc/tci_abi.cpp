@@ -75,6 +75,7 @@ struct tci_ctx {
     char* zbuf = nullptr;  // mapped pinned host memory the small path's kernels write into
     char* zdev = nullptr;  // its device address
     int small_sweep = 1;   // device-resident small sweeps (tci_sweep_small.hip; env TCI_SWEEP_SMALL=0)
+    int sw_lu_wave = 1;    // their bonds with m, n <= 32 on the one-wave rrLU (env TCI_SW_LUWAVE=0: off)
     int32_t* sw_ws = nullptr;   // their six banks of index sets
     size_t capSwWs = 0;
     char* sw_inbuf = nullptr;   // device copy of the input image
@@ -1021,6 +1022,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
+    if (const char* e = getenv("TCI_SW_LUWAVE")) c->sw_lu_wave = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = atoi(e) != 0;
     if (const char* e = getenv("TCI_EPOCH_KINDS")) c->persist_kinds = atoi(e);
@@ -2698,6 +2700,7 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
     a.s1fwd = s1 ? s1->forward : 0;
     a.s1tens = s1 ? s1->tensors : 0;
     a.reltol = s1 ? s1->reltol : 1e-14;
+    a.lu_wave = c->sw_lu_wave;
     a.tens = nullptr;
     a.tcap = 0;
     if (s1 && s1->tensors) {  // the site tensors in HBM: [site] (offset, count), then the data

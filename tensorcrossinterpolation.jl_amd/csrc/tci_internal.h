@@ -398,6 +398,7 @@ struct SweepSmallArgs {
     double reltol;         // mode 2: the rrLU's reltol
     double* tens;          // mode 2: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
     int64_t tcap;          // mode 2: doubles available after the 2 L table entries
+    int lu_wave = 1;       // bonds with m, n <= 32: the one-wave rrLU (sw_lu_wave; env TCI_SW_LUWAVE=0: off)
 };
 // sweep1site! on the device (mode 2): the host's request and where the site tensors go
 struct SwSweep1 {

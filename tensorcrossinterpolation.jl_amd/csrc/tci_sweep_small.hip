@@ -498,6 +498,168 @@ __device__ int sw_lu_regs(double* S, int ldS, int m, int n, int mr, double relto
     return np;
 }
 
+// ---- one-wave rrLU for m, n <= 32 (every bond of C3 / C4): sw_lu_regs's algorithm on ONE wave,
+// lane (tr, tc) of an 8 x 8 grid owning rows tr + 8 a and columns tc + 8 b (a, b < 4) in registers.
+// The winner is found by DPP + readlane and is then uniform in every lane, so a pivot needs no
+// workgroup barrier: the pivot column / row go through LDS under wave-level fences only
+// (wave_sync). The same candidates in the same (abs2, column position, row position) order, the same
+// true division and separate multiply / subtract on the same values as sw_lu_regs, hence the same
+// pivots and bits. The other waves wait at the closing barrier.
+constexpr int kSwWaveN = 32;
+
+__device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double reltol, double abstol, int leftorth,
+                          int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red, double* pvl,
+                          int* nslot, double* dslot, double& error, double& maxerror, int& nanfl,
+                          bool posout = false) {
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const int lane = tid, tr = lane & 7, tc = lane >> 3;
+        double v[4][4];
+        int rpos[4], cpos[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) rpos[a] = tr + 8 * a < m ? tr + 8 * a : -1;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) cpos[b] = tc + 8 * b < n ? tc + 8 * b : -1;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                v[a][b] = (rpos[a] >= 0 && cpos[b] >= 0) ? S[tr + 8 * a + (tc + 8 * b) * ldS] : 0.0;
+        if (lane < m) rowphys[lane] = lane;
+        if (lane < n) colphys[lane] = lane;
+        if (lane == 0) *nslot = 0;
+        double bv, bx;
+        unsigned bk;
+        auto take = [&](double a2, unsigned key, double val) {
+            const bool better = (a2 > bv) || (a2 == bv && key < bk);  // NaN never wins
+            bv = better ? a2 : bv;
+            bk = better ? key : bk;
+            bx = better ? val : bx;
+        };
+        bv = -1.0;
+        bk = 0xffffffffu;
+        bx = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (rpos[a] >= 0 && cpos[b] >= 0)
+                    take(__dmul_rn(v[a][b], v[a][b]), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], v[a][b]);
+        double mxe = 0.0, err = __longlong_as_double(0x7ff8000000000000LL);
+        int np = 0, fl = 0;
+        wave_sync();
+        for (int k = 0; k < mr; ++k) {
+            wave_best(bv, bk, bx);  // uniform from here on
+            int pp = (int)(bk & 0xffffu), qq = (int)(bk >> 16);
+            double val = bx;
+            if (!(bv >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
+                pp = qq = k;
+                const int r0 = rowphys[k], c0 = colphys[k];
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if (tr + 8 * a == r0 && tc + 8 * b == c0) *dslot = v[a][b];
+                wave_sync();
+                val = *dslot;
+            }
+            err = fabs(val);
+            if (((fabs(err) < reltol * mxe) || (fabs(err) < abstol)) && k > 0) break;
+            mxe = jl_max(mxe, err);
+            np = k + 1;
+            if (lane == 0) pvl[k] = val;
+            if (isnan(val)) fl |= 3;  // the pivot sits on both tril and triu
+            const int pr = rowphys[pp], pc = colphys[qq];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
+            const double piv = val;
+            auto norm_col = [&](auto bc) {
+                constexpr int b = decltype(bc)::value;
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    if (rpos[a] > k) {
+                        const double x = leftorth ? v[a][b] / piv : v[a][b];
+                        v[a][b] = x;
+                        xv[tr + 8 * a] = x;
+                        fl |= isnan(x) ? 1 : 0;
+                    }
+            };
+            auto norm_row = [&](auto ac) {
+                constexpr int a = decltype(ac)::value;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (cpos[b] > k) {
+                        const double y = leftorth ? v[a][b] : v[a][b] / piv;
+                        v[a][b] = y;
+                        yv[tc + 8 * b] = y;
+                        fl |= isnan(y) ? 2 : 0;
+                    }
+            };
+            if (tc == (pc & 7)) {
+                switch (pc >> 3) {
+                case 0: norm_col(std::integral_constant<int, 0>{}); break;
+                case 1: norm_col(std::integral_constant<int, 1>{}); break;
+                case 2: norm_col(std::integral_constant<int, 2>{}); break;
+                default: norm_col(std::integral_constant<int, 3>{}); break;
+                }
+            }
+            if (tr == (pr & 7)) {
+                switch (pr >> 3) {
+                case 0: norm_row(std::integral_constant<int, 0>{}); break;
+                case 1: norm_row(std::integral_constant<int, 1>{}); break;
+                case 2: norm_row(std::integral_constant<int, 2>{}); break;
+                default: norm_row(std::integral_constant<int, 3>{}); break;
+                }
+            }
+            wave_sync();
+            if (lane == 0) {
+                int t = rowphys[k];
+                rowphys[k] = rowphys[pp];
+                rowphys[pp] = t;
+                t = colphys[k];
+                colphys[k] = colphys[qq];
+                colphys[qq] = t;
+            }
+            double xr[4], yc[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) xr[a] = rpos[a] > k ? xv[tr + 8 * a] : 0.0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) yc[b] = cpos[b] > k ? yv[tc + 8 * b] : 0.0;
+            bv = -1.0;
+            bk = 0xffffffffu;
+            bx = 0.0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (rpos[a] > k && cpos[b] > k) {
+                        const double nv = __dsub_rn(v[a][b], __dmul_rn(xr[a], yc[b]));
+                        v[a][b] = nv;
+                        take(__dmul_rn(nv, nv), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], nv);
+                    }
+            wave_sync();  // this pivot's xv / yv reads before the next pivot's writes
+        }
+        if (fl) atomicOr(nslot, fl);
+        if (posout) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (rpos[a] >= 0 && cpos[b] >= 0) S[rpos[a] + cpos[b] * ldS] = v[a][b];
+        }
+        if (lane == 0) red[0] = SmallCand{err, (unsigned)np, 0u, mxe};
+    }
+    __syncthreads();  // the permutations, pivots, flags, position-order S and the results
+    nanfl = *nslot;
+    error = red[0].v;
+    maxerror = red[0].val;
+    const int np = (int)red[0].key;
+    __syncthreads();  // red[] is reused by the caller
+    return np;
+}
+
 // ---- the kernel
 // Index-set slots: every site has three slots per kind (I / J), physical banks 2 s (I) and 2 s + 1
 // (J) of slot s; per site the roles current / history / extra point at slots. An iteration's
@@ -760,7 +922,10 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int* rp = perm;
                 int* cp = perm + m;
                 int np, fl;
-                if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
+                if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {  // one-wave rrLU
+                    np = sw_lu_wave(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                                    &nanflag, &dslot, error, maxerror, fl);
+                } else if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
                     np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                     &nanflag, &dslot, error, maxerror, fl, SWP_ACC);
                 } else {
@@ -929,7 +1094,10 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
             int* rp = perm;
             int* cp = perm + m;
             int np, fl;
-            if (m <= kSwRegN && n <= kSwRegN) {
+            if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {
+                np = sw_lu_wave(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                                &nanflag, &dslot, error, maxerror, fl, a.s1tens != 0);
+            } else if (m <= kSwRegN && n <= kSwRegN) {
                 np = sw_lu_regs(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                 &nanflag, &dslot, error, maxerror, fl, SWP_ACC, a.s1tens != 0);
             } else {
