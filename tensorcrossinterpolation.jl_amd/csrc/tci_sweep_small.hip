@@ -498,32 +498,35 @@ __device__ int sw_lu_regs(double* S, int ldS, int m, int n, int mr, double relto
     return np;
 }
 
-// ---- one-wave rrLU for m, n <= 32 (every bond of C3 / C4): sw_lu_regs's algorithm on ONE wave,
-// lane (tr, tc) of an 8 x 8 grid owning rows tr + 8 a and columns tc + 8 b (a, b < 4) in registers.
+// ---- one-wave rrLU for m, n <= 64 (the bonds of C3 / C4): sw_lu_regs's algorithm on ONE wave,
+// lane (tr, tc) of an 8 x 8 grid owning rows tr + 8 a and columns tc + 8 b (a, b < TILE: 4 for
+// m, n <= 32, 8 for <= 64; the kernel runs one 256-thread workgroup, so a lane may hold 64 doubles).
 // The winner is found by DPP + readlane and is then uniform in every lane, so a pivot needs no
 // workgroup barrier: the pivot column / row go through LDS under wave-level fences only
 // (wave_sync). The same candidates in the same (abs2, column position, row position) order, the same
 // true division and separate multiply / subtract on the same values as sw_lu_regs, hence the same
 // pivots and bits. The other waves wait at the closing barrier.
-constexpr int kSwWaveN = 32;
+constexpr int kSwWaveN = 64;
 
+template <int TILE>
 __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double reltol, double abstol, int leftorth,
                           int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red, double* pvl,
                           int* nslot, double* dslot, double& error, double& maxerror, int& nanfl,
                           bool posout = false) {
+    static_assert(8 * TILE <= kSwWaveN, "tile");
     const int tid = threadIdx.x;
     if (tid < 64) {
         const int lane = tid, tr = lane & 7, tc = lane >> 3;
-        double v[4][4];
-        int rpos[4], cpos[4];
+        double v[TILE][TILE];
+        int rpos[TILE], cpos[TILE];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) rpos[a] = tr + 8 * a < m ? tr + 8 * a : -1;
+        for (int a = 0; a < TILE; ++a) rpos[a] = tr + 8 * a < m ? tr + 8 * a : -1;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) cpos[b] = tc + 8 * b < n ? tc + 8 * b : -1;
+        for (int b = 0; b < TILE; ++b) cpos[b] = tc + 8 * b < n ? tc + 8 * b : -1;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < TILE; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < TILE; ++b)
                 v[a][b] = (rpos[a] >= 0 && cpos[b] >= 0) ? S[tr + 8 * a + (tc + 8 * b) * ldS] : 0.0;
         if (lane < m) rowphys[lane] = lane;
         if (lane < n) colphys[lane] = lane;
@@ -540,9 +543,9 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
         bk = 0xffffffffu;
         bx = 0.0;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < TILE; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < TILE; ++b)
                 if (rpos[a] >= 0 && cpos[b] >= 0)
                     take(__dmul_rn(v[a][b], v[a][b]), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], v[a][b]);
         double mxe = 0.0, err = __longlong_as_double(0x7ff8000000000000LL);
@@ -556,9 +559,9 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
                 pp = qq = k;
                 const int r0 = rowphys[k], c0 = colphys[k];
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < TILE; ++a)
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < TILE; ++b)
                         if (tr + 8 * a == r0 && tc + 8 * b == c0) *dslot = v[a][b];
                 wave_sync();
                 val = *dslot;
@@ -571,47 +574,40 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
             if (isnan(val)) fl |= 3;  // the pivot sits on both tril and triu
             const int pr = rowphys[pp], pc = colphys[qq];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
+            for (int a = 0; a < TILE; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
+            for (int b = 0; b < TILE; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
+            // normalisation (true division) of the pivot column / row by their owners: lane column
+            // pc mod 8 holds physical column pc in slot pc / 8 (uniform), lane row pr mod 8 row pr
             const double piv = val;
-            auto norm_col = [&](auto bc) {
-                constexpr int b = decltype(bc)::value;
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-                    if (rpos[a] > k) {
-                        const double x = leftorth ? v[a][b] / piv : v[a][b];
-                        v[a][b] = x;
-                        xv[tr + 8 * a] = x;
-                        fl |= isnan(x) ? 1 : 0;
-                    }
-            };
-            auto norm_row = [&](auto ac) {
-                constexpr int a = decltype(ac)::value;
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (cpos[b] > k) {
-                        const double y = leftorth ? v[a][b] : v[a][b] / piv;
-                        v[a][b] = y;
-                        yv[tc + 8 * b] = y;
-                        fl |= isnan(y) ? 2 : 0;
-                    }
-            };
+            const int bsel = pc >> 3, asel = pr >> 3;
             if (tc == (pc & 7)) {
-                switch (pc >> 3) {
-                case 0: norm_col(std::integral_constant<int, 0>{}); break;
-                case 1: norm_col(std::integral_constant<int, 1>{}); break;
-                case 2: norm_col(std::integral_constant<int, 2>{}); break;
-                default: norm_col(std::integral_constant<int, 3>{}); break;
-                }
+#pragma unroll
+                for (int b = 0; b < TILE; ++b)
+                    if (b == bsel) {
+#pragma unroll
+                        for (int a = 0; a < TILE; ++a)
+                            if (rpos[a] > k) {
+                                const double x = leftorth ? v[a][b] / piv : v[a][b];
+                                v[a][b] = x;
+                                xv[tr + 8 * a] = x;
+                                fl |= isnan(x) ? 1 : 0;
+                            }
+                    }
             }
             if (tr == (pr & 7)) {
-                switch (pr >> 3) {
-                case 0: norm_row(std::integral_constant<int, 0>{}); break;
-                case 1: norm_row(std::integral_constant<int, 1>{}); break;
-                case 2: norm_row(std::integral_constant<int, 2>{}); break;
-                default: norm_row(std::integral_constant<int, 3>{}); break;
-                }
+#pragma unroll
+                for (int a = 0; a < TILE; ++a)
+                    if (a == asel) {
+#pragma unroll
+                        for (int b = 0; b < TILE; ++b)
+                            if (cpos[b] > k) {
+                                const double y = leftorth ? v[a][b] : v[a][b] / piv;
+                                v[a][b] = y;
+                                yv[tc + 8 * b] = y;
+                                fl |= isnan(y) ? 2 : 0;
+                            }
+                    }
             }
             wave_sync();
             if (lane == 0) {
@@ -622,18 +618,18 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
                 colphys[k] = colphys[qq];
                 colphys[qq] = t;
             }
-            double xr[4], yc[4];
+            double xr[TILE], yc[TILE];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) xr[a] = rpos[a] > k ? xv[tr + 8 * a] : 0.0;
+            for (int a = 0; a < TILE; ++a) xr[a] = rpos[a] > k ? xv[tr + 8 * a] : 0.0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) yc[b] = cpos[b] > k ? yv[tc + 8 * b] : 0.0;
+            for (int b = 0; b < TILE; ++b) yc[b] = cpos[b] > k ? yv[tc + 8 * b] : 0.0;
             bv = -1.0;
             bk = 0xffffffffu;
             bx = 0.0;
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < TILE; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < TILE; ++b)
                     if (rpos[a] > k && cpos[b] > k) {
                         const double nv = __dsub_rn(v[a][b], __dmul_rn(xr[a], yc[b]));
                         v[a][b] = nv;
@@ -644,9 +640,9 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
         if (fl) atomicOr(nslot, fl);
         if (posout) {
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < TILE; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < TILE; ++b)
                     if (rpos[a] >= 0 && cpos[b] >= 0) S[rpos[a] + cpos[b] * ldS] = v[a][b];
         }
         if (lane == 0) red[0] = SmallCand{err, (unsigned)np, 0u, mxe};
@@ -658,6 +654,18 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
     const int np = (int)red[0].key;
     __syncthreads();  // red[] is reused by the caller
     return np;
+}
+
+// dispatch by size: 4 x 4 tiles per lane up to 32, 8 x 8 up to 64
+__device__ __forceinline__ int sw_lu_wave_any(double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
+                                              int leftorth, int* rowphys, int* colphys, double* xv, double* yv,
+                                              SmallCand* red, double* pvl, int* nslot, double* dslot, double& error,
+                                              double& maxerror, int& nanfl, bool posout = false) {
+    if (m <= 32 && n <= 32)
+        return sw_lu_wave<4>(S, ldS, m, n, mr, reltol, abstol, leftorth, rowphys, colphys, xv, yv, red, pvl, nslot,
+                             dslot, error, maxerror, nanfl, posout);
+    return sw_lu_wave<8>(S, ldS, m, n, mr, reltol, abstol, leftorth, rowphys, colphys, xv, yv, red, pvl, nslot,
+                         dslot, error, maxerror, nanfl, posout);
 }
 
 // ---- the kernel
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int* cp = perm + m;
                 int np, fl;
                 if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {  // one-wave rrLU
-                    np = sw_lu_wave(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                    np = sw_lu_wave_any(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                     &nanflag, &dslot, error, maxerror, fl);
                 } else if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
                     np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
@@ -1095,7 +1103,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
             int* cp = perm + m;
             int np, fl;
             if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {
-                np = sw_lu_wave(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                np = sw_lu_wave_any(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                 &nanflag, &dslot, error, maxerror, fl, a.s1tens != 0);
             } else if (m <= kSwRegN && n <= kSwRegN) {
                 np = sw_lu_regs(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
