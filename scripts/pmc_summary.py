@@ -18,6 +18,8 @@ from collections import defaultdict
 
 def family(name):
     short = name.split("(")[0].replace("void ", "").strip()
+    if short.startswith("tci::k_pass_mf_epoch<"):  # persistent shadow-epoch launch (several passes each)
+        return "rrlu_read_only_persistent"
     if short.startswith("tci::k_pass_mf<"):  # <P, EXT, RF>: RF = the shadow refresh pass
         targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
         return "rrlu_refresh_pass" if len(targs) > 2 and targs[2] == "true" else "rrlu_read_only_pass"
@@ -27,7 +29,13 @@ def family(name):
         return {"1": "rrlu_write_back_pass", "2": "rrlu_refresh_pass"}.get(short[-2], "rrlu_read_only_pass")
     if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
         targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
-        return "rrlu_write_back_pass" if targs[1] == "true" else "rrlu_read_only_pass"
+        if targs[1] == "true":
+            return "rrlu_write_back_pass"
+        if targs[0] == "0":  # the initial argmax of A (k = -1)
+            return "rrlu_initial_pass"
+        if targs[0] == "1" and len(targs) > 2 and targs[2] == "true":  # pass 0: reads A, writes the shadow
+            return "rrlu_pass0"
+        return "rrlu_read_only_pass"
     return short
 
 
