@@ -265,6 +265,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dom, "avg_launch_ms": round(avg_launch_ms, 5), "launches": dom_launches,
+                     "launches_note": "read-only passes sampled by HIP events (every stride-th pass; pass 0 is "
+                                      "its own family, passes.pass0); avg_launch_ms includes the event pair",
                      "algorithmic_bytes_per_launch": bytes_per_launch, "passes": other,
                      "deferred_depth_nb": nb, "epochs": args.epochs, "shadow_search": shadow, "shadow_bytes": sh_bytes,
                      "step_algorithmic_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
@@ -275,6 +277,9 @@ def main():
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
     out["roofline"].update(pmc_traffic(dom_key, m, n, r, nb, args.epochs, shadow, sh_bytes))
+    # the same fraction from the committed rocprofv3 kernel trace of this configuration: every
+    # read-only pass's device time (no event overhead, pass 0 apart) over the schedule's pass count
+    out["roofline"].update(trace_frac(m, n, r, nb, args.epochs, shadow, sh_bytes))
     # roofline calibration on the same buffers: 16-B stream read and stream copy, best grid
     import ctypes as C
     nel = A.ld * n
@@ -333,7 +338,8 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_c13_pmc_summary.json")
+TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r05_c13_trace_roofline.json")  # scripts/trace_roofline.py
 PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 3, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 
@@ -349,6 +355,20 @@ def pmc_traffic(fam, m, n, r, nb, epochs, shadow, sh_bytes):
     return {"traffic": rec["hbm_bytes_per_launch"],
             "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE, "
                               f"{rec['dispatches_profiled']} dispatches)"}
+
+
+def trace_frac(m, n, r, nb, epochs, shadow, sh_bytes):
+    """roofline fraction of the read-only pass from the committed kernel trace summary (rocprof)."""
+    if ({"m": m, "n": n, "r": r, "nb": nb, "epochs": epochs, "shadow": shadow, "sh_bytes": sh_bytes} != PMC_CONFIG
+            or not os.path.exists(TRACE_ROOFLINE)):
+        return {}
+    with open(TRACE_ROOFLINE) as fh:
+        rec = json.load(fh).get("read_only_pass")
+    if not rec:
+        return {}
+    return {"frac_rocprof": rec["frac_of_8TBps"], "avg_us_per_pass_rocprof": rec["avg_us_per_pass"],
+            "rocprof_source": os.path.relpath(TRACE_ROOFLINE, ROOT) + " (kernel trace of bench.py --steps 3 "
+                              "--warmup 1 --no-extras --no-cpu: read-only passes' device time / passes)"}
 
 
 def sharded_extras(T, ctx, dist, world, rank, full_res):
