@@ -84,6 +84,9 @@ def len_sched(m, n, r, nb, epochs, shadow, sh_bytes):
     return a, b, c
 
 
+_OUT_FD = 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +111,11 @@ def main():
     ap.add_argument("--no-shadow", action="store_true",
                     help="exact fp64 read-only passes instead of the certified fp16 shadow search")
     args = ap.parse_args()
+    # the result is ONE JSON line on stdout: native libraries' banners (RCCL prints its version
+    # block to fd 1 when the sharded extras create a communicator) go to stderr instead
+    global _OUT_FD
+    _OUT_FD = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -330,7 +338,8 @@ def main():
         out["parity"] = parity_vs_cpu(dev_res, cpu_res, r)
         parity_ok = out["parity"]["ok"]
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(_OUT_FD, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
     if not parity_ok:

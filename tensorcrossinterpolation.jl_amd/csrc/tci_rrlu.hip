@@ -2035,7 +2035,10 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
     const int64_t lda = g.lda, ldx = g.ldx, ldy = g.ldy;
     const int m = g.m, n = g.n, k = g.k, cb = g.cb, rev = g.rev, leftorth = g.leftorth;
     const int P = g.pe;  // 1 .. kMaxPendR
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the wave index is uniform: kept in SGPRs, so the chunk (from the slice's counter, read back
+    // with readfirstlane) and with it every column index and column pointer of the streaming loop
+    // is scalar work -- per column the loop's VALU does the arithmetic and a 32-bit row offset only
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int slice = wave % kXSlices, rep = wave / kXSlices;
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile;
     const int tiles_c = (n + cb - 1) / cb;
@@ -2101,7 +2104,7 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
         const int rp0 = rowok ? rowpos[r0] : -1, rp1 = pair ? rowpos[r0 + 1] : -1;
         const bool in0 = rp0 > k, in1 = rp1 > k;
         const bool wact = MODE != 0 || __any(in0 || in1);
-        double* const base = A + (rowok ? r0 : 0);
+        const uint32_t roff = rowok ? r0 : 0;  // the lane's row offset within a column
         for (int g0 = 0; g0 < ntc; g0 += G) {
             const int gcols = min(G, ntc - g0) * cb;
             const int nch = gcols / kXU;
@@ -2147,11 +2150,14 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
             __syncthreads();
             if (g0 == 0 && half == 0) PPROF(2);
             if (!wact) continue;
+            // a chunk is kXU consecutive columns of one column tile (kXU divides cb): one scalar
+            // column index per chunk, the column pointers scalar (SGPR base + the lane's row offset)
             auto load_chunk = [&](int h, double2 (&v)[kXU]) {
+                const int j0 = col_of(g0, h * kXU);
 #pragma unroll
                 for (int u = 0; u < kXU; ++u) {
-                    const int j = min(col_of(g0, h * kXU + u), n - 1);
-                    const double2* pa = reinterpret_cast<const double2*>(base + (int64_t)j * lda);
+                    const double* colp = A + (int64_t)min(j0 + u, n - 1) * lda;
+                    const double2* pa = reinterpret_cast<const double2*>(colp + roff);
                     if constexpr (MODE == 1 && TCI_FLUSH_NTL) {
                         typedef double dv2 __attribute__((ext_vector_type(2)));
                         const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(pa));
@@ -2166,10 +2172,12 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                 bool any = false;
 #pragma unroll
                 for (int u = 0; u < kXU; ++u) {
-                    cp[u] = L.cpos[h * kXU + u];
+                    cp[u] = __builtin_amdgcn_readfirstlane(L.cpos[h * kXU + u]);
                     any |= cp[u] > k;
                 }
                 if (!any) return;
+                const int j0 = col_of(g0, h * kXU);
+#pragma unroll 2
                 for (int s = 0; s < P; ++s) {
 #if TCI_PX_EXP & 1  // timing experiment only (wrong values): no LDS read of the x's
                     const dv2 x = dv2{1.0 + s, 0.5 * s};
@@ -2195,13 +2203,18 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                         v[u].y = __dsub_rn(v[u].y, __dmul_rn(x.y, y[u]));
                     }
                 }
+                // the chunk's largest |value| of the lane's trailing elements (0 for the others;
+                // NaN never wins a candidate test, and fmax drops it): if its square does not reach
+                // the lane's best, no element of the chunk does (x -> x*x is monotone under
+                // rounding), and the per-element tests are skipped
+                double mx0 = 0.0, mx1 = 0.0;  // (maxnum of subtraction results: one v_max_f64 each)
 #pragma unroll
                 for (int u = 0; u < kXU; ++u) {
                     if (cp[u] <= k) continue;
-                    const int j = col_of(g0, h * kXU + u);
+                    const int j = j0 + u;
                     if constexpr (MODE == 1) {  // trailing rows only (see k_pass2's write-back)
                         if (in0 || in1) {
-                            double2* pa = reinterpret_cast<double2*>(base + (int64_t)j * lda);
+                            double2* pa = reinterpret_cast<double2*>(A + (int64_t)j * lda + roff);
                             if (!in1) {
                                 pa->x = v[u].x;
                             } else if (!in0) {
@@ -2215,7 +2228,7 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                     }
                     if constexpr (MODE != 0 && kShHalf) {
                         if (rowok) {
-                            _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
+                            _Float16* ps = reinterpret_cast<_Float16*>(g.S) + (int64_t)j * g.lds + roff;
                             const _Float16 h0 = in0 ? (_Float16)(float)(v[u].x * shs) : (_Float16)0.0f;
                             if (pair) {
                                 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -2225,17 +2238,27 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                             }
                         }
                     }
-                    const double a0 = __dmul_rn(v[u].x, v[u].x), a1 = __dmul_rn(v[u].y, v[u].y);
-                    if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
-                        if (in0) cand_take(best, CandR{a0, v[u].x, cp[u], rp0, j, r0});
-                        if (in1) cand_take(best, CandR{a1, v[u].y, cp[u], rp1, j, r0 + 1});
+                    mx0 = fmax(mx0, fabs(v[u].x));
+                    mx1 = fmax(mx1, fabs(v[u].y));
+                }
+                const double mx = fmax(in0 ? mx0 : 0.0, in1 ? mx1 : 0.0);
+                if (__dmul_rn(mx, mx) >= best.v) {
+#pragma unroll
+                    for (int u = 0; u < kXU; ++u) {
+                        if (cp[u] <= k) continue;
+                        const int j = j0 + u;
+                        const double a0 = __dmul_rn(v[u].x, v[u].x), a1 = __dmul_rn(v[u].y, v[u].y);
+                        if ((in0 && a0 >= best.v) || (in1 && a1 >= best.v)) {
+                            if (in0) cand_take(best, CandR{a0, v[u].x, cp[u], rp0, j, r0});
+                            if (in1) cand_take(best, CandR{a1, v[u].y, cp[u], rp1, j, r0 + 1});
+                        }
                     }
                 }
             };
             auto grab = [&]() -> int {
                 int h = 0;
                 if (lane == 0) h = atomicAdd(&L.cnt[slice], 1);
-                return __shfl(h, 0);
+                return __builtin_amdgcn_readfirstlane(h);  // every lane active here: lane 0's ticket
             };
             double2 va[kXU], vb[kXU];
             int h0 = rep, h1 = rep + kXReps;
