@@ -433,13 +433,40 @@ def sharded_extras(T, ctx, dist, world, rank, full_res):
             barrier()
             times.append(time.perf_counter() - t0)
         dt = tmax(min(times))
+        used = ctx.lib.tci_last_shard_exchange(ctx.h)
         rec = {"m": m, "n": n, "r": r, "ranks": world, "npivot": out[0], "ms": round(dt * 1e3, 3),
                "GFLOPs": round(rrlu_flops(m, n, out[0]) / dt / 1e9, 1),
-               "exchange": ("candidate first: all-gather of 32-B candidates, then the winning column from "
-                            "its owner by an element-wise uint64 max (DESIGN.md 7)") if world > 1 else
-                           "none (one rank: the pass tail commits, as unsharded)",
+               "exchange": {0: "none (one rank: the pass tail commits, as unsharded)",
+                            1: "two collectives: all-gather of 32-B candidates, then the winning column from "
+                               "its owner by an element-wise uint64 max (DESIGN.md 7)",
+                            2: "fused: ONE all-gather per pivot of every rank's 32-B candidate and its own "
+                               "candidate column (DESIGN.md 7)"}.get(used, used),
                "epochs": ctx.lib.tci_rrlu_epochs_for(ctx.h, m, n),
-               "exchange_bytes_per_pivot": {"allgather_candidates": 32 * world, "allreduce_column": 8 * (m + 32)}}
+               "exchange_bytes_per_pivot": {"fused_allgather_recv": 8 * (m + 36) * world,
+                                            "two_collective": {"allgather_candidates": 32 * world,
+                                                               "allreduce_column": 8 * (m + 32)}}}
+        if world == 1 and m == 8192:
+            # the per-pivot exchange's own cost, measured through a one-rank RCCL communicator (the
+            # collectives run, moving nothing across links): ms per factorisation in both forms
+            xo = {}
+            for xm in (1, 2):
+                ctx.check(ctx.lib.tci_set_shard_exchange(ctx.h, xm))
+                ts = []
+                for _ in range(reps):
+                    W.copy_from(A0)
+                    barrier()
+                    t0 = time.perf_counter()
+                    o2 = rrlu_sharded(W, m, n, j0, nloc, comm=dcomm, maxrank=r)
+                    barrier()
+                    ts.append(time.perf_counter() - t0)
+                xo[{1: "two_collective", 2: "fused"}[xm]] = {
+                    "ms": round(min(ts) * 1e3, 3), "pivots_equal": bool(o2[0] == out[0] and
+                                                                      np.array_equal(o2[2], out[2]) and
+                                                                      np.array_equal(o2[3], out[3]))}
+            ctx.check(ctx.lib.tci_set_shard_exchange(ctx.h, 0))
+            for v in xo.values():
+                v["us_per_pivot_over_unsharded"] = round((v["ms"] - rec["ms"]) * 1e3 / max(out[0], 1), 2)
+            rec["one_rank_rccl_exchange"] = xo
         A0.free()
         W.free()
         if rank == 0:

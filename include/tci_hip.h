@@ -133,6 +133,15 @@ int tci_set_rrlu_mid(tci_ctx* ctx, int enabled);
 int tci_set_rrlu_persist(tci_ctx* ctx, int enabled);
 /* 1 once a persistent launch of this context gave up (see tci_set_rrlu_persist), else 0. */
 int tci_rrlu_persist_faulted(tci_ctx* ctx);
+/* Per-pivot exchange of tci_rrlu_sharded_d (the candidate selection of _optimizerrlu!,
+ * matrixlu.jl:356-369, across column shards): 1 = two collectives (all-gather of the 32-B
+ * candidate records, then an element-wise max of the winning column as a broadcast), 2 = fused (ONE
+ * all-gather of every rank's record together with its own candidate column), 0 = by size (fused
+ * while (N - 1) x 8 (m + 36) B <= 4 MiB; the default; env TCI_SHARD_EXCHANGE). Identical results in
+ * every mode. */
+int tci_set_shard_exchange(tci_ctx* ctx, int mode);
+/* The exchange the last tci_rrlu_sharded_d ran: 0 none (one rank, no communicator), 1, 2 as above. */
+int tci_last_shard_exchange(tci_ctx* ctx);
 /* Certified shadow search in the read-only passes of the pass pipeline: the write-back passes also
  * keep a shadow of the stale values -- fp16 scaled per write-back epoch (2 B/element; fp32 in
  * the TCI_SH_HALF=0 build) -- and a read-only pass streams it instead of the fp64 values, applies

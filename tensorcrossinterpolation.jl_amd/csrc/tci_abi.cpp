@@ -136,6 +136,8 @@ struct tci_ctx {
     size_t capShSend = 0;
     double* shrecv = nullptr;
     size_t capShRecv = 0;
+    int sh_exchange = 0;       // per-pivot exchange: 0 by size, 1 two collectives, 2 fused (one all-gather)
+    int sh_exchange_used = 0;  // what the last sharded rrLU ran (0: none, one rank without a communicator)
     Cand* lout = nullptr;
     size_t capLout = 0;
     int64_t sh_np = 0, sh_nloc = 0, sh_c0 = 0, sh_m = 0, sh_n = 0;
@@ -864,9 +866,18 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
         return set_err(c, TCI_ERR_ARG, "rrlu_sharded: a single rank must hold every column");
     if ((st = ensure(c, &c->lout, &c->capLout, (size_t)nranks + 1))) return st;  // [own, all-gathered ...]
     const int64_t cw = tci::shard_col(m);
+    // the per-pivot exchange: fused = ONE all-gather of [record | own candidate
+    // column] (N x (m + kMaxPendR + 4) words received per rank), two-collective = a 32-B-per-rank
+    // all-gather of the records, then an element-wise max of the winner's column (m + kMaxPendR
+    // words) as a broadcast from a root no rank knows in advance. By size: fused while the extra
+    // bytes it moves stay under kFusedMax (they cost less than the second collective's latency)
+    const int64_t fw = tci::kCandWords + cw;
+    constexpr int64_t kFusedMax = 4 << 20;
+    const bool fused = multi && (c->sh_exchange == 2 || (c->sh_exchange == 0 && (int64_t)(nranks - 1) * fw * 8 <= kFusedMax));
+    c->sh_exchange_used = multi ? (fused ? 2 : 1) : 0;
     if (multi) {
-        if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)cw))) return st;
-        if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)cw))) return st;
+        if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)(fused ? fw : cw)))) return st;
+        if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)(fused ? fw * nranks : cw)))) return st;
     }
     const int mi = (int)m, nl1 = (int)(nloc + 1);  // local columns + the ghost
     tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, (int)n);
@@ -936,15 +947,23 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     uint64_t* colrecv = multi ? reinterpret_cast<uint64_t*>(c->shrecv) : nullptr;
     auto select = [&](int selk) -> int {
         if (!multi) return TCI_OK;  // committed by the pass tail
+        if (fused) {
+            tci::launch_shard_pack(c->stream, c->lout, dA, lda, mi, c->ybuf, ldy, c0, (int)nloc, colsend);
+            if (int e = shard_exchange(c, comm, exch, user, 0, colsend, colrecv, fw)) return e;
+            tci::launch_shard_commit(c->stream, colrecv, fw, nranks, nullptr, 1, mi, selk, c->st, reltol, abstol,
+                                     c->rowpos, c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0,
+                                     (int)nloc, dA, lda, c->ybuf, ldy);
+            return TCI_OK;
+        }
         {
-            int e = shard_exchange(c, comm, exch, user, 0, c->lout, recvC, 4);
+            int e = shard_exchange(c, comm, exch, user, 0, c->lout, recvC, tci::kCandWords);
             if (e) return e;
             tci::launch_shard_pick(c->stream, recvC, nranks, dA, lda, mi, c->ybuf, ldy, c0, (int)nloc, colsend);
             if ((e = shard_exchange(c, comm, exch, user, 1, colsend, colrecv, cw))) return e;
         }
-        tci::launch_shard_commit(c->stream, recvC, nranks, colrecv, mi, selk, c->st, reltol, abstol,
-                                 c->rowpos, c->colpos, c->rowperm, c->colperm, c->pivv, c->colposL, c0, (int)nloc,
-                                 dA, lda, c->ybuf, ldy);
+        tci::launch_shard_commit(c->stream, reinterpret_cast<const uint64_t*>(recvC), tci::kCandWords, nranks,
+                                 colrecv, 0, mi, selk, c->st, reltol, abstol, c->rowpos, c->colpos, c->rowperm,
+                                 c->colperm, c->pivv, c->colposL, c0, (int)nloc, dA, lda, c->ybuf, ldy);
         return TCI_OK;
     };
     // the two-level epoch of rrlu_device, decided by the GLOBAL shape so that every
@@ -1025,6 +1044,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_SW_LUWAVE")) c->sw_lu_wave = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = atoi(e) != 0;
+    if (const char* e = getenv("TCI_SHARD_EXCHANGE")) c->sh_exchange = std::max(0, std::min(atoi(e), 2));
     if (const char* e = getenv("TCI_EPOCH_KINDS")) c->persist_kinds = atoi(e);
     if (const char* e = getenv("TCI_EPOCH_MAXPASS")) c->persist_maxpass = std::max(1, atoi(e));
     if (const char* e = getenv("TCI_C128_NB")) c->c128_nb = std::max(0, std::min(atoi(e), tci::kMaxPend - 1));
@@ -1155,6 +1175,15 @@ int tci_set_rrlu_persist(tci_ctx* c, int enabled) {
 }
 
 int tci_rrlu_persist_faulted(tci_ctx* c) { return c ? c->persist_faulted : -1; }
+
+int tci_set_shard_exchange(tci_ctx* c, int mode) {
+    if (!c) return TCI_ERR_ARG;
+    if (mode < 0 || mode > 2) return set_err(c, TCI_ERR_ARG, "shard exchange must be 0 (by size), 1 or 2");
+    c->sh_exchange = mode;
+    return TCI_OK;
+}
+
+int tci_last_shard_exchange(tci_ctx* c) { return c ? c->sh_exchange_used : -1; }
 
 int tci_set_timing(tci_ctx* c, int enabled) {
     c->timing = enabled > 0;

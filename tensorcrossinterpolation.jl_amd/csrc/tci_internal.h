@@ -264,13 +264,22 @@ void launch_extract(hipStream_t s, const double* Lp, int64_t ldlp, const double*
 // to the replicated row / global column maps and installs the ghost. Per pivot 32 B x N + 8 (m +
 // kMaxPendR) B cross the ranks, not N x 8 m. One rank: no exchange, the commit reads the column in
 // place.
+// The fused form (one collective per pivot): every rank all-gathers its record
+// AND its own candidate column, kCandWords + shard_col(m) words per rank (k_shard_pack), and
+// k_shard_commit takes the winner's column from the winner's slot -- N x 8 (m + kMaxPendR + 4) B
+// received per rank instead of two collective latencies.
 inline int64_t shard_col(int64_t m) { return m + kMaxPendR; }
+constexpr int kCandWords = (int)(sizeof(Cand) / 8);
+static_assert(sizeof(Cand) % 8 == 0, "candidate records are whole uint64 words");
+void launch_shard_pack(hipStream_t s, const Cand* own_rec, const double* A, int64_t lda, int m, const double* Y,
+                       int64_t ldy, int64_t c0, int nloc, uint64_t* send);
 void launch_shard_init(hipStream_t s, int32_t* colpos_loc, int nloc, int64_t c0);
 void launch_shard_pick(hipStream_t s, const Cand* recv, int nranks, const double* A, int64_t lda, int m,
                        const double* Y, int64_t ldy, int64_t c0, int nloc, uint64_t* colsend);
-// colrecv null (one rank): the winner's column and pending y's are read from this rank's A / Y
-void launch_shard_commit(hipStream_t s, const Cand* recv, int nranks, const uint64_t* colrecv, int m, int k,
-                         RrluState* st, double reltol, double abstol, int32_t* rowpos,
+// recv: rank r's record at recv + r * rstride words. colrecv null and fused 0 (one rank): the
+// winner's column and pending y's are read from this rank's A / Y; fused 1: from the winner's slot
+void launch_shard_commit(hipStream_t s, const uint64_t* recv, int64_t rstride, int nranks, const uint64_t* colrecv,
+                         int fused, int m, int k, RrluState* st, double reltol, double abstol, int32_t* rowpos,
                          int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
                          int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
                          int64_t ldy);

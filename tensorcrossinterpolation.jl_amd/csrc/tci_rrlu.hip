@@ -3223,12 +3223,14 @@ __device__ __forceinline__ double bits_dbl(uint64_t u) { return __longlong_as_do
 __device__ __forceinline__ uint64_t dbl_bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
 // every block reduces the N published candidates in rank order (the reference's tie order) to the
-// same winner; -1: no rank has a candidate
-__device__ __forceinline__ int shard_winner(const Cand* __restrict__ recv, int nranks, CandR& w) {
+// same winner; -1: no rank has a candidate. Rank r's record at recv + r * rstride (uint64 words: 4
+// for the two-collective exchange's packed records, the fused record + column stride otherwise)
+__device__ __forceinline__ int shard_winner(const uint64_t* __restrict__ recv, int64_t rstride, int nranks,
+                                            CandR& w) {
     w = cand_none();
     int wr = -1;
     for (int r = 0; r < nranks; ++r) {
-        const Cand h = recv[r];
+        const Cand h = *reinterpret_cast<const Cand*>(recv + r * rstride);
         if (h.v >= 0.0 && cand_better(h.v, h.cpos, h.rpos, w.v, w.cpos, w.rpos)) {
             w = CandR{h.v, h.val, h.cpos, h.rpos, h.pcol, h.prow};
             wr = r;
@@ -3245,7 +3247,7 @@ __global__ __launch_bounds__(256) void k_shard_pick(const Cand* __restrict__ rec
     __shared__ int own_s;
     if (threadIdx.x == 0) {
         CandR w;
-        const int wr = shard_winner(recv, nranks, w);
+        const int wr = shard_winner(reinterpret_cast<const uint64_t*>(recv), kCandWords, nranks, w);
         own_s = (wr >= 0 && w.pc >= c0 && w.pc < c0 + nloc) ? (int)(w.pc - c0) : -1;
     }
     __syncthreads();
@@ -3267,11 +3269,47 @@ void launch_shard_pick(hipStream_t s, const Cand* recv, int nranks, const double
                        nranks, A, lda, m, Y, ldy, c0, nloc, colsend);
 }
 
+// the fused exchange (one all-gather per pivot): every rank publishes [its own record | the pending
+// y's and stale values of its own candidate column] (kCandWords + shard_col(m) words); the record
+// is written by block 0, the column only when the rank has a candidate (never read otherwise)
+__global__ __launch_bounds__(256) void k_shard_pack(const Cand* __restrict__ own_rec,
+                                                    const double* __restrict__ A, int64_t lda, int m,
+                                                    const double* __restrict__ Y, int64_t ldy, int64_t c0, int nloc,
+                                                    uint64_t* __restrict__ send) {
+    const Cand h = *own_rec;
+    if (blockIdx.x == 0 && threadIdx.x < kCandWords)
+        send[threadIdx.x] = reinterpret_cast<const uint64_t*>(own_rec)[threadIdx.x];
+    const int own = (h.v >= 0.0 && h.pcol >= c0 && h.pcol < c0 + nloc) ? (int)(h.pcol - c0) : -1;
+    if (own < 0) return;
+    uint64_t* colsend = send + kCandWords;
+    const double* col = A + (int64_t)own * lda;
+    if (blockIdx.x == 0 && threadIdx.x < kMaxPendR) colsend[threadIdx.x] = dbl_bits(Y[(int64_t)threadIdx.x * ldy + own]);
+    const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        v[u] = i < m ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < m) colsend[kMaxPendR + i] = dbl_bits(v[u]);
+    }
+}
+
+void launch_shard_pack(hipStream_t s, const Cand* own_rec, const double* A, int64_t lda, int m, const double* Y,
+                       int64_t ldy, int64_t c0, int nloc, uint64_t* send) {
+    hipLaunchKernelGGL(k_shard_pack, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, own_rec,
+                       A, lda, m, Y, ldy, c0, nloc, send);
+}
+
 // Every block reduces the N candidates to the same winner and installs its slice of the ghost
 // column; block 0 alone commits (stop test, maps, st). A ghost installed after a stop is never read
 // (the passes return at once). colrecv null: one rank, the winning column is this rank's own.
-__global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ recv, int nranks,
-                                                      const uint64_t* __restrict__ colrecv, int m, int k,
+__global__ __launch_bounds__(256) void k_shard_commit(const uint64_t* __restrict__ recv, int64_t rstride,
+                                                      int nranks, const uint64_t* __restrict__ colrecv,
+                                                      int fused, int m, int k,
                                                       RrluState* st, double reltol, double abstol, int32_t* rowpos,
                                                       int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g,
                                                       double* pivvals, int32_t* colpos_loc, int64_t c0, int nloc,
@@ -3279,7 +3317,7 @@ __global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ r
     __shared__ int win_s, own_s;
     if (threadIdx.x == 0) {
         CandR w;
-        const int wr = shard_winner(recv, nranks, w);
+        const int wr = shard_winner(recv, rstride, nranks, w);
         win_s = wr;
         own_s = (wr >= 0 && w.pc >= c0 && w.pc < c0 + nloc) ? (int)(w.pc - c0) : -1;
         if (blockIdx.x == 0 && !st->done) {
@@ -3298,6 +3336,7 @@ __global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ r
     // the ghost: the winner's stale column and its pending y's (no winner: every trailing value
     // NaN, as the reference's column would be after the division by a NaN pivot)
     const int wr = win_s, own = own_s;
+    if (fused) colrecv = recv + (int64_t)(wr >= 0 ? wr : 0) * rstride + kCandWords;  // the winner's column
     double* gcol = A + (int64_t)nloc * lda;
     const double qnan = __longlong_as_double(0x7ff8000000000000LL);
     const double* lcol = A + (int64_t)(own >= 0 ? own : 0) * lda;
@@ -3321,13 +3360,13 @@ __global__ __launch_bounds__(256) void k_shard_commit(const Cand* __restrict__ r
     }
 }
 
-void launch_shard_commit(hipStream_t s, const Cand* recv, int nranks, const uint64_t* colrecv, int m, int k,
-                         RrluState* st, double reltol, double abstol, int32_t* rowpos,
+void launch_shard_commit(hipStream_t s, const uint64_t* recv, int64_t rstride, int nranks, const uint64_t* colrecv,
+                         int fused, int m, int k, RrluState* st, double reltol, double abstol, int32_t* rowpos,
                          int32_t* colpos_g, int64_t* rowphys, int64_t* colphys_g, double* pivvals,
                          int32_t* colpos_loc, int64_t c0, int nloc, double* A, int64_t lda, double* Y,
                          int64_t ldy) {
     hipLaunchKernelGGL(k_shard_commit, dim3((m + 1023) / 1024 > 0 ? (m + 1023) / 1024 : 1), dim3(256), 0, s, recv,
-                       nranks, colrecv, m, k, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals,
+                       rstride, nranks, colrecv, fused, m, k, st, reltol, abstol, rowpos, colpos_g, rowphys, colphys_g, pivvals,
                        colpos_loc, c0, nloc, A, lda, Y, ldy);
 }
 

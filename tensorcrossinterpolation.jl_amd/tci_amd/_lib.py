@@ -54,6 +54,8 @@ SIGNATURES = {
     "tci_last_kernel_units": ([vp, C.c_int, pdbl, pi64, pi64], C.c_int),
     "tci_set_rrlu_persist": ([vp, C.c_int], C.c_int),
     "tci_rrlu_persist_faulted": ([vp], C.c_int),
+    "tci_set_shard_exchange": ([vp, C.c_int], C.c_int),
+    "tci_last_shard_exchange": ([vp], C.c_int),
     "tci_set_timing": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_flush": ([vp, C.c_int], C.c_int),
     "tci_set_rrlu_epochs": ([vp, C.c_int], C.c_int),

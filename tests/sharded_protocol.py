@@ -14,12 +14,16 @@ addpivot! (matrixlu.jl:295-322, separate multiply and subtract) on its own colum
 column taken from the winner's record. The result must equal the unsharded oracle bit for bit --
 which checks the protocol (tie order across ranks, the stop test, the replicated maps), not the
 device kernels (those are checked against the same oracle in tests/test_gpu_sharded.py).
+
+fused=True is the one-collective form (tci_set_shard_exchange mode 2, k_shard_pack): every rank
+all-gathers its candidate TOGETHER with its own candidate column (bits), and every rank takes the
+winning column from the winner's slot -- the same winner, the same bits, one exchange per pivot.
 """
 import numpy as np
 
 
 def sharded_rrlu(A_loc, m, n, c0, allgather, allreduce_max_u64, maxrank=None, reltol=1e-14, abstol=0.0,
-                 leftorth=True):
+                 leftorth=True, fused=False):
     """A_loc: this rank's m x nloc block (physical = original indices). allgather(vec) returns the
     rank-major concatenation of every rank's equal-length float64 vector; allreduce_max_u64(words)
     the element-wise max over the ranks of uint64 vectors. Returns npivot, error, rowperm, colperm
@@ -48,18 +52,25 @@ def sharded_rrlu(A_loc, m, n, c0, allgather, allreduce_max_u64, maxrank=None, re
             _, _, i, j = min(key)
             best = (float(mx), float(sub[i, j]), int(colpos[c0 + Cc[j]]), int(rowpos[R[i]]), int(c0 + Cc[j]),
                     int(R[i]))
-        allr = allgather(np.array(best, np.float64)).reshape(-1, 6)
-        win = None
+        if fused:  # [candidate | own candidate column as bits], one all-gather
+            own = A[:, best[4] - c0].copy() if best[4] >= 0 else np.zeros(m)
+            allr = allgather(np.concatenate([np.array(best, np.float64), own])).reshape(-1, 6 + m)
+        else:
+            allr = allgather(np.array(best, np.float64)).reshape(-1, 6)
+        win, wr = None, -1
         for r in range(allr.shape[0]):
             c = tuple(allr[r, :6])
             c = (c[0], c[1], int(c[2]), int(c[3]), int(c[4]), int(c[5]))
             if c[4] >= 0 and (win is None or _better(c, win)):
-                win = c
+                win, wr = c, r
         a2, val, cp, rp, pc, pr = win
-        # the owner of the winning column contributes it (as bits), the others zeros
-        mine = c0 <= pc < c0 + nloc
-        contrib = A[:, pc - c0].copy().view(np.uint64) if mine else np.zeros(m, np.uint64)
-        col = np.ascontiguousarray(allreduce_max_u64(contrib), np.uint64).view(np.float64)
+        if fused:
+            col = np.ascontiguousarray(allr[wr, 6:]).view(np.uint64).view(np.float64)
+        else:
+            # the owner of the winning column contributes it (as bits), the others zeros
+            mine = c0 <= pc < c0 + nloc
+            contrib = A[:, pc - c0].copy().view(np.uint64) if mine else np.zeros(m, np.uint64)
+            col = np.ascontiguousarray(allreduce_max_u64(contrib), np.uint64).view(np.float64)
         err = abs(val)
         error = err
         if (err < reltol * maxerror or err < abstol) and k > 0:

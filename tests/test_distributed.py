@@ -170,7 +170,7 @@ def test_sharded_tci2_two_ranks_one_gpu(tmp_path, shard_rrlu):
 
 
 # ------------------------------------------------------------------ column-sharded rrLU protocol
-def _shard_worker(rank, world, port, outdir):
+def _shard_worker(rank, world, port, outdir, fused=False):
     import torch.distributed as dist
 
     sys.path.insert(0, HERE)
@@ -195,7 +195,7 @@ def _shard_worker(rank, world, port, outdir):
             m, n = A.shape
             j0, j1 = column_blocks(n, world)[rank]
             npv, err, rp, cp, L, U = sharded_rrlu(A[:, j0:j1], m, n, j0, comm.allgather_flat,
-                                                  comm.allreduce_max_u64, **kw)
+                                                  comm.allreduce_max_u64, fused=fused, **kw)
             U = comm.allreduce_sum(U)
             ref = O.OracleLU(A, maxrank=kw.get("maxrank", min(m, n)), reltol=kw.get("reltol", 1e-14),
                              leftorthogonal=kw.get("leftorth", True))
@@ -209,13 +209,15 @@ def _shard_worker(rank, world, port, outdir):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_rrlu_protocol_gloo(tmp_path, world):
+@pytest.mark.parametrize("fused", [False, True])
+def test_sharded_rrlu_protocol_gloo(tmp_path, world, fused):
     """The column-sharded rrLU protocol (local argmax, all-gather of the candidates, the winning
-    column from its owner through a uint64 max, the same commit on every rank) reproduces the
-    unsharded oracle bit for bit (tests/sharded_protocol.py)."""
+    column from its owner through a uint64 max -- or, fused, one all-gather of candidates with
+    their columns -- the same commit on every rank) reproduces the unsharded oracle bit for bit
+    (tests/sharded_protocol.py)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path), fused), nprocs=world, join=True)
     for r in range(world):
         res = json.load(open(tmp_path / f"rank{r}.json"))
         assert all(res.values()), (r, res)

@@ -96,7 +96,7 @@ def test_sharded_one_rank_bitwise(ctx, name, shadow, epochs):
     assert all(res.values()), res
 
 
-def _multi_worker(rank, world, port, outdir, mode, epochs=0):
+def _multi_worker(rank, world, port, outdir, mode, epochs=0, exmode=0):
     import torch.distributed as dist
 
     sys.path.insert(0, HERE)
@@ -104,6 +104,7 @@ def _multi_worker(rank, world, port, outdir, mode, epochs=0):
     try:
         ctx = T.Context(0)
         ctx.check(ctx.lib.tci_set_rrlu_epochs(ctx.h, epochs))
+        ctx.check(ctx.lib.tci_set_shard_exchange(ctx.h, exmode))
         host = Comm(device="cpu")
         comm = exchange = None
         if mode == "rccl":
@@ -115,6 +116,8 @@ def _multi_worker(rank, world, port, outdir, mode, epochs=0):
             out = _run_rank(ctx, A, rank, world, kw, comm=comm, exchange=exchange)
             L, U = rrlu_sharded_factors(ctx, A.shape[0], A.shape[1], out[0], host_comm=host)
             res[name] = _check(A, kw, out, L, U)
+            # the exchange that ran: fused (2) by size at these shapes unless forced
+            res[name]["exchange"] = ctx.lib.tci_last_shard_exchange(ctx.h) == (exmode or 2)
         if comm is not None:
             comm.close()
         ctx.close()
@@ -125,13 +128,17 @@ def _multi_worker(rank, world, port, outdir, mode, epochs=0):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,mode,epochs", [(2, "host", 0), (3, "host", 0), (1, "rccl", 0), (2, "host", 3),
-                                               (1, "rccl", 3)])
-def test_sharded_multi_rank_bitwise(tmp_path, world, mode, epochs):
-    """epochs 3: the two-level epoch across ranks (the ghost column carries every exact-pending y)."""
+@pytest.mark.parametrize("world,mode,epochs,exmode", [
+    (2, "host", 0, 1), (2, "host", 0, 2), (3, "host", 0, 1), (3, "host", 0, 0), (1, "rccl", 0, 1),
+    (1, "rccl", 0, 2), (2, "host", 3, 1), (2, "host", 3, 2), (1, "rccl", 3, 0)])
+def test_sharded_multi_rank_bitwise(tmp_path, world, mode, epochs, exmode):
+    """epochs 3: the two-level epoch across ranks (the ghost column carries every exact-pending y).
+    exmode: the per-pivot exchange -- 1 two collectives (record all-gather + column max-broadcast),
+    2 the fused all-gather of record + own candidate column, 0 by size (fused here)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_multi_worker, args=(world, _free_port(), str(tmp_path), mode, epochs), nprocs=world, join=True)
+    mp.spawn(_multi_worker, args=(world, _free_port(), str(tmp_path), mode, epochs, exmode), nprocs=world,
+             join=True)
     for r in range(world):
         res = json.load(open(tmp_path / f"rank{r}.json"))
         bad = {k: v for k, v in res.items() if not all(v.values())}
@@ -211,6 +218,7 @@ def _metric_worker(rank, world, port, outdir):
         out = _run_rank(ctx, A, rank, world, kw, exchange=HostExchange(ctx, host))
         L, U = rrlu_sharded_factors(ctx, m, n, out[0], host_comm=host)
         res = _check(A, kw, out, L, U) if rank == 0 else {"skipped": True}
+        res["fused_exchange"] = ctx.lib.tci_last_shard_exchange(ctx.h) == 2
         ctx.close()
         with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
             json.dump(res, fh)
