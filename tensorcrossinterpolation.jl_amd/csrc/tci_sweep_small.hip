@@ -308,7 +308,7 @@ __device__ __forceinline__ void wave_best(double& bv, unsigned& bk, double& bx) 
 #define LUP(i)                                                       \
     do {                                                             \
         const unsigned long long t_ = wall_clock64();                \
-        lup_acc[i] += t_ - lup_t;                                    \
+        if (lup_acc) lup_acc[i] += t_ - lup_t;                       \
         lup_t = t_;                                                  \
     } while (0)
 #else
@@ -512,9 +512,12 @@ template <int TILE>
 __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double reltol, double abstol, int leftorth,
                           int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red, double* pvl,
                           int* nslot, double* dslot, double& error, double& maxerror, int& nanfl,
-                          bool posout = false) {
+                          bool posout = false, unsigned long long* lup_acc = nullptr) {
     static_assert(8 * TILE <= kSwWaveN, "tile");
     const int tid = threadIdx.x;
+#ifdef TCI_SW_PROF
+    unsigned long long lup_t = wall_clock64();
+#endif
     if (tid < 64) {
         const int lane = tid, tr = lane & 7, tc = lane >> 3;
         double v[TILE][TILE];
@@ -551,8 +554,10 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
         double mxe = 0.0, err = __longlong_as_double(0x7ff8000000000000LL);
         int np = 0, fl = 0;
         wave_sync();
+        LUP(0);
         for (int k = 0; k < mr; ++k) {
             wave_best(bv, bk, bx);  // uniform from here on
+            LUP(1);
             int pp = (int)(bk & 0xffffu), qq = (int)(bk >> 16);
             double val = bx;
             if (!(bv >= 0.0)) {  // every trailing value NaN: Julia keeps (k, k)
@@ -577,6 +582,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
             for (int a = 0; a < TILE; ++a) rpos[a] = rpos[a] == k ? pp : (rpos[a] == pp ? k : rpos[a]);
 #pragma unroll
             for (int b = 0; b < TILE; ++b) cpos[b] = cpos[b] == k ? qq : (cpos[b] == qq ? k : cpos[b]);
+            LUP(2);
             // normalisation (true division) of the pivot column / row by their owners: lane column
             // pc mod 8 holds physical column pc in slot pc / 8 (uniform), lane row pr mod 8 row pr
             const double piv = val;
@@ -609,6 +615,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
                             }
                     }
             }
+            LUP(3);
             wave_sync();
             if (lane == 0) {
                 int t = rowphys[k];
@@ -623,6 +630,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
             for (int a = 0; a < TILE; ++a) xr[a] = rpos[a] > k ? xv[tr + 8 * a] : 0.0;
 #pragma unroll
             for (int b = 0; b < TILE; ++b) yc[b] = cpos[b] > k ? yv[tc + 8 * b] : 0.0;
+            LUP(4);
             bv = -1.0;
             bk = 0xffffffffu;
             bx = 0.0;
@@ -635,8 +643,11 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
                         v[a][b] = nv;
                         take(__dmul_rn(nv, nv), ((unsigned)cpos[b] << 16) | (unsigned)rpos[a], nv);
                     }
+            LUP(5);
             wave_sync();  // this pivot's xv / yv reads before the next pivot's writes
+            LUP(6);
         }
+        LUP(7);
         if (fl) atomicOr(nslot, fl);
         if (posout) {
 #pragma unroll
@@ -653,6 +664,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
     maxerror = red[0].val;
     const int np = (int)red[0].key;
     __syncthreads();  // red[] is reused by the caller
+    LUP(8);
     return np;
 }
 
@@ -660,12 +672,13 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
 __device__ __forceinline__ int sw_lu_wave_any(double* S, int ldS, int m, int n, int mr, double reltol, double abstol,
                                               int leftorth, int* rowphys, int* colphys, double* xv, double* yv,
                                               SmallCand* red, double* pvl, int* nslot, double* dslot, double& error,
-                                              double& maxerror, int& nanfl, bool posout = false) {
+                                              double& maxerror, int& nanfl, bool posout = false,
+                                              unsigned long long* lup_acc = nullptr) {
     if (m <= 32 && n <= 32)
         return sw_lu_wave<4>(S, ldS, m, n, mr, reltol, abstol, leftorth, rowphys, colphys, xv, yv, red, pvl, nslot,
-                             dslot, error, maxerror, nanfl, posout);
+                             dslot, error, maxerror, nanfl, posout, lup_acc);
     return sw_lu_wave<8>(S, ldS, m, n, mr, reltol, abstol, leftorth, rowphys, colphys, xv, yv, red, pvl, nslot,
-                         dslot, error, maxerror, nanfl, posout);
+                         dslot, error, maxerror, nanfl, posout, lup_acc);
 }
 
 // ---- the kernel
@@ -932,7 +945,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int np, fl;
                 if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {  // one-wave rrLU
                     np = sw_lu_wave_any(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
-                                    &nanflag, &dslot, error, maxerror, fl);
+                                    &nanflag, &dslot, error, maxerror, fl, false, SWP_ACC);
                 } else if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
                     np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                     &nanflag, &dslot, error, maxerror, fl, SWP_ACC);
@@ -999,8 +1012,10 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                    swp_acc[5] * 0.01 / swp_n, swp_acc[6] * 0.01 / swp_n, swp_acc[7] * 0.01 / swp_n,
                    swp_acc[2] * 0.01 / swp_n, swp_acc[3] * 0.01 / swp_n);
         if (tid == 0)
-            printf("[sweep_small] regs-LU us total: load+take %.1f | wave argmax %.1f | barrier1 %.1f | row argmax %.1f | "
-                   "decide+maps %.1f | normalise %.1f | barrier2 %.1f | update %.1f | loop exit %.1f | NaN %.1f\n",
+            printf("[sweep_small] LU us total (regs-LU | one-wave LU): load+take %.1f | wave argmax %.1f | barrier1 %.1f | "
+                   "row argmax %.1f | decide+maps %.1f | normalise %.1f | barrier2 %.1f | update %.1f | loop exit %.1f | "
+                   "NaN %.1f  (one-wave: 0 load+take, 1 argmax, 2 stop+maps, 3 normalise, 4 swap+xy, 5 update, "
+                   "6 sync, 7 exit, 8 closing barriers)\n",
                    lu_acc[0] * 0.01, lu_acc[1] * 0.01, lu_acc[2] * 0.01, lu_acc[3] * 0.01, lu_acc[4] * 0.01,
                    lu_acc[5] * 0.01, lu_acc[6] * 0.01, lu_acc[7] * 0.01, lu_acc[8] * 0.01, lu_acc[9] * 0.01);
         if (tid == 0)
