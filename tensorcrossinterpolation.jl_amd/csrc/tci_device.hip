@@ -312,30 +312,28 @@ void launch_fill_uniform(hipStream_t s, double* A, int64_t m, int64_t n, int64_t
 // Pi[R + ldo*j] -- an HBM-write-bound stream. Other kinds evaluate directly per element.
 // the kinds, St, leg_state() and combine<KIND>(): tci_funcdev.h
 
-// Row states: R in [0, m*D); i = R % m, c = R / m (centre index, only for M == 1).
-__global__ void k_state_rows(FuncDev f, const int32_t* __restrict__ I, int m, int nl, int M,
-                             int D, St* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t R = gid; R < (int64_t)m * D; R += stride) {
-        const int i = (int)(R % m), c = (int)(R / m);
-        out[R] = leg_state(f, I + (int64_t)i * nl, nl, 0, M ? c + 1 : 0);
+// Row states: R in [0, m*D); i = R % m, c = R / m (centre index, only for M == 1); column states
+// per j; the row states, the column states and the Lorentzian quotient table in ONE launch (block ranges
+// [0, gr) rows, [gr, gr + gc) columns, then the table): the three are independent, and as three
+// launches their ~4 us each of launch latency was ~12 % of an 8192^2 Pi's device time
+__global__ void k_state_prep(FuncDev f, const int32_t* __restrict__ I, int m, int nl, int M, int D,
+                             St* __restrict__ rs, int gr, const int32_t* __restrict__ J, int n, int nr,
+                             int toff, St* __restrict__ cs, int gc, double* __restrict__ tab, int64_t ntab) {
+    const int b = (int)blockIdx.x;
+    if (b < gr) {
+        for (int64_t R = (int64_t)b * blockDim.x + threadIdx.x; R < (int64_t)m * D; R += (int64_t)gr * blockDim.x) {
+            const int i = (int)(R % m), c = (int)(R / m);
+            rs[R] = leg_state(f, I + (int64_t)i * nl, nl, 0, M ? c + 1 : 0);
+        }
+    } else if (b < gr + gc) {
+        for (int64_t j = (int64_t)(b - gr) * blockDim.x + threadIdx.x; j < n; j += (int64_t)gc * blockDim.x)
+            cs[j] = leg_state(f, J + j * nr, nr, toff, 0);
+    } else {
+        const double p0 = f.params[0];
+        const int gt = (int)gridDim.x - gr - gc;
+        for (int64_t s = (int64_t)(b - gr - gc) * blockDim.x + threadIdx.x; s < ntab; s += (int64_t)gt * blockDim.x)
+            tab[s] = p0 / (double)(s + 1);
     }
-}
-
-__global__ void k_state_cols(FuncDev f, const int32_t* __restrict__ J, int n, int nr, int toff,
-                             St* __restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t j = gid; j < n; j += stride) {
-        out[j] = leg_state(f, J + j * nr, nr, toff, 0);
-    }
-}
-
-__global__ void k_lorentz_table(FuncDev f, double* __restrict__ tab, int64_t ntab) {
-    const double p0 = f.params[0];
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ntab; s += (int64_t)gridDim.x * blockDim.x)
-        tab[s] = p0 / (double)(s + 1);
 }
 
 __device__ __forceinline__ void block_maxabs(double v, unsigned long long* maxbits) {
@@ -955,14 +953,13 @@ void launch_batcheval(hipStream_t s, const FuncDev& f, const int32_t* I, int m, 
     if (staged_kind(f.kind)) {
         St* rs = reinterpret_cast<St*>(scratch);
         St* cs = rs + mR;
-        hipLaunchKernelGGL(k_state_rows, dim3(grid_for(mR, 4096)), dim3(256), 0, s, f, I, m, nl, M,
-                           D, rs);
-        hipLaunchKernelGGL(k_state_cols, dim3(grid_for(n, 4096)), dim3(256), 0, s, f, J, n, nr,
-                           f.L - nr, cs);
         double* tab = reinterpret_cast<double*>(cs + n);
         const int64_t ntab = f.kind == F_LORENTZ ? f.ntab : 0;
-        if (ntab > 0)
-            hipLaunchKernelGGL(k_lorentz_table, dim3(grid_for(ntab, 256)), dim3(256), 0, s, f, tab, ntab);
+        {
+            const int gr = grid_for(mR, 4096), gc = grid_for(n, 4096), gt = ntab > 0 ? grid_for(ntab, 256) : 0;
+            hipLaunchKernelGGL(k_state_prep, dim3(gr + gc + gt), dim3(256), 0, s, f, I, m, nl, M, D, rs, gr, J, n,
+                               nr, f.L - nr, cs, gc, tab, ntab);
+        }
         const int64_t ntiles = ((mR + 511) / 512) * ((n + kAsmCols - 1) / kAsmCols);
         const int grid = (int)(ntiles < 4096 ? (ntiles > 0 ? ntiles : 1) : 4096);
         const int vec = (ldo % 2 == 0) && ((uintptr_t)out % 16 == 0);
