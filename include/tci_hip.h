@@ -207,6 +207,13 @@ int tci_func_create_c128(tci_ctx* ctx, const tci_func* const* re, int32_t nre,
  * (batcheval.jl:131-175) for a BatchEvaluator whose sets already live on the device. */
 int tci_batcheval_dd(tci_ctx* ctx, const tci_func* f, const int32_t* d_I, int64_t m, int32_t nl, const int32_t* d_J,
                      int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo, uint64_t* d_maxbits);
+/* As tci_batcheval_dd with HOST index tables: they are copied (pinned stage owned by this entry,
+ * asynchronous upload) and the call returns without synchronising -- the column-sharded 2-site
+ * update (ShardedBatchEvaluator) evaluates its block, runs tci_rrlu_sharded_d (which synchronises
+ * at its end anyway) and only then reads *d_maxbits: one host synchronisation per bond instead of
+ * two. I / J may be reused by the caller as soon as the call returns. */
+int tci_batcheval_da(tci_ctx* ctx, const tci_func* f, const int32_t* I, int64_t m, int32_t nl, const int32_t* J,
+                     int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo, uint64_t* d_maxbits);
 /* ----------------------------------------------------------- batch eval
  * Replaces _batchevaluate_dispatch (batcheval.jl:131-175) plus maxabs (util.jl:34-43) as used by
  * updatemaxsample! (tensorci2.jl:636-638).

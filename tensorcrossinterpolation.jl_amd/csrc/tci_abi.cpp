@@ -100,6 +100,16 @@ struct tci_ctx {
     size_t capScratch2 = 0;
     int32_t* dI = nullptr;
     size_t capI = 0;
+    // tci_batcheval_da's own index tables and pinned stage (no other entry touches them, so its
+    // uploads may still be in flight when the call returns); ev_ina: its last upload
+    int32_t* dIa = nullptr;
+    size_t capIa = 0;
+    int32_t* dJa = nullptr;
+    size_t capJa = 0;
+    char* hina = nullptr;
+    size_t capHina = 0;
+    hipEvent_t ev_ina = nullptr;
+    bool ev_ina_live = false;
     int32_t* dJ = nullptr;
     size_t capJ = 0;
     int32_t* dI2 = nullptr;
@@ -1097,6 +1107,9 @@ int tci_ctx_destroy(tci_ctx* c) {
         if (e) hipEventDestroy(e);
     if (c->hmaxbits) hipHostFree(c->hmaxbits);
     if (c->hin) hipHostFree(c->hin);
+    if (c->hina) hipHostFree(c->hina);
+    fr(c->dIa); fr(c->dJa);
+    if (c->ev_ina) hipEventDestroy(c->ev_ina);
     if (c->hout) hipHostFree(c->hout);
     if (c->zbuf) hipHostFree(c->zbuf);
     fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens);
@@ -1370,6 +1383,31 @@ int tci_batcheval_dd(tci_ctx* c, const tci_func* f, const int32_t* dI, int64_t m
     if (f->kind == TCI_F_C128)
         return set_err(c, TCI_ERR_ARG, "a ComplexF64 integrand needs the ComplexF64 entries (*_c128_*)");
     return batcheval_launch(c, f, dI, m, nl, dJ, n, nr, M, d_out, ldo,
+                            reinterpret_cast<unsigned long long*>(d_maxbits));
+}
+
+int tci_batcheval_da(tci_ctx* c, const tci_func* f, const int32_t* I, int64_t m, int32_t nl, const int32_t* J,
+                     int64_t n, int32_t nr, int32_t M, double* d_out, int64_t ldo, uint64_t* d_maxbits) {
+    if (!c || !f || !d_maxbits || (m > 0 && nl > 0 && !I) || (n > 0 && nr > 0 && !J)) return TCI_ERR_ARG;
+    if (f->kind == TCI_F_HOST || f->kind == TCI_F_C128)
+        return set_err(c, TCI_ERR_ARG, "tci_batcheval_da: host and ComplexF64 integrands need tci_batcheval_d / *_c128_*");
+    int st;
+    const size_t bi = (size_t)std::max<int64_t>(m * nl, 0) * 4, bj = (size_t)std::max<int64_t>(n * nr, 0) * 4;
+    if ((st = ensure(c, &c->dIa, &c->capIa, std::max<size_t>(bi / 4, 1)))) return st;
+    if ((st = ensure(c, &c->dJa, &c->capJa, std::max<size_t>(bj / 4, 1)))) return st;
+    if (!c->ev_ina) HIPCHK(c, hipEventCreateWithFlags(&c->ev_ina, hipEventDisableTiming));
+    if (c->ev_ina_live) HIPCHK(c, hipEventSynchronize(c->ev_ina));  // the last upload has left the stage
+    c->ev_ina_live = false;
+    if ((st = ensure_pinned(c, &c->hina, &c->capHina, bi + bj + 16))) return st;
+    if (bi) memcpy(c->hina, I, bi);
+    if (bj) memcpy(c->hina + bi, J, bj);
+    if (bi) HIPCHK(c, hipMemcpyAsync(c->dIa, c->hina, bi, hipMemcpyHostToDevice, c->stream));
+    if (bj) HIPCHK(c, hipMemcpyAsync(c->dJa, c->hina + bi, bj, hipMemcpyHostToDevice, c->stream));
+    if (bi || bj) {
+        HIPCHK(c, hipEventRecord(c->ev_ina, c->stream));
+        c->ev_ina_live = true;
+    }
+    return batcheval_launch(c, f, c->dIa, m, nl, c->dJa, n, nr, M, d_out, ldo,
                             reinterpret_cast<unsigned long long*>(d_maxbits));
 }
 

@@ -73,6 +73,7 @@ SIGNATURES = {
     "tci_batcheval_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_batcheval_d": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, pdbl], C.c_int),
     "tci_batcheval_dd": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, vp], C.c_int),
+    "tci_batcheval_da": ([vp, vp, vp, i64, i32, vp, i64, i32, i32, vp, i64, vp], C.c_int),
     "tci_rrlu_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, i64, pi64, pdbl],
                    C.c_int),
     "tci_rrlu_c128_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, i64, pi64, pdbl,

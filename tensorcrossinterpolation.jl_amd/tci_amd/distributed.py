@@ -146,12 +146,21 @@ class ShardedBatchEvaluator:
             self._exchange = HostExchange(self.local.ctx, self.comm)
         return self._exchange
 
-    def local_block_device(self, I, J, M=0):
+    def local_block_device(self, I, J, M=0, defer_max=False):
         """This rank's block of Pi evaluated into HBM, as an m x (nloc + 1) device matrix (the last
-        column is the sharded rrLU's scratch), plus (j0, j1) and the global max|Pi|."""
+        column is the sharded rrLU's scratch), plus (j0, j1) and the global max|Pi|.
+
+        defer_max (catalog integrands): the block is evaluated with tci_batcheval_da -- the index
+        tables uploaded asynchronously, max|Pi| folded into a device word, no host synchronisation
+        -- and the third result is a callable that reads the word and reduces it over the ranks
+        (with any local evaluation error, so that a failure raises on every rank together). The
+        caller runs the collective work that follows first (the sharded rrLU, which synchronises at
+        its end), then calls it: one host synchronisation per bond."""
         from . import _lib
 
         ctx = self.local.ctx
+        if defer_max and getattr(self.local, "kind", None) not in (None, 10):  # 10: TCI_F_HOST
+            return self._local_block_deferred(I, J, M)
         I = np.ascontiguousarray(np.asarray(I, np.int32))
         J = np.ascontiguousarray(np.asarray(J, np.int32))
         m, nl = I.shape
@@ -177,6 +186,47 @@ class ShardedBatchEvaluator:
             except Exception as e:  # raised on every rank by the reduction (no rank left waiting)
                 err = e
         return view, (j0, j1), self.comm.allreduce_maxabs(mx, err)
+
+    def _local_block_deferred(self, I, J, M):
+        from . import _lib
+
+        ctx = self.local.ctx
+        I = np.ascontiguousarray(np.asarray(I, np.int32))
+        J = np.ascontiguousarray(np.asarray(J, np.int32))
+        m, nl = I.shape
+        D = self.localdims[nl] if M == 1 else 1
+        j0, j1 = self.block(len(J))
+        nloc = j1 - j0
+        rows = m * D
+        ld = max(16, (rows + 15) // 16 * 16)
+        need = ld * (nloc + 1)
+        if self._buf is None or self._buf.size < need:
+            if self._buf is not None:
+                self._buf.free()
+            self._buf = _DevBuf(ctx, int(need * 1.25) + 1024)
+        if getattr(self, "_maxword", None) is None:
+            self._maxword = _DevBuf(ctx, 1)
+        zero = np.zeros(1, np.uint64)
+        ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, self._maxword.ptr, _lib.ptr(zero), 8))
+        view = _DevView(ctx, self._buf.ptr, rows, nloc + 1, ld)
+        err = None
+        if nloc > 0 and rows > 0:
+            Jl = np.ascontiguousarray(J[j0:j1])
+            try:
+                ctx.check(ctx.lib.tci_batcheval_da(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), nloc,
+                                                   Jl.shape[1], M, view.ptr, ld, self._maxword.ptr))
+            except Exception as e:  # raised on every rank by the deferred reduction
+                err = e
+
+        def reduce_max():
+            bits = np.zeros(1, np.uint64)
+            mx = 0.0
+            if err is None and nloc > 0 and rows > 0:
+                ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, _lib.ptr(bits), self._maxword.ptr, 8))
+                mx = float(bits.view(np.float64)[0])
+            return self.comm.allreduce_maxabs(mx, err)
+
+        return view, (j0, j1), reduce_max
 
     @property
     def device_gather(self):
@@ -294,12 +344,18 @@ class ShardedBatchEvaluator:
         tensorci2.update_pivots_device (pivot positions, pivot errors, max|Pi|; no factors)."""
         rows = np.asarray(rows, np.int32)
         cols = np.asarray(cols, np.int32)
-        view, (j0, j1), gmx = self.local_block_device(rows, cols, 0)
+        # catalog integrands: the block evaluated without a host synchronisation, max|Pi| reduced
+        # after the factorisation (whose end synchronises anyway); a rank whose evaluation failed
+        # still takes part in the sharded rrLU (on whatever its block holds) and then raises with
+        # every other rank in the reduction -- no rank is left waiting in an exchange
+        view, (j0, j1), gmx = self.local_block_device(rows, cols, 0, defer_max=True)
         m, n = len(rows), len(cols)
         npv, err, rp, cp, pe = rrlu_sharded(view, m, n, j0, j1 - j0, comm=self.device_comm,
                                             exchange=None if self.device_comm is not None else self.exchange(),
                                             maxrank=min(int(maxrank), m, n), reltol=reltol, abstol=abstol,
                                             leftorthogonal=leftorth)
+        if callable(gmx):
+            gmx = gmx()
         return {"rowidx": rp[:npv].copy(), "colidx": cp[:npv].copy(), "pivoterrors": pe.copy(), "maxabs": gmx,
                 "npivot": npv}
 

@@ -96,3 +96,36 @@ def test_dd_rejects_host_and_null(ctx):
     f = T.lorentz([3] * 4, ctx=ctx)
     r = ctx.lib.tci_batcheval_dd(ctx.h, f.h, None, 1, 2, None, 1, 2, 0, None, 1, None)
     assert r != 0
+
+
+@pytest.mark.parametrize("M", [0, 1])
+def test_da_equals_d(ctx, M):
+    """tci_batcheval_da (host tables, asynchronous upload, device running maximum; the sharded 2-site
+    update's evaluation): bitwise tci_batcheval_d's Pi and max, over several back-to-back calls whose
+    host tables are overwritten as soon as each call returns."""
+    ld = [10] * 8
+    f = T.lorentz(ld, ctx=ctx)
+    rng = np.random.default_rng(11 + M)
+    nl = 4
+    dmax = T.DeviceMatrix(2, 1, ctx=ctx)
+    outs = [T.DeviceMatrix(200 * (10 if M else 1), 150, ctx=ctx) for _ in range(3)]
+    try:
+        ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, dmax.ptr, T._lib.ptr(np.zeros(1, np.uint64)), 8))
+        I = np.zeros((200, nl), np.int32)
+        J = np.zeros((150, 8 - nl - M), np.int32)
+        refs, mxs = [], []
+        for out in outs:
+            I[:] = rng.integers(1, 11, I.shape)
+            J[:] = rng.integers(1, 11, J.shape)
+            ctx.check(ctx.lib.tci_batcheval_da(ctx.h, f.h, T._lib.ptr(I), 200, nl, T._lib.ptr(J), 150, J.shape[1], M,
+                                               out.ptr, out.ld, dmax.ptr))
+            ref, mx = f.pi(I.copy(), J.copy(), M)
+            refs.append(ref)
+            mxs.append(mx)
+        for out, ref in zip(outs, refs):
+            assert np.array_equal(out.to_host(), ref)
+        assert dmax_value(ctx, dmax) == max(mxs)
+    finally:
+        dmax.free()
+        for o in outs:
+            o.free()
