@@ -14,8 +14,8 @@
 #   pmcsum             scripts/pmc_summary.py over this call's TAG_pmc* passes -> TAG_pmc_summary.json
 #   avail              rocprofv3 --list-avail                                  -> TAG_avail.txt
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS                                      -> TAG_py_SCRIPT.txt
-# Round 4's one-off call scripts (scripts/r04/sN.sh) are in the git history; what each ran is listed
-# in profiles/README.md.
+# Round 4's one-off call scripts (scripts/r04/sN.sh) are in the git history; what each ran, and
+# which profiles/ files each call's results became, is listed in profiles/README.md.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
