@@ -248,6 +248,16 @@ int tci_rrlu_inplace_d(tci_ctx* ctx, double* d_A, int64_t m, int64_t n, int64_t 
                        int64_t maxrank, double reltol, double abstol, int leftorth,
                        int64_t* rowperm, int64_t* colperm, int64_t* npivot, double* lasterror,
                        double* pivoterrors);
+/* rrlu(A) on device memory (matrixlu.jl:455-463: `rrlu!(copy(A))`): d_src (m x n, ld ldsrc) is
+ * left untouched and d_W (ld ldw, even; 16-byte aligned; must not overlap d_src) receives the copy
+ * and is used as the work matrix, as tci_rrlu_inplace_d. The copy is fused into the initial argmax
+ * pass (it reads the input once and writes the work matrix as it searches) where the pass pipeline
+ * runs; the one-launch small / mid paths copy first. Same outputs and results as copying d_src into
+ * d_W and calling tci_rrlu_inplace_d. */
+int tci_rrlu_copy_d(tci_ctx* ctx, const double* d_src, int64_t ldsrc, double* d_W, int64_t m, int64_t n,
+                    int64_t ldw, int64_t maxrank, double reltol, double abstol, int leftorth,
+                    int64_t* rowperm, int64_t* colperm, int64_t* npivot, double* lasterror,
+                    double* pivoterrors);
 
 /* rrlu(A::Matrix{ComplexF64}) (matrixlu.jl:455-463; the _optimizerrlu! loop :346-396 on complex
  * entries). A, L, U are ComplexF64 stored interleaved (re, im) column-major

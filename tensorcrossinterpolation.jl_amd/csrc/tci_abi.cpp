@@ -449,10 +449,21 @@ int rrlu_epochs(const tci_ctx* c, int64_t m, int64_t n) {
     return (double)m * (double)n >= 2.4e7 ? 3 : 1;
 }
 
+// dsrc (optional): the input, ld ldsrc; dA is then the work matrix it is copied into (rrlu's copy,
+// matrixlu.jl:462) -- by the pass pipeline's initial argmax pass as it reads (one read of the input,
+// not a copy kernel and then the pass), by an explicit copy ahead of the one-launch paths
 int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64_t maxrank,
-                double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out) {
+                double reltol, double abstol, int leftorth, int64_t* np_out, double* err_out,
+                const double* dsrc = nullptr, int64_t ldsrc = 0) {
     int st;
     c->sh_valid = 0;  // the shared rrLU buffers are about to be overwritten
+    auto copy_input = [&]() -> int {
+        if (dsrc && m > 0 && n > 0)
+            HIPCHK(c, hipMemcpy2DAsync(dA, lda * sizeof(double), dsrc, ldsrc * sizeof(double), m * sizeof(double),
+                                       n, hipMemcpyDeviceToDevice, c->stream));
+        dsrc = nullptr;
+        return TCI_OK;
+    };
     if ((st = ensure(c, &c->rowperm, &c->capPerm, (size_t)m + 1))) return st;
     if ((st = ensure(c, &c->colperm, &c->capColperm, (size_t)n + 1))) return st;
     if ((st = ensure(c, &c->rowpos, &c->capRowpos, (size_t)m + 1))) return st;
@@ -464,6 +475,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if (mr < 0) mr = 0;
     c->ldUp = std::max<int64_t>(mr, 1);
     if (m == 0 || n == 0 || mr == 0) {
+        if ((st = copy_input())) return st;
         HIPCHK(c, hipMemcpyAsync(c->hst, c->st, sizeof(RrluState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         *np_out = 0;
@@ -473,6 +485,9 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
     if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
     if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * n)))) return st;
+    if (dsrc && ((c->small_path && tci::rrlu_small_fits(m, n)) ||
+                 (c->mid_path && !c->mid_faulted && c->ncu > 0 && tci::rrlu_mid_fits(m, n, c->ncu))))
+        if ((st = copy_input())) return st;
     if (c->small_path && tci::rrlu_small_fits(m, n)) {
         // the whole factorisation in one workgroup's LDS: one launch instead of one per pivot
         HIPCHK(c, tci::launch_rrlu_small(c->stream, dA, lda, mi, ni, (int)mr, reltol, abstol,
@@ -568,7 +583,10 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     const int nbx = nb * epochs;
     g.nbs = nb;
     g.pe = g.ps = 0;
+    g.Asrc = dsrc;  // (the initial pass copies the input into A as it reads it)
+    g.ldsrc = ldsrc;
     tci::launch_pass(c->stream, 0, false, shadow, g, grid);  // argmax of A, selects pivot 0
+    g.Asrc = nullptr;
     // The pass schedule: pass kk applies PE exact / PS shadow pending updates and is a
     // write-back (flush), a refresh, or read-only; te / ts: the first pivot whose update is pending in
     // fp64 / in the shadow. A deterministic function of kk, so a resume can replay it.
@@ -1438,6 +1456,25 @@ int tci_rrlu_inplace_d(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda
     if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
     int st;
     if ((st = rrlu_device(c, dA, m, n, lda, maxrank, reltol, abstol, leftorth, npivot, lasterror)))
+        return st;
+    if ((st = extract_LU(c, m, n, *npivot, leftorth, false, false))) return st;  // NaN checks
+    if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;
+    return pivot_errors(c, *npivot, *lasterror, pivoterrors);
+}
+
+int tci_rrlu_copy_d(tci_ctx* c, const double* d_src, int64_t ldsrc, double* dW, int64_t m, int64_t n, int64_t ldw,
+                    int64_t maxrank, double reltol, double abstol, int leftorth, int64_t* rowperm,
+                    int64_t* colperm, int64_t* npivot, double* lasterror, double* pivoterrors) {
+    if (!c || !npivot || !lasterror) return TCI_ERR_ARG;
+    if (m < 0 || n < 0 || ldw < m || (ldw & 1) || ((uintptr_t)dW & 15) || ldsrc < m || (m > 0 && n > 0 && !d_src))
+        return set_err(c, TCI_ERR_ARG, "rrlu: need ld >= m for both matrices, ldw even and a 16-byte aligned work matrix");
+    if (m > INT32_MAX / 2 || n > INT32_MAX / 2) return set_err(c, TCI_ERR_ARG, "matrix too large");
+    // the two must not overlap: the copy is fused into a pass that reads one while writing the other
+    const uintptr_t s0 = (uintptr_t)d_src, s1 = (uintptr_t)(d_src + ldsrc * std::max<int64_t>(n, 1));
+    const uintptr_t w0 = (uintptr_t)dW, w1 = (uintptr_t)(dW + ldw * std::max<int64_t>(n, 1));
+    if (m > 0 && n > 0 && s0 < w1 && w0 < s1) return set_err(c, TCI_ERR_ARG, "rrlu: input and work matrix overlap");
+    int st;
+    if ((st = rrlu_device(c, dW, m, n, ldw, maxrank, reltol, abstol, leftorth, npivot, lasterror, d_src, ldsrc)))
         return st;
     if ((st = extract_LU(c, m, n, *npivot, leftorth, false, false))) return st;  // NaN checks
     if ((st = fetch_perms(c, rowperm, colperm, rowperm ? m : 0, colperm ? n : 0))) return st;

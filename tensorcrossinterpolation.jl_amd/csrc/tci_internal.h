@@ -80,6 +80,10 @@ struct PassArgs {
     // last written -- by a write-back or a refresh -- after pivot k - ps); shadow epochs since the
     // last write-back are nbs pivots long. pe == ps: no refresh since the write-back.
     int pe = 0, ps = 0, nbs = 0;
+    // rrlu's copy (matrixlu.jl:462) fused into the initial argmax pass: that pass reads the input
+    // from Asrc (ld ldsrc) and writes it to A while it searches (null: A already holds the input)
+    const double* Asrc = nullptr;
+    int64_t ldsrc = 0;
 };
 
 // Selection fields of PassArgs as seen by the device.

@@ -522,6 +522,8 @@ struct PassK {
     float* S;  // fp32 shadow of the stale values (ld lds), or null
     int64_t lds;
     int pe, ps, nbs;  // two-level epoch: exact / shadow pending counts, shadow epoch length
+    const double* Asrc;  // initial pass only: the input to copy into A while searching (or null)
+    int64_t ldsrc;
 };
 
 // LDS of a one-workgroup-per-CU pass: the staged columns' y's [local column][slot] in fp64 (and
@@ -609,6 +611,11 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
     const int r0 = tr * kRowsPerTile + slice * 128 + 2 * lane;
     const bool rowok = r0 < m, pair = r0 + 1 < m;
     double* const base = A + (rowok ? r0 : 0);  // rows past m read row 0 (never used)
+    // the initial pass with rrlu's copy fused: it reads the input (ld ldsrc) and stores every value
+    // it reads into A (uniform; the copy's read of the input is this pass's own read)
+    const bool cpy = P == 0 && g.Asrc != nullptr;
+    const double* const sbase = cpy ? g.Asrc + (rowok ? r0 : 0) : base;
+    const int64_t slda = cpy ? g.ldsrc : lda;
     auto chunk_col = [&](int g0, int h) -> int {
         const int it = g0 + (h * U) / cb;
         return (q + (rev ? ntc - 1 - it : it) * nq) * cb + (h * U) % cb;
@@ -617,7 +624,7 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
         const int j = chunk_col(g0, h);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double2* pa = reinterpret_cast<const double2*>(base + (int64_t)min(j + u, n - 1) * lda);
+            const double2* pa = reinterpret_cast<const double2*>(sbase + (int64_t)min(j + u, n - 1) * slda);
             if constexpr (FLUSH && TCI_FLUSH_NTL) {
                 typedef double dv2 __attribute__((ext_vector_type(2)));
                 const dv2 w = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(pa));
@@ -737,6 +744,13 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
         auto column = [&](double2 v, int lc, int j) {
             const int cp = cpos_s[lc];
             if (cp <= k) return;
+            if (P == 0 && cpy && rowok) {  // (columns past n: cp = -1, returned above)
+                double* pw = base + (int64_t)j * lda;
+                if (pair)
+                    *reinterpret_cast<double2*>(pw) = v;
+                else
+                    pw[0] = v.x;
+            }
             if constexpr (SH && kShHalf && !FLUSH && P > 0) {
                 // pass 0 of an fp16 shadow: the shadow of the stale values (A itself), whose bound
                 // |pivot 0| is known only now. Every row: the epoch starts at pivot 0, so pivot
@@ -2544,7 +2558,7 @@ void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, in
                       g.ticket, g.reltol, g.abstol,  g.selk,    nullptr, 0};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
                   g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
-                  g.pe, g.ps, g.nbs};
+                  g.pe, g.ps, g.nbs, g.Asrc, g.ldsrc};
     const EpochArgs e{npass, serp, sync, timeout};
     if (g.pe > g.ps)
         hipLaunchKernelGGL((k_pass_mf_epoch<true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
@@ -2584,7 +2598,7 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
                       g.ticket, g.reltol, g.abstol,  g.selk,    g.lout, g.pc_off};
     const PassK a{g.A,  g.lda, g.m,  g.n,   g.k,        g.X,    g.ldx, g.Y,   g.ldy,
                   g.Lp, g.ldl, g.Up, g.ldu, g.leftorth, g.cand, g.cb,  g.rev, g.S, g.lds,
-                  g.pe, g.ps, g.nbs};
+                  g.pe, g.ps, g.nbs, g.Asrc, g.ldsrc};
     if (shadow && kShHalf) {
         // fp16: the shadow's scale needs |pivot 0|, so the initial pass only selects, and pass 0
         // (exact) writes the shadow of A; write-backs write the shadow of the new stale values
@@ -2637,7 +2651,7 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
                           h.ticket, h.reltol, h.abstol,  h.selk,    h.lout, h.pc_off};
         const PassK a{h.A,  h.lda, h.m,  h.n,   h.k,        h.X,    h.ldx, h.Y,   h.ldy,
                       h.Lp, h.ldl, h.Up, h.ldu, h.leftorth, h.cand, h.cb,  h.rev, h.S, h.lds,
-                      h.pe, h.ps, h.nbs};
+                      h.pe, h.ps, h.nbs, h.Asrc, h.ldsrc};
         hipLaunchKernelGGL((k_pass_x<1>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
         return;
     }

@@ -89,6 +89,8 @@ SIGNATURES = {
     "tci_tt_evaluate_c128_h": ([vp, C.c_int32, vp, vp, vp, i64, vp, i64, vp], C.c_int),
     "tci_rrlu_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, pi64, pdbl, vp],
                            C.c_int),
+    "tci_rrlu_copy_d": ([vp, vp, i64, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, pi64, pdbl, vp],
+                        C.c_int),
     "tci_luci_h": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),
     "tci_luci_inplace_d": ([vp, vp, i64, i64, i64, i64, dbl, dbl, C.c_int, vp, vp, vp, vp, vp, pi64], C.c_int),
     "tci_update_pivots_h": ([vp, vp, vp, i64, i32, vp, i64, i32, i64, dbl, dbl, C.c_int, C.c_int, vp,

@@ -245,8 +245,11 @@ class DeviceMatrix:
 
 
 def rrlu_inplace_device(dm, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftorthogonal=True,
-                        want_perms=True):
-    """rrlu! on a DeviceMatrix: returns (npivot, error, rowperm, colperm, pivoterrors)."""
+                        want_perms=True, src=None):
+    """rrlu! on a DeviceMatrix: returns (npivot, error, rowperm, colperm, pivoterrors).
+    src (a DeviceMatrix of the same shape, not overlapping dm): rrlu(src) -- src is copied into dm
+    (matrixlu.jl:462) by the factorisation's first pass as it reads it (tci_rrlu_copy_d), and dm
+    is the work matrix; src is left untouched."""
     ctx = dm.ctx
     m, n = dm.m, dm.n
     rowperm = np.zeros(max(m, 1), np.int64) if want_perms else None
@@ -255,6 +258,15 @@ def rrlu_inplace_device(dm, maxrank=INT64_MAX, reltol=1e-14, abstol=0.0, leftort
     pe = np.zeros(mr + 1)
     npv = C.c_int64()
     err = C.c_double()
+    if src is not None:
+        if (src.m, src.n) != (m, n):
+            raise ValueError("rrlu: src and the work matrix differ in shape")
+        ctx.check(ctx.lib.tci_rrlu_copy_d(ctx.h, src.ptr, src.ld, dm.ptr, m, n, dm.ld, int(min(maxrank, INT64_MAX)),
+                                          float(reltol), float(abstol), int(bool(leftorthogonal)),
+                                          _lib.ptr(rowperm), _lib.ptr(colperm), C.byref(npv),
+                                          C.byref(err), _lib.ptr(pe)))
+        k = npv.value
+        return k, err.value, rowperm, colperm, pe[: k + 1]
     ctx.check(ctx.lib.tci_rrlu_inplace_d(ctx.h, dm.ptr, m, n, dm.ld, int(min(maxrank, INT64_MAX)),
                                          float(reltol), float(abstol), int(bool(leftorthogonal)),
                                          _lib.ptr(rowperm), _lib.ptr(colperm), C.byref(npv),

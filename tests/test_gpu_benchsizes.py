@@ -66,3 +66,26 @@ def test_rrlu_device_inplace_metric_bitwise(ctx):
     assert np.array_equal(cp[:n] - 1, ref.colpermutation)
     assert err == ref.error
     assert np.array_equal(pe, ref.pivoterrors)
+
+
+@pytest.mark.timeout(300)
+def test_rrlu_device_copy_metric_bitwise(ctx):
+    """bench.py's step as it runs now: rrlu(A) with the copy fused into the initial pass
+    (tci_rrlu_copy_d) at the metric size -- permutations, npivot, lu.error and pivot errors bitwise
+    the oracle's, and the input untouched."""
+    m = n = 8192
+    r = 256
+    A, ref = oracle(m, n, r, True)
+    src = T.DeviceMatrix(m, n, ctx=ctx)
+    src.fill_uniform(seed=0)
+    W = T.DeviceMatrix(m, n, ctx=ctx)
+    npv, err, rp, cp, pe = T.rrlu_inplace_device(W, maxrank=r, src=src)
+    untouched = bool(np.array_equal(src.to_host(), A))
+    W.free()
+    src.free()
+    assert untouched
+    assert npv == ref.npivot
+    assert np.array_equal(rp[:m] - 1, ref.rowpermutation)
+    assert np.array_equal(cp[:n] - 1, ref.colpermutation)
+    assert err == ref.error
+    assert np.array_equal(pe, ref.pivoterrors)
