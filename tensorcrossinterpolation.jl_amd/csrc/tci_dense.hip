@@ -516,7 +516,7 @@ __device__ __forceinline__ void wave_argmax(double& bv, int& bi) {
 
 constexpr int kRegPanelThreads = 1024;
 
-template <int NBP, int RPT>
+template <int NBP, int RPT, int NT = kRegPanelThreads>
 struct RegPanel {  // one thread's state (the column steps are unrolled by recursion: every index of v
     double v[RPT][NBP];  // is a constant, so v lives in registers)
     double bv;
@@ -529,10 +529,10 @@ struct RegPanel {  // one thread's state (the column steps are unrolled by recur
     double* crow;
 };
 
-template <int NBP, int RPT, int C>
-__device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
+template <int NBP, int RPT, int C, int NT>
+__device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT, NT>& S) {
     if constexpr (C < NBP) {
-        constexpr int NT = kRegPanelThreads, NW = NT / 64;
+        constexpr int NW = NT / 64;
         if (C < S.nbp) {
             const int tid = S.tid;
             wave_argmax(S.bv, S.bi);
@@ -595,18 +595,20 @@ __device__ __forceinline__ void reg_panel_col(RegPanel<NBP, RPT>& S) {
                 }
             }
         }
-        reg_panel_col<NBP, RPT, C + 1>(S);
+        reg_panel_col<NBP, RPT, C + 1, NT>(S);
     }
 }
 
-template <int NBP, int RPT>
-__global__ __launch_bounds__(kRegPanelThreads) void k_getrf_panel_reg(double* __restrict__ A, int r, int jb,
-                                                                      int nbp, int* __restrict__ piv) {
-    constexpr int NT = kRegPanelThreads, NW = NT / 64;
+// NT threads: 1024 (one row per thread up to 1024 rows) or 256 (four waves, one per SIMD, RPT rows
+// per thread: cheaper barriers, more update work per thread -- TCI_GETRF_NT A/B)
+template <int NBP, int RPT, int NT = kRegPanelThreads>
+__global__ __launch_bounds__(NT) void k_getrf_panel_reg(double* __restrict__ A, int r, int jb,
+                                                        int nbp, int* __restrict__ piv) {
+    constexpr int NW = NT / 64;
     __shared__ double sv[NW];
     __shared__ int si[NW];
     __shared__ double prow[NBP], crow[NBP];
-    RegPanel<NBP, RPT> S;
+    RegPanel<NBP, RPT, NT> S;
     S.tid = threadIdx.x;
     S.rows = r - jb;
     S.nbp = nbp;
@@ -634,7 +636,7 @@ __global__ __launch_bounds__(kRegPanelThreads) void k_getrf_panel_reg(double* __
             if (a > S.bv) { S.bv = a; S.bi = i; }
         }
     }
-    reg_panel_col<NBP, RPT, 0>(S);
+    reg_panel_col<NBP, RPT, 0, NT>(S);
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
         const int i = S.tid + u * NT;
@@ -717,10 +719,22 @@ void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv, bool reg) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_getrf_panel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         kPanelLds);
     // panels in registers (k_getrf_panel_reg) unless the context's dense mask drops kDenseGetrfReg
+    // 256 threads (four waves, RPT rows each) by default: 9.32 -> 8.95 ms for the r = 1024 solve
+    // (getrf 6.93 -> 6.58 ms; profiles/r05_l1_ab_getrf_nt.txt); TCI_GETRF_NT=1024 for the A/B
+    static const int nt_env = [] {
+        const char* e = getenv("TCI_GETRF_NT");
+        return e ? atoi(e) : 256;
+    }();
     for (int jb = 0; jb < r;) {
         const int rows = r - jb;
         int nbp;
-        if (reg && rows <= kRegPanelThreads) {
+        if (reg && nt_env == 256 && rows <= 1024) {
+            nbp = std::min(24, rows);
+            hipLaunchKernelGGL((k_getrf_panel_reg<24, 4, 256>), dim3(1), dim3(256), 0, s, A, r, jb, nbp, piv);
+        } else if (reg && nt_env == 256 && rows <= 2048) {
+            nbp = std::min(16, rows);
+            hipLaunchKernelGGL((k_getrf_panel_reg<16, 8, 256>), dim3(1), dim3(256), 0, s, A, r, jb, nbp, piv);
+        } else if (reg && rows <= kRegPanelThreads) {
             nbp = std::min(24, rows);
             hipLaunchKernelGGL((k_getrf_panel_reg<24, 1>), dim3(1), dim3(kRegPanelThreads), 0, s, A, r, jb, nbp, piv);
         } else if (reg && rows <= 2 * kRegPanelThreads) {
