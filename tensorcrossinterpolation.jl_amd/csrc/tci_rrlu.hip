@@ -2027,21 +2027,36 @@ constexpr int kXU = TCI_XU;   // columns per chunk (two chunks in flight per lan
 static_assert(kXU == 4 || kXU == 8, "chunks of 4 or 8 columns (cb is a multiple of 8)");
 constexpr int kXSlices = kXHalf / 128;
 constexpr int kXReps = kP2Threads / 64 / kXSlices;
+// Geometry of the deep exact body by workgroup size: NT = 1024 (one workgroup per CU, 512-row
+// tiles in two 256-row halves: also the fallback body of k_pass_mf) or NT = 512 for the write-back
+// launch (two workgroups per CU, 256-row tiles in two 128-row halves, 64 KiB of LDS each: one
+// workgroup's staging and y_k chains overlap the other's streaming)
+template <int NT>
+struct PxGeom {
+    static constexpr int Half = NT == 1024 ? 256 : 128;  // rows whose x's are in LDS at a time
+    static constexpr int Tile = 2 * Half;                // rows of a workgroup's tile
+    static constexpr int Slices = Half / 128;
+    static constexpr int Reps = NT / 64 / Slices;
+};
 // (16-B aligned: the update loop reads a lane's two x's and two y's with one ds_read_b128 each -- as
 // ds_read2_b64 pairs at a 16-B lane stride the x reads were 4-way bank conflicts, and the loop was
 // LDS-bound: round 4's 31.5 M conflict cycles per deep write-back)
-struct alignas(16) PxLds {
-    alignas(16) double xs[kMaxPendR * kXHalf];   // x_s of the half-tile's rows
-    alignas(16) double ys[kMaxPendR * kXStage];  // y_s of the staged columns
+template <int NT>
+struct alignas(16) PxLdsT {
+    alignas(16) double xs[kMaxPendR * PxGeom<NT>::Half];  // x_s of the half-tile's rows
+    alignas(16) double ys[kMaxPendR * kXStage];          // y_s of the staged columns
     double xa[kMaxPendR];            // X[s][a] (pivot row a)
     double yb[kMaxPendR];            // Y[s][b] (pivot column b)
     int cpos[kXStage];
-    int cnt[kXSlices];
+    int cnt[PxGeom<NT>::Slices];
 };
+using PxLds = PxLdsT<kP2Threads>;
 
-template <int MODE, bool COH = false>
-__device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, PxLds& L, CandR& best,
+template <int MODE, bool COH = false, int NT = kP2Threads>
+__device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, PxLdsT<NT>& L, CandR& best,
                                            unsigned long long (&pt)[8]) {
+    constexpr int kXHalf = PxGeom<NT>::Half, kXSlices = PxGeom<NT>::Slices, kXReps = PxGeom<NT>::Reps;
+    constexpr int kRowsPerTile = PxGeom<NT>::Tile, kP2Threads = NT;
     RrluState* st = sel.st;
     const int32_t* rowpos = sel.rowpos;
     const int32_t* colpos = sel.colpos;
@@ -2311,15 +2326,15 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
     return true;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kP2Threads) void k_pass_x(PassK g, SelArgs sel) {
-    __shared__ PxLds L;
+template <int MODE, int NT = kP2Threads>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_pass_x(PassK g, SelArgs sel) {
+    __shared__ PxLdsT<NT> L;
     [[maybe_unused]] unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PPROF(0);
     CandR best = cand_none();
-    if (!passx_body<MODE>(g, sel, L, best, pt)) return;
+    if (!passx_body<MODE, false, NT>(g, sel, L, best, pt)) return;
     PPROF(3);
-    pass_tail<kP2Threads>(best, sel, g.cand, pt, g.m, g.pe, MODE);
+    pass_tail<NT>(best, sel, g.cand, pt, g.m, g.pe, MODE);
 }
 
 template <int P, bool EXT, bool RF>
@@ -2652,7 +2667,19 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
         const PassK a{h.A,  h.lda, h.m,  h.n,   h.k,        h.X,    h.ldx, h.Y,   h.ldy,
                       h.Lp, h.ldl, h.Up, h.ldu, h.leftorth, h.cand, h.cb,  h.rev, h.S, h.lds,
                       h.pe, h.ps, h.nbs, h.Asrc, h.ldsrc};
-        hipLaunchKernelGGL((k_pass_x<1>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        // TCI_PASSX_NT=512: 512-thread workgroups, two per CU, over 256-row tiles -- the same column
+        // sets (nq) with twice the row tiles (A/B; default one 1024-thread workgroup per 512-row tile)
+        static const int px_nt = [] {
+            const char* e = getenv("TCI_PASSX_NT");
+            return e ? atoi(e) : 1024;
+        }();
+        const int tiles_r = (h.m + kRowsPerTile - 1) / kRowsPerTile;
+        const int nq = grid / tiles_r;
+        const int tiles_r2 = (h.m + PxGeom<512>::Tile - 1) / PxGeom<512>::Tile;
+        if (px_nt == 512 && (int64_t)tiles_r2 * nq <= kMaxPassGrid)
+            hipLaunchKernelGGL((k_pass_x<1, 512>), dim3(tiles_r2 * nq), dim3(512), 0, s, a, sel);
+        else
+            hipLaunchKernelGGL((k_pass_x<1>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
         return;
     }
     const int PP = kind == 1 || !(shadow && kShHalf) ? h.pe : h.ps;
