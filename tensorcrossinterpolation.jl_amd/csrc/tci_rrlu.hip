@@ -2667,11 +2667,13 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
         const PassK a{h.A,  h.lda, h.m,  h.n,   h.k,        h.X,    h.ldx, h.Y,   h.ldy,
                       h.Lp, h.ldl, h.Up, h.ldu, h.leftorth, h.cand, h.cb,  h.rev, h.S, h.lds,
                       h.pe, h.ps, h.nbs, h.Asrc, h.ldsrc};
-        // TCI_PASSX_NT=512: 512-thread workgroups, two per CU, over 256-row tiles -- the same column
-        // sets (nq) with twice the row tiles (A/B; default one 1024-thread workgroup per 512-row tile)
+        // 512-thread workgroups, two per CU, over 256-row tiles -- the same column sets (nq) with
+        // twice the row tiles: one workgroup's staging and y_k chains overlap the other's streaming
+        // (8192^2: 298-300 -> 289-290 us per write-back, profiles/r05_o1_ab_passx_nt.txt; 497 parity
+        // tests green on it). TCI_PASSX_NT=1024: one 1024-thread workgroup per 512-row tile
         static const int px_nt = [] {
             const char* e = getenv("TCI_PASSX_NT");
-            return e ? atoi(e) : 1024;
+            return e ? atoi(e) : 512;
         }();
         const int tiles_r = (h.m + kRowsPerTile - 1) / kRowsPerTile;
         const int nq = grid / tiles_r;
