@@ -361,28 +361,51 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
     }
     __syncthreads();
     if (!last_s) return;
-    // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
-    constexpr int CPT = kMaxPassGrid / NT;
     // the physical row / column at position selk (swapped by the commit) and the running maximum
     // pivot error (the stop test): requested with the candidates, not after them
     int64_t rk = -1, ck = -1;
     double mxe = 0.0;
-    if (threadIdx.x == 0) {
-        rk = sel.rowphys[sel.selk];
-        ck = sel.colphys[sel.selk];
-        mxe = st->maxerror;
-    }
-    CandR cs[CPT];
+    CandR w;
+    constexpr int kWaveCand = 8;  // candidates per lane when wave 0 alone reduces
+    if ((int)gridDim.x <= 64 * kWaveCand) {
+        // wave 0 alone: every lane's candidates in flight at once, one wave reduction, no barrier
+        // (the other waves of the committing workgroup are done)
+        if (threadIdx.x >= 64) return;
+        if (threadIdx.x == 0) {
+            rk = sel.rowphys[sel.selk];
+            ck = sel.colphys[sel.selk];
+            mxe = st->maxerror;
+        }
+        CandR cs[kWaveCand];
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-        const int i = threadIdx.x + u * NT;
-        cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
-    }
-    CandR w = cs[0];
+        for (int u = 0; u < kWaveCand; ++u) {
+            const int i = threadIdx.x + u * 64;
+            cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
+        }
+        w = cs[0];
 #pragma unroll
-    for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
-    __syncthreads();  // block_reduce_cand's LDS slots are reused
-    block_reduce_cand<NT>(w);
+        for (int u = 1; u < kWaveCand; ++u) cand_take(w, cs[u]);
+        wave_reduce_cand(w);
+    } else {
+        // all of this thread's candidate loads in flight at once (grid <= kMaxPassGrid)
+        constexpr int CPT = kMaxPassGrid / NT;
+        if (threadIdx.x == 0) {
+            rk = sel.rowphys[sel.selk];
+            ck = sel.colphys[sel.selk];
+            mxe = st->maxerror;
+        }
+        CandR cs[CPT];
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int i = threadIdx.x + u * NT;
+            cs[u] = i < (int)gridDim.x ? load_cand_sc1(cand + i) : cand_none();
+        }
+        w = cs[0];
+#pragma unroll
+        for (int u = 1; u < CPT; ++u) cand_take(w, cs[u]);
+        __syncthreads();  // block_reduce_cand's LDS slots are reused
+        block_reduce_cand<NT>(w);
+    }
 #endif
     if (threadIdx.x == 0) {
         __hip_atomic_store(sel.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
