@@ -261,10 +261,22 @@ __device__ __forceinline__ CandR load_cand_sc1(const Cand* src) {
 #endif
 #if TCI_PASS_PROF
 __device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
+__device__ unsigned long long g_pprof_x[kMaxPassGrid * 4];  // thread 0's prologue sub-phases (k_pass_mf)
 __shared__ unsigned g_exam_lds;  // exact examinations of this workgroup (k_pass_mf)
 #define PPROF(i) (pt[i] = wall_clock64())
+#define PPROFX(i)                                                                                   \
+    do {                                                                                            \
+        if (threadIdx.x == 0)                                                                       \
+            __hip_atomic_store(&g_pprof_x[blockIdx.x * 4 + (i)], wall_clock64(), __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_AGENT);                                           \
+    } while (0)
 #else
 #define PPROF(i) ((void)pt)
+#define PPROFX(i) ((void)0)
+#endif
+
+#ifndef TCI_PASS_ONEP
+#define TCI_PASS_ONEP 0  // 1: every EXT read-only pass launches one instance, k_pass_mf<kEpochMaxP, true, false, true>
 #endif
 
 #ifndef TCI_TICKET_XCD
@@ -488,6 +500,26 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
             }
             printf("  [k=%d] thread 0: entry->pivot known %.2f | ->end of startup %.2f | ->y's staged %.2f | ->streaming %.2f\n",
                    sel.selk, s06 / G * us, s61 / G * us, s17 / G * us, s72 / G * us);
+            {  // k_pass_mf prologue sub-phases of thread 0 (0 when the kernel has none)
+                double x0 = 0, x1 = 0, x2 = 0, x3 = 0;
+                int nxs = 0;
+                for (int i = 0; i < (int)gridDim.x; ++i) {
+                    unsigned long long t0 = __hip_atomic_load(&gp[i * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long q[4];
+                    for (int z = 0; z < 4; ++z)
+                        q[z] = __hip_atomic_load(&g_pprof_x[i * 4 + z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (q[0] < t0 || q[3] < q[0]) continue;  // a stale stamp of another kernel
+                    x0 += (double)(q[0] - t0);
+                    x1 += (double)(q[1] - q[0]);
+                    x2 += (double)(q[2] - q[1]);
+                    x3 += (double)(q[3] - q[2]);
+                    ++nxs;
+                }
+                if (nxs)
+                    printf("  [k=%d] thread 0 prologue (%d wgs): entry->pivot in hand %.2f | ->prefetches issued %.2f | "
+                           "->certificate %.2f | ->x/y chain inputs issued %.2f\n",
+                           sel.selk, nxs, x0 / nxs * us, x1 / nxs * us, x2 / nxs * us, x3 / nxs * us);
+            }
             printf("  [k=%d] end by XCD: %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f | by round: %.1f %.1f %.1f %.1f\n",
                    sel.selk, (ex[0] / nx[0] - t0min) * us, (ex[1] / nx[1] - t0min) * us,
                    (ex[2] / nx[2] - t0min) * us, (ex[3] / nx[3] - t0min) * us,
@@ -1425,11 +1457,15 @@ __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int n
             sumM += fabs(at(t));
             maxM = fmax(maxM, fabs(at(t)));
         }
-        const double s = sh_scale(e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1)));  // sh_bound(pv, e)
+        const double B = e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1));  // sh_bound(pv, e)
+        const double s = sh_scale(B);
+        // 1 / s: s is a power of two (or 0, then unused), so x / s == x * rs exactly -- the two
+        // fp64 divisions per epoch had been ~1/3 of this function's time on the pass's critical path
+        const double rs = kShHalf ? (s > 0.0 ? ldexp(1.0, ilogb(B) - kShExp) : 0.0) : 1.0;
         const double Mfd = fabs(at(e)) + d;
         const double mag = Mfd + 2.0 * sumM;
-        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 / s + 0x1p-19 * sumM +
-                                        (double)P * 0x1p-24 / s + (double)(3 * P + 4) * 0x1p-23 * mag
+        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 * rs + 0x1p-19 * sumM +
+                                        (double)P * 0x1p-24 * rs + (double)(3 * P + 4) * 0x1p-23 * mag
                                   : 0.0;
         c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -TCI_SH_TIGHT);
         if (cur) {
@@ -1503,6 +1539,10 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         bq = (int)ldc<true>(&st->q);
         piv = ldc<true>(&st->pval);
     }
+#if TCI_PASS_PROF
+    if (threadIdx.x == 0) asm volatile("" ::"s"(a), "s"(bq));  // (the pivot in hand)
+#endif
+    PPROFX(0);
     // thread / workgroup indices: inside the persistent epoch kernel (COH) made opaque per pass, so
     // that nothing derived from them is hoisted out of its pass loop (kept live across every pass,
     // those values spilled the body's registers)
@@ -1605,7 +1645,30 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         pend_pre<COH>(pre, stager ? g.Y + (jst >= 0 && jst < n ? jst : 0) : g.X + (rrow < m ? rrow : 0),
                  stager ? ldy : ldx, PE - 1);
     }
+    PPROFX(1);
+    // The pivot-dependent chain inputs go out before the certificate is derived, so that its scalar
+    // arithmetic (~2 us at PE ~ 28, EXT prologue profile of round 5) overlaps their round trip: EXT,
+    // lane s of every wave holds the pivot's side, X[s][a] (stager waves) or Y[s][bq] (row waves) --
+    // one load per lane, no barrier; the row threads' A[row][bq], the stagers' A[a][column] (EXT).
+    // (Clamped: after the last pivot the state's p, q are not meaningful; those values are unused.)
+    // The chains that readlane upl run on whole waves (the stager / row split is by wave): a
+    // spilled upl reloaded under a partial exec mask would leave the inactive lanes' values undefined.
+    const int ac = min(max(a, 0), m - 1), bc = min(max(bq, 0), n - 1);
+    const int jj = jst >= 0 && jst < n ? jst : 0;
+    [[maybe_unused]] double upl = 0.0;
+    if constexpr (EXT) {
+        upl = ldc<COH>((stager ? g.X + ac : g.Y + bc) + (int64_t)min(lane, kMaxPendR - 1) * (stager ? ldx : ldy));
+    }
+    double a0 = 0.0;
+    if (!stager)
+        a0 = g.A[(rrow < m ? rrow : 0) + (int64_t)bc * lda];
+    else if constexpr (EXT)
+        a0 = g.A[ac + (int64_t)jj * lda];
     const ShCert cert = sh_cert(certw, k, Pr, PE, g.nbs > 0 ? g.nbs : Pr);
+#if TCI_PASS_PROF
+    if (threadIdx.x == 0) asm volatile("" ::"v"(cert.eps));
+#endif
+    PPROFX(2);
 #ifdef TCI_EPOCH_DEBUG
     {
         const double c0 = readlane_dbl(certw, 0), c1 = readlane_dbl(certw, 1), c2 = readlane_dbl(certw, 2),
@@ -1622,14 +1685,6 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         RF ? (float)(sh_scale(sh_bound(pv, k + 1)) / shs) : 1.0f;  // a power of two: exact
     if (st_done) return kMfStop;
     PPROF(6);
-    // EXT: lane s of every wave holds the pivot's side, X[s][a] (stager waves) or Y[s][bq] (row
-    // waves) -- one load per lane, no barrier. The chains that readlane it run on whole waves (the
-    // stager / row split is by wave): a spilled upl reloaded under a partial exec mask would leave
-    // the inactive lanes' values undefined.
-    [[maybe_unused]] double upl = 0.0;
-    if constexpr (EXT) {
-        upl = ldc<COH>((stager ? g.X + a : g.Y + bq) + (int64_t)min(lane, kMaxPendR - 1) * (stager ? ldx : ldy));
-    }
     if (!stager) {
         // row thread: x_k of its row (the reference's operation order), the split A fragment row
         // -(x_0 .. x_{P-1}) with the data masking of rows outside the trailing block
@@ -1640,7 +1695,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             for (int s = 0; s < P - 1; ++s)
                 if (s < Pr - 1) xs[s] = ldc<COH>(g.X + (int64_t)(off + s) * ldx + rr);
         }
-        double xk = g.A[rr + (int64_t)bq * lda];
+        double xk = a0;
         if constexpr (EXT) {  // all PE - 1 exact pending updates
             // the shadow-pending x's first: pivot-independent, in flight with the chain's loads
             // (requested after the chain they were one more round trip before the barrier)
@@ -1700,11 +1755,9 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // (Requesting the first group's shadow-pending y's here too, with the chain's loads, would save
     // the staging's round trip for them, but holding them across the chain spills: 2 VGPRs at
     // P = 3, 4, 10-14 at P = 9, 10.)
+    PPROFX(3);
     if constexpr (EXT) {
-        if (stager) {
-            const int jj = jst >= 0 && jst < n ? jst : 0;
-            yk0 = pend_chain<COH>(g.A[a + (int64_t)jj * lda], pre, g.Y + jj, ldy, upl, PE - 1);
-        }
+        if (stager) yk0 = pend_chain<COH>(a0, pre, g.Y + jj, ldy, upl, PE - 1);
     }
     PPROF(1);
     bool act = false;
@@ -2360,7 +2413,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     pass_tail<NT>(best, sel, g.cand, pt, g.m, g.pe, MODE);
 }
 
-template <int P, bool EXT, bool RF>
+// RT: one instance for every shadow-pending count (P its bound, g.ps the count): the EXT passes of
+// all depths then run the same code, which stays in the instruction cache from pass to pass
+template <int P, bool EXT, bool RF, bool RT = false>
 __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     __shared__ union {
         P2Lds<P> x;
@@ -2373,7 +2428,7 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     if (threadIdx.x == 0) g_exam_lds = 0;  // (read after the body's barriers)
 #endif
     CandR best = cand_none();
-    const int r = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, pt);
+    const int r = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, pt, RT ? g.ps : P);
     bool go = r == kMfDone;
     if (r == kMfExact) {  // uniform: every workgroup derives the same certificate
         if constexpr (RF)
@@ -2652,6 +2707,8 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
             if constexpr (TCI_SH_MFMA && P <= kMfMaxP) {
                 if (ext && rf)
                     hipLaunchKernelGGL((k_pass_mf<P, true, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+                else if (ext && TCI_PASS_ONEP)
+                    hipLaunchKernelGGL((k_pass_mf<kEpochMaxP, true, false, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
                 else if (ext)
                     hipLaunchKernelGGL((k_pass_mf<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
                 else if (rf)
