@@ -347,8 +347,8 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_z1_pmc_summary.json")
-TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r05_z1_trace_roofline.json")  # scripts/trace_roofline.py
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_z3_pmc_summary.json")
+TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r05_z3_trace_roofline.json")  # scripts/trace_roofline.py
 PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 3, "shadow": True, "sh_bytes": 2}  # the profiled command
 
 

@@ -26,7 +26,8 @@ def family(name):
     if short.startswith("tci::k_pass_sh<"):
         return "rrlu_read_only_pass"
     if short.startswith("tci::k_pass_x<"):  # <MODE>: 1 write-back, 0 / 2 exact fallbacks
-        return {"1": "rrlu_write_back_pass", "2": "rrlu_refresh_pass"}.get(short[-2], "rrlu_read_only_pass")
+        mode = short[short.index("<") + 1:short.rindex(">")].split(",")[0].strip()  # <MODE, NT>
+        return {"1": "rrlu_write_back_pass", "2": "rrlu_refresh_pass"}.get(mode, "rrlu_read_only_pass")
     if short.startswith(("tci::k_pass<", "tci::k_pass2<")):
         targs = [t.strip() for t in short[short.index("<") + 1:short.rindex(">")].split(",")]
         if targs[1] == "true":

@@ -28,7 +28,8 @@ def family(name):
         t = [x.strip() for x in s[s.index("<") + 1:s.rindex(">")].split(",")]
         return "refresh" if t[2] == "true" else "read_only_per_pass"
     if s.startswith("tci::k_pass_x<"):
-        return {"1": "write_back", "2": "refresh"}.get(s[-2], "read_only_per_pass")
+        mode = s[s.index("<") + 1:s.rindex(">")].split(",")[0].strip()  # <MODE, NT>
+        return {"1": "write_back", "2": "refresh"}.get(mode, "read_only_per_pass")
     if s.startswith("tci::k_pass2<"):
         t = [x.strip() for x in s[s.index("<") + 1:s.rindex(">")].split(",")]
         if t[0] == "0":
