@@ -523,6 +523,9 @@ int tci_free_d(tci_ctx* ctx, void* p);
 int tci_memcpy_h2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int tci_memcpy_d2h(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int tci_memcpy_d2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+/* bytes bytes of dst set to (unsigned char)value, stream-ordered on the context stream (no host
+ * synchronisation; e.g. the device max word of tci_batcheval_da) */
+int tci_memset_d(tci_ctx* ctx, void* dst, int value, int64_t bytes);
 /* strided copy of `height` rows of `width` bytes (e.g. matrix columns between leading dimensions) */
 int tci_memcpy2d_d2d(tci_ctx* ctx, void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
                      int64_t height);

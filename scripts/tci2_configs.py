@@ -18,14 +18,34 @@ import tci_amd as T  # noqa: E402
 ORACLE = os.environ.get("TCI2_CONFIGS_ORACLE", "0") == "1"  # also time the CPU oracle (where bounded)
 
 
-def run(name, f, localdims, initialpivots=None, oracle_ok=False, **kw):
+def _timed(f, localdims, initialpivots, kw, reps):
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = T.crossinterpolate2(f, localdims, initialpivots, **kw)
+        wall = time.perf_counter() - t0
+        best = wall if best is None else min(best, wall)
+    return best, out
+
+
+REPS = int(os.environ.get("TCI2_REPS", "3"))
+
+
+def run(name, f, localdims, initialpivots=None, oracle_ok=False, reps=None, **kw):
+    """wall_s: crossinterpolate2 doing the reference's work (fillsitetensors! evaluates P and
+    solves every site tensor after each sweep2site!, tensorci2.jl:1254-1256); wall_s_lazy: the same
+    run with lazy_sitetensors=True (those solves skipped where no global search reads them --
+    identical results, fewer f evaluations). Best of `reps` after a warm-up."""
+    reps = REPS if reps is None else reps
     T.crossinterpolate2(f, localdims, initialpivots, **dict(kw, maxiter=1))  # warm the kernels
-    t0 = time.perf_counter()
-    tci, ranks, errors = T.crossinterpolate2(f, localdims, initialpivots, **kw)
-    wall = time.perf_counter() - t0
-    res = {"config": name, "wall_s": round(wall, 4), "iterations": len(ranks),
+    wall, (tci, ranks, errors) = _timed(f, localdims, initialpivots, kw, reps)
+    res = {"config": name, "wall_s": round(wall, 4), "lazy_sitetensors": False, "iterations": len(ranks),
            "ranks": ranks, "final_error": errors[-1], "linkdims": tci.linkdims(),
            "kwargs": {k: v for k, v in kw.items() if k != "rng"}}
+    if kw.get("nsearchglobalpivot", 5) == 0:
+        wl, (tl, rl, el) = _timed(f, localdims, initialpivots, dict(kw, lazy_sitetensors=True), reps)
+        res["wall_s_lazy"] = round(wl, 4)
+        res["lazy_identical"] = bool(rl == ranks and list(el) == list(errors) and tl.linkdims() == tci.linkdims())
     if ORACLE and oracle_ok and kw.get("nsearchglobalpivot", 5) == 0:
         # the CPU oracle (1 core, deterministic mode) on the same integrand, initial pivots and kwargs
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -105,13 +125,18 @@ def configs():
         K, L, d = 1024, 12, 32
         f = T.cp_function(0.5 + rng.random((K, L, d)))
         p0 = T.optfirstpivot(f, [d] * L)
+        kw = dict(tolerance=1e-10, maxbonddim=1024, maxiter=3, nsearchglobalpivot=0)
         t0 = time.perf_counter()
-        tci, ranks, errors = T.crossinterpolate2(f, [d] * L, [p0], tolerance=1e-10, maxbonddim=1024,
-                                                 maxiter=3, nsearchglobalpivot=0)
+        tci, ranks, errors = T.crossinterpolate2(f, [d] * L, [p0], **kw)  # the reference's work
         wall = time.perf_counter() - t0
         res = {"config": "C5: 12d CP-rank-1024 synthetic d=32 tol=1e-10 maxbonddim=1024 maxiter=3",
-               "wall_s": round(wall, 3), "iterations": len(ranks), "ranks": ranks,
+               "wall_s": round(wall, 3), "lazy_sitetensors": False, "iterations": len(ranks), "ranks": ranks,
                "final_error": errors[-1], "linkdims": tci.linkdims()}
+        if os.environ.get("TCI2_C5_LAZY", "1") == "1":
+            t0 = time.perf_counter()
+            _, rl, el = T.crossinterpolate2(f, [d] * L, [p0], lazy_sitetensors=True, **kw)
+            res["wall_s_lazy"] = round(time.perf_counter() - t0, 3)
+            res["lazy_identical"] = bool(rl == ranks and list(el) == list(errors))
         gp = os.path.join(ROOT, "tests", "golden", "c5_golden.json")
         if os.path.exists(gp):  # the committed oracle result (tests/golden/make_c5_golden.py)
             import json as _json

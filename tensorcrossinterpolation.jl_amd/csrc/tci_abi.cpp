@@ -485,6 +485,11 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     if ((st = ensure(c, &c->pivv, &c->capPivv, (size_t)mr + 1))) return st;
     if ((st = ensure(c, &c->Lp, &c->capLp, (size_t)(m * mr)))) return st;
     if ((st = ensure(c, &c->Up, &c->capUp, (size_t)(mr * n)))) return st;
+    // the fused copy reads the input as 16-B row pairs (k_pass2's load_chunk): an odd ldsrc or a
+    // source not 16-byte aligned would give misaligned loads (and, with an odd m and ldsrc == m, a
+    // read 8 B past the last column), so such an input is copied first
+    if (dsrc && ((ldsrc & 1) || ((uintptr_t)dsrc & 15)))
+        if ((st = copy_input())) return st;
     if (dsrc && ((c->small_path && tci::rrlu_small_fits(m, n)) ||
                  (c->mid_path && !c->mid_faulted && c->ncu > 0 && tci::rrlu_mid_fits(m, n, c->ncu))))
         if ((st = copy_input())) return st;
@@ -608,7 +613,8 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
     // (persist == 2, a test mode: also when the grid exceeds one workgroup per CU -- it is then NOT
     // co-resident and the launch must give up, after 2 ms instead of 0.5 s, and resume)
     bool persist = c->persist && !c->persist_faulted && shadow && tci::shadow_two_level() && c->ncu > 0 &&
-                   ((grid <= c->ncu && c->pass_gridx == 1) || c->persist == 2) && tci::epoch_fits(mi, ni, g.cb, grid);
+                   ((grid <= c->ncu && c->pass_gridx == 1) || c->persist == 2) && tci::epoch_fits(mi, ni, g.cb, grid) &&
+                   2 * grid <= kMaxGrid && grid <= 1024;  // candidates double-buffered by pass parity, reduced by 1024 threads
     const long long ptimeout = c->persist == 2 ? 200000 : 50000000;  // 100 MHz ticks
     int64_t nlaunch = 0;  // persistent launches issued (their sync slots)
     if (persist) {
@@ -904,8 +910,24 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
     const bool fused = multi && (c->sh_exchange == 2 || (c->sh_exchange == 0 && (int64_t)(nranks - 1) * fw * 8 <= kFusedMax));
     c->sh_exchange_used = multi ? (fused ? 2 : 1) : 0;
     if (multi) {
-        if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)(fused ? fw : cw)))) return st;
-        if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)(fused ? fw * nranks : cw)))) return st;
+        if ((st = ensure(c, &c->shsend, &c->capShSend, (size_t)std::max<int64_t>(fused ? fw : cw, 2)))) return st;
+        if ((st = ensure(c, &c->shrecv, &c->capShRecv, (size_t)std::max<int64_t>(fused ? fw * nranks : cw, 2)))) return st;
+    }
+    // every rank must run the same exchange form (a fused all-gather on one rank against two
+    // collectives on another would hang RCCL): the choice follows each rank's own setting
+    // (tci_set_shard_exchange / TCI_SHARD_EXCHANGE), so the ranks check that they agree once per
+    // factorisation -- one element-wise max of [fused, !fused]: both 1 means they differ, and
+    // every rank sees it in the same reduction and fails together
+    if (multi && nranks > 1) {
+        const uint64_t mine[2] = {fused ? 1u : 0u, fused ? 0u : 1u};
+        uint64_t got[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(c->shsend, mine, sizeof(mine), hipMemcpyHostToDevice, c->stream));
+        if ((st = shard_exchange(c, comm, exch, user, 1, c->shsend, c->shrecv, 2))) return st;
+        HIPCHK(c, hipMemcpyAsync(got, c->shrecv, sizeof(got), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (got[0] && got[1])
+            return set_err(c, TCI_ERR_ARG, "rrlu_sharded: the ranks chose different exchange forms "
+                                           "(tci_set_shard_exchange / TCI_SHARD_EXCHANGE must be uniform)");
     }
     const int mi = (int)m, nl1 = (int)(nloc + 1);  // local columns + the ghost
     tci::launch_init_state(c->stream, c->st, c->rowpos, c->rowperm, mi, c->colpos, c->colperm, (int)n);
@@ -1071,7 +1093,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
     if (const char* e = getenv("TCI_SW_LUWAVE")) c->sw_lu_wave = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
-    if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = atoi(e) != 0;
+    if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = tci::kEpochGrid && atoi(e) != 0;
     if (const char* e = getenv("TCI_SHARD_EXCHANGE")) c->sh_exchange = std::max(0, std::min(atoi(e), 2));
     if (const char* e = getenv("TCI_EPOCH_KINDS")) c->persist_kinds = atoi(e);
     if (const char* e = getenv("TCI_EPOCH_MAXPASS")) c->persist_maxpass = std::max(1, atoi(e));
@@ -1200,6 +1222,8 @@ int tci_set_rrlu_mid(tci_ctx* c, int enabled) {
 int tci_set_rrlu_persist(tci_ctx* c, int enabled) {
     if (!c) return TCI_ERR_ARG;
     if (enabled < 0 || enabled > 2) return set_err(c, TCI_ERR_ARG, "persist must be 0, 1 or 2 (test mode)");
+    if (enabled && !tci::kEpochGrid)
+        return set_err(c, TCI_ERR_ARG, "the persistent epoch grid is not built (default; -DTCI_EPOCH_GRID=1)");
     c->persist = enabled;
     c->persist_faulted = 0;
     return TCI_OK;
@@ -2405,6 +2429,11 @@ int tci_free_d(tci_ctx* c, void* p) {
 int tci_memcpy_h2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TCI_OK;
+}
+int tci_memset_d(tci_ctx* c, void* dst, int value, int64_t bytes) {
+    if (!c || (bytes > 0 && !dst) || bytes < 0) return TCI_ERR_ARG;
+    if (bytes > 0) HIPCHK(c, hipMemsetAsync(dst, value, (size_t)bytes, c->stream));
     return TCI_OK;
 }
 int tci_memcpy_d2h(tci_ctx* c, void* dst, const void* src, int64_t bytes) {

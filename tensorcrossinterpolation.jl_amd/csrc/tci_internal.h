@@ -217,6 +217,14 @@ void launch_pass(hipStream_t s, int P, bool flush, bool shadow, const PassArgs& 
 #define TCI_EPOCH_MAXP 10
 #endif
 constexpr int kEpochMaxP = TCI_EPOCH_MAXP;
+// The persistent epoch grid was measured slower than the per-pass launches and is
+// compiled only with -DTCI_EPOCH_GRID=1 (make variant NAME=epoch VFLAGS=-DTCI_EPOCH_GRID=1); the
+// default build has no k_pass_mf_epoch, epoch_fits() is false and tci_set_rrlu_persist(ctx, 1 | 2)
+// is refused.
+#ifndef TCI_EPOCH_GRID
+#define TCI_EPOCH_GRID 0
+#endif
+constexpr bool kEpochGrid = TCI_EPOCH_GRID != 0;
 constexpr int kEpochSlot = 64;  // unsigned words per launch (its ticket at 0; a 256-B line of its own)
 void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, int serp, unsigned* sync,
                        long long timeout);

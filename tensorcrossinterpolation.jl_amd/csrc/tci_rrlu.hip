@@ -2468,8 +2468,9 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
 // every later pass launch returns at once. Nothing is selected for the aborted pass, so the host
 // resumes with per-pass launches at pass st->np - 1 (every pass write is idempotent). A certificate
 // that fails (uniform) or an all-NaN trailing block ends the launch the same way with st->done = 3.
-constexpr unsigned kEpochAbort = 0x80000000u;
 constexpr int kEpochMaxCols = 15360;  // columns per workgroup the LDS column map holds (int16 positions)
+#if TCI_EPOCH_GRID
+constexpr unsigned kEpochAbort = 0x80000000u;
 
 // thread 0: wait until `target` arrivals. 1: complete, 0: abort
 __device__ __forceinline__ int epoch_wait(unsigned* ticket, unsigned target, long long timeout, RrluState* st) {
@@ -2659,9 +2660,14 @@ void launch_pass_epoch(hipStream_t s, const PassArgs& g, int grid, int npass, in
         hipLaunchKernelGGL((k_pass_mf_epoch<false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel, e);
 }
 
+#else
+void launch_pass_epoch(hipStream_t, const PassArgs&, int, int, int, unsigned*, long long) {}
+#endif
+
 // whether the persistent epoch launch takes this shape: its LDS column map holds int16 positions of
 // at most kEpochMaxCols columns per workgroup
 bool epoch_fits(int m, int n, int cb, int grid) {
+    if (!kEpochGrid) return false;
     const int tiles_r = (m + kRowsPerTile - 1) / kRowsPerTile, tiles_c = (n + cb - 1) / cb;
     const int nq = grid / tiles_r;
     if (nq < 1 || n > 32768) return false;

@@ -139,6 +139,7 @@ SIGNATURES = {
     "tci_malloc_d": ([vp, C.POINTER(vp), i64], C.c_int),
     "tci_free_d": ([vp, vp], C.c_int),
     "tci_memcpy_h2d": ([vp, vp, vp, i64], C.c_int),
+    "tci_memset_d": ([vp, vp, C.c_int, i64], C.c_int),
     "tci_memcpy_d2h": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy_d2d": ([vp, vp, vp, i64], C.c_int),
     "tci_memcpy2d_d2d": ([vp, vp, i64, vp, i64, i64, i64], C.c_int),

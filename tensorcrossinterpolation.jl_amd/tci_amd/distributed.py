@@ -206,24 +206,28 @@ class ShardedBatchEvaluator:
             self._buf = _DevBuf(ctx, int(need * 1.25) + 1024)
         if getattr(self, "_maxword", None) is None:
             self._maxword = _DevBuf(ctx, 1)
-        zero = np.zeros(1, np.uint64)
-        ctx.check(ctx.lib.tci_memcpy_h2d(ctx.h, self._maxword.ptr, _lib.ptr(zero), 8))
         view = _DevView(ctx, self._buf.ptr, rows, nloc + 1, ld)
         err = None
-        if nloc > 0 and rows > 0:
-            Jl = np.ascontiguousarray(J[j0:j1])
-            try:
+        try:
+            # the max word zeroed stream-ordered (no host synchronisation), then the block
+            ctx.check(ctx.lib.tci_memset_d(ctx.h, self._maxword.ptr, 0, 8))
+            if nloc > 0 and rows > 0:
+                Jl = np.ascontiguousarray(J[j0:j1])
                 ctx.check(ctx.lib.tci_batcheval_da(ctx.h, self.local.h, _lib.ptr(I), m, nl, _lib.ptr(Jl), nloc,
                                                    Jl.shape[1], M, view.ptr, ld, self._maxword.ptr))
-            except Exception as e:  # raised on every rank by the deferred reduction
-                err = e
+        except Exception as e:  # raised on every rank by the deferred reduction
+            err = e
 
         def reduce_max():
-            bits = np.zeros(1, np.uint64)
+            nonlocal err
             mx = 0.0
             if err is None and nloc > 0 and rows > 0:
-                ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, _lib.ptr(bits), self._maxword.ptr, 8))
-                mx = float(bits.view(np.float64)[0])
+                try:  # a failed read-back also reaches the reduction: no rank is left waiting in it
+                    bits = np.zeros(1, np.uint64)
+                    ctx.check(ctx.lib.tci_memcpy_d2h(ctx.h, _lib.ptr(bits), self._maxword.ptr, 8))
+                    mx = float(bits.view(np.float64)[0])
+                except Exception as e:
+                    err = e
             return self.comm.allreduce_maxabs(mx, err)
 
         return view, (j0, j1), reduce_max

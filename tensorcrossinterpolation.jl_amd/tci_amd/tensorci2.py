@@ -557,8 +557,15 @@ class TensorCI2:
                  sweepstrategy="backandforth", pivotsearch="full", verbosity=0, loginterval=10,
                  normalizeerror=True, ncheckhistory=3, globalpivotfinder=None, maxnglobalpivot=5,
                  nsearchglobalpivot=5, tolmarginglobalsearch=10.0, strictlynested=False,
-                 checkbatchevaluatable=False, checkconvglobalpivot=True, rng=None):
-        """optimize! (tensorci2.jl:1018-1172). Returns (ranks, errors ./ errornormalization)."""
+                 checkbatchevaluatable=False, checkconvglobalpivot=True, rng=None, lazy_sitetensors=False):
+        """optimize! (tensorci2.jl:1018-1172). Returns (ranks, errors ./ errornormalization).
+
+        lazy_sitetensors (not a reference keyword; default False = the reference's work): with no
+        global pivot search the site tensors that fillsitetensors! solves after every sweep2site!
+        (tensorci2.jl:1254-1256, :599-629) are never read -- sweep1site! rebuilds all of them at the
+        end -- so True skips their P evaluations and solves and keeps only updatemaxsample!. Ranks,
+        errors, sets and the final tensors are identical; what differs is the work done and the
+        number of f evaluations (visible to a counting or caching evaluator)."""
         errors, ranks, nglobalpivots = [], [], []
         # any BatchEvaluator is accepted (tensorci2.jl:1044): the device evaluators and every
         # HostFunctionEvaluator (pointwise, threaded or batch: it always exposes the batch interface)
@@ -590,12 +597,13 @@ class TensorCI2:
         # The solved site tensors of fillsitetensors! are read only by a global pivot search;
         # with no search they are unobservable (sweep1site! below rebuilds all of them).
         searches = getattr(finder, "nsearch", 1) > 0
+        lazy = bool(lazy_sitetensors) and not searches
         for it in range(1, maxiter + 1):
             errornormalization = self.maxsamplevalue if normalizeerror else 1.0
             abstol = tol * errornormalization
             self.sweep2site(f, 2, iter1=1, abstol=abstol, maxbonddim=maxbonddim, pivotsearch=pivotsearch,
                             strictlynested=strictlynested, verbosity=verbosity, sweepstrategy=sweepstrategy,
-                            fillsitetensors=True, lazy_sitetensors=not searches)
+                            fillsitetensors=True, lazy_sitetensors=lazy)
             errors.append(self.pivoterror())
             globalpivots = finder(self, f, abstol, verbosity=verbosity, rng=rng) if searches else []
             self.addglobalpivots(globalpivots)

@@ -169,6 +169,64 @@ def test_sharded_tci2_two_ranks_one_gpu(tmp_path, shard_rrlu):
     assert res[0]["linkdims"] == res[1]["linkdims"]
 
 
+def _gpu_fail_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import tci_amd as T
+
+        ctx = T.context(0)
+        local = T.lorentz([8] * 6, ctx=ctx)
+        fs = ShardedBatchEvaluator(local, Comm(device="cpu"), shard_rrlu=True)
+        kw = dict(tolerance=1e-10, maxiter=8, nsearchglobalpivot=0)
+        lib = ctx.lib
+        real = lib.tci_batcheval_da
+        calls = [0]
+
+        def failing(*a):  # the last rank's deferred evaluation fails from its third call on
+            calls[0] += 1
+            return 1 if calls[0] >= 3 else real(*a)
+
+        res = {}
+        if rank == world - 1:
+            lib.tci_batcheval_da = failing
+        try:
+            T.crossinterpolate2(fs, [8] * 6, **kw)
+            res["raised"] = None
+        except T.TCIError as e:
+            res["raised"] = "own:" + str(e)
+        except RuntimeError as e:
+            res["raised"] = "other:" + str(e)
+        finally:
+            lib.tci_batcheval_da = real
+        res["calls"] = calls[0]
+        # the group and the device path are still usable afterwards
+        tci, ranks, errors = T.crossinterpolate2(fs, [8] * 6, **kw)
+        ref, rranks, rerrors = T.crossinterpolate2(local, [8] * 6, **kw)
+        res["after"] = ranks == rranks and list(errors) == list(rerrors)
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_sharded_deferred_eval_failure_two_ranks_one_gpu(tmp_path):
+    """with shard_rrlu the block is evaluated by tci_batcheval_da and max|Pi| reduced only
+    after the sharded rrLU; a rank whose evaluation fails still takes part in the factorisation and
+    then raises, and every other rank raises with it in the same reduction -- nobody is left inside
+    an exchange, and the group works afterwards."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_gpu_fail_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        want = "own:" if r == 1 else "other:"
+        assert res["raised"] and res["raised"].startswith(want) and res["after"], (r, res)
+
+
 # ------------------------------------------------------------------ column-sharded rrLU protocol
 def _shard_worker(rank, world, port, outdir, fused=False):
     import torch.distributed as dist

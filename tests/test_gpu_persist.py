@@ -24,12 +24,33 @@ def rand(m, n, seed):
     return O.fill_uniform(m * n, seed=seed).reshape((m, n), order="F")
 
 
+NOT_BUILT = "persistent epoch grid not built (the default build; make variant VFLAGS=-DTCI_EPOCH_GRID=1)"
+
+
 def make_ctx(persist=1):
     c = T.Context(0)
     c.check(c.lib.tci_set_rrlu_small(c.h, 0))
     c.check(c.lib.tci_set_rrlu_mid(c.h, 0))
-    c.check(c.lib.tci_set_rrlu_persist(c.h, persist))
+    rc = c.lib.tci_set_rrlu_persist(c.h, persist)
+    if rc != 0 and persist:
+        c.close()
+        pytest.skip(NOT_BUILT)
+    c.check(rc)
     return c
+
+
+def test_default_build_refuses_persist():
+    """The grid was measured slower and is compiled only on request: a build
+    without it refuses tci_set_rrlu_persist(ctx, 1 | 2) with TCI_ERR_ARG, and 0 is always accepted."""
+    c = T.Context(0)
+    try:
+        assert c.lib.tci_set_rrlu_persist(c.h, 0) == 0
+        rc = c.lib.tci_set_rrlu_persist(c.h, 1)
+        if rc != 0:
+            assert rc == 1  # TCI_ERR_ARG
+            assert "TCI_EPOCH_GRID" in c.lib.tci_last_error(c.h).decode()
+    finally:
+        c.close()
 
 
 @pytest.fixture(scope="module")

@@ -50,6 +50,8 @@ def _run(ctx, m, n, r, ld_src=None, leftorth=True, seed=3, epochs=0):
 
 @pytest.mark.parametrize("m,n,r,ld_src,leftorth,epochs", [
     (3001, 2501, 200, 3008, True, 0),    # pass pipeline, odd shape, input ld != work ld
+    (3001, 2501, 200, 3001, True, 0),    # odd input ld (== m): copied first, not read as row pairs
+    (1999, 1800, 100, 2003, False, 0),   # odd input ld > m
     (2500, 3100, 150, None, False, 0),   # right-orthogonal
     (4100, 4000, 120, 4112, True, 3),    # two-level epoch forced (refresh, EXT, deep write-back)
     (90, 70, 70, 96, True, 0),           # one-workgroup small path (explicit copy first)

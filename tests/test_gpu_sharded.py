@@ -145,6 +145,47 @@ def test_sharded_multi_rank_bitwise(tmp_path, world, mode, epochs, exmode):
         assert not bad, (r, bad)
 
 
+def _mismatch_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ctx = T.Context(0)
+        ctx.check(ctx.lib.tci_set_shard_exchange(ctx.h, 1 + rank % 2))  # rank 0 two collectives, rank 1 fused
+        exchange = HostExchange(ctx, Comm(device="cpu"))
+        A, kw = _cases()["random_1000x900_r100"]
+        res = {}
+        try:
+            _run_rank(ctx, A, rank, world, kw, exchange=exchange)
+            res["raised"] = None
+        except T.TCIArgumentError as e:
+            res["raised"] = str(e)
+        # agreeing again, the same ranks factorise bitwise
+        ctx.check(ctx.lib.tci_set_shard_exchange(ctx.h, 0))
+        out = _run_rank(ctx, A, rank, world, kw, exchange=exchange)
+        L, U = rrlu_sharded_factors(ctx, A.shape[0], A.shape[1], out[0], host_comm=Comm(device="cpu"))
+        res["after"] = all(_check(A, kw, out, L, U).values())
+        ctx.close()
+        with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
+            json.dump(res, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(200)
+def test_sharded_exchange_forms_must_agree(tmp_path):
+    """the exchange form follows each rank's own setting; ranks that disagree fail
+    together with TCI_ERR_ARG (one agreement reduction per factorisation) instead of issuing
+    collectives of different kinds and counts."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_mismatch_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        res = json.load(open(tmp_path / f"rank{r}.json"))
+        assert res["raised"] and "exchange forms" in res["raised"] and res["after"], (r, res)
+
+
 def _gather_worker(rank, world, port, outdir):
     import torch.distributed as dist
 
