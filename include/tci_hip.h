@@ -370,6 +370,22 @@ int tci_tci2_get_sets(tci_tci2* tci, int which, int64_t* counts, int32_t* packed
  * kinds. *handled = 0: not done here (other kinds, a non-square pivot matrix, a site too large);
  * the caller runs its own loop (tci_sitetensor_h / a batch maxabs per site). */
 int tci_tci2_fill_maxsample(tci_tci2* tci, const tci_func* f, int* handled);
+/* fillsitetensors! as the reference runs it (globalsearch.jl:202-208; setsitetensor!,
+ * tensorci2.jl:599-629): per site Pi1, updatemaxsample!, P = f(Iset[p+1] x Jset[p]) and the solve
+ * T = transpose(transpose(P) \ transpose(Pi1)) (LAPACK getrf / getrs of P^T, partial pivoting, the
+ * oracle's operation order), the last site T = Pi1 -- all sites in one device launch for the staged
+ * catalog kinds (pivot matrices up to 64 x 64). Site p's tensor at tensors[offsets[2p]],
+ * offsets[2p+1] doubles, column-major (len(Iset[p]) d) x len(Jset[p]); capacity in doubles.
+ * *handled = 0: not done here (as tci_tci2_fill_maxsample, or a pivot matrix over 64); the caller
+ * runs tci_sitetensor_h per site. */
+int tci_tci2_fill_solve(tci_tci2* tci, const tci_func* f, double* tensors, int64_t capacity, int64_t* offsets,
+                        int* handled);
+/* tci_tci2_sweep2site followed by tci_tci2_fill_solve's work in the same device launch when the
+ * device-resident path runs; *filled = 0: the caller runs its own fill loop. */
+int tci_tci2_sweep2site_fillsolve(tci_tci2* tci, const tci_func* f, int32_t niter, int32_t iter1,
+                                  double abstol, int64_t maxbonddim, int32_t sweepstrategy,
+                                  int32_t strictlynested, double* tensors, int64_t capacity,
+                                  int64_t* offsets, int* filled);
 /* Replaces sweep1site!(tci, f, sweepdirection; reltol, abstol, maxbonddim, updatetensors)
  * (tensorci2.jl:659-725) for the staged catalog kinds when every bond fits the one-workgroup
  * rrLU: the whole sweep in one device launch (per bond kronecker product on the sweep's side, Pi,

@@ -279,9 +279,11 @@ int ensure(tci_ctx* c, T** p, size_t* cap, size_t n) {
 // fp16 shadow: its padding rows [m, lds) of every column are read by the MFMA search (as part of
 // a lane's 16-row load) and must be zero; no pass writes them
 int zero_shadow_pad(tci_ctx* c, int64_t lds, int64_t m, int64_t n) {
-    if (tci::shadow_elem_bytes() != 2 || lds <= m || n <= 0) return TCI_OK;
-    HIPCHK(c, hipMemset2DAsync(reinterpret_cast<char*>(c->sbuf) + 2 * m, (size_t)(2 * lds), 0,
-                               (size_t)(2 * (lds - m)), (size_t)n, c->stream));
+    const int eb = tci::shadow_elem_bytes();
+    if (eb > 2 || lds <= m || n <= 0) return TCI_OK;
+    // the shadow of 0: fp16 0x0000, 8-bit code 0x80 (offset binary)
+    HIPCHK(c, hipMemset2DAsync(reinterpret_cast<char*>(c->sbuf) + eb * m, (size_t)(eb * lds), eb == 1 ? 0x80 : 0,
+                               (size_t)(eb * (lds - m)), (size_t)n, c->stream));
     return TCI_OK;
 }
 
@@ -662,7 +664,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
                 g.rev = c->serpentine ? (int)((kk + 1) & 1) : 0;
                 const bool sampled = kk % c->timing_stride == 0;
                 // pass 0 (shadow on: the exact pass that writes the shadow of A) is a family of its own
-                const bool pass0 = kk == 0 && shadow && tci::shadow_elem_bytes() == 2 && !s.flush;
+                const bool pass0 = kk == 0 && shadow && tci::shadow_elem_bytes() <= 2 && !s.flush;
                 ev_begin(c, s.flush ? 0 : s.refresh ? 23 : pass0 ? tci_ctx::kFamPass0 : 2, sampled,
                          s.flush || s.refresh || pass0 ? -1 : (s.PE > s.PS ? 24 : 3) + s.PS);
                 tci::launch_pass(c->stream, s.PE, s.flush, shadow, g, grid, s.flush ? 1 : s.refresh ? 2 : 0);
@@ -2836,6 +2838,7 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
     a.lu_wave = c->sw_lu_wave;
     a.tens = nullptr;
     a.tcap = 0;
+    a.fsolve = mode != 2 && s1 && s1->tensors ? 1 : 0;  // a fill that also solves the site tensors
     if (s1 && s1->tensors) {  // the site tensors in HBM: [site] (offset, count), then the data
         if ((st = ensure(c, &c->sw_tens, &c->capSwTens, (size_t)(2 * L + s1->tcap)))) return st;
         a.tens = c->sw_tens;
@@ -2851,7 +2854,8 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
         for (int p = 0; p < L; ++p) bytes += (size_t)cn[(size_t)b * L + p] * width(b, p) * 4;
     if (bytes > outcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: output image overflow");
     out.assign(c->sw_out, c->sw_out + bytes);
-    if (s1 && s1->tensors && hdr[0] == 0 && s1->table) {  // the tensors the sweep wrote, one copy
+    // the tensors the sweep (mode 2) or the solving fill wrote (fill status hdr[8] == 0), one copy
+    if (s1 && s1->tensors && hdr[0] == 0 && s1->table && (mode == 2 || hdr[8] == 0)) {
         const int64_t used = hdr[10];
         if (used < 0 || used > s1->tcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: tensor overflow");
         HIPCHK(c, hipMemcpyAsync(s1->table, c->sw_tens, (size_t)(2 * L) * 8, hipMemcpyDeviceToHost, c->stream));

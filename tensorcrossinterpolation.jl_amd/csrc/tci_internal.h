@@ -120,12 +120,13 @@ struct FuncDev {
 
 // ---- rrLU (tci_rrlu.hip)
 int argmax_grid(int m, int n, int k, int cb, int max_grid);
-// bytes per element of the rrLU passes' shadow (2: fp16, scaled per epoch; 4: fp32)
+// bytes per element of the rrLU passes' shadow (1: 8-bit codes, 2: fp16, both scaled per epoch;
+// 4: fp32)
 int shadow_elem_bytes();
 bool shadow_two_level();
-// the MFMA search's refresh stores reach the whole fp16 shadow (lds x n) through one 32-bit buffer
-// offset: the two-level epoch needs lds * n * 2 <= 0xFFFFFFF0 bytes
-inline bool refresh_fits(int64_t lds, int64_t n) { return lds * n * 2 <= (int64_t)0xFFFFFFF0; }
+// the MFMA search's refresh stores reach the whole shadow (lds x n) through one 32-bit buffer
+// offset: the two-level epoch needs lds * n * shadow_elem_bytes() <= 0xFFFFFFF0 bytes
+inline bool refresh_fits(int64_t lds, int64_t n) { return lds * n * shadow_elem_bytes() <= (int64_t)0xFFFFFFF0; }
 // pass after pivot k (k = -1: initial argmax) with P pending updates (slot P-1 = pivot k); its
 // last workgroup selects pivot g.selk
 // One 1024-thread workgroup per CU with wave-level dynamic column chunks (k_pass2).
@@ -415,15 +416,16 @@ struct SweepSmallArgs {
     int mode;              // 0: sweep2site! iterations; 1: fillsitetensors!'s maxsample update only;
                            // 2: sweep1site! (s1fwd, s1tens, reltol below)
     int fill;              // mode 0: the maxsample update after the iterations too (header [8] / [9])
+    int fsolve = 0;        // modes 0 (fill) / 1: also setsitetensor!'s solve, the tensors into tens / tcap
     int s1fwd, s1tens;     // mode 2: forward sweep; site tensors (MatrixLUCI factors) wanted
     double reltol;         // mode 2: the rrLU's reltol
-    double* tens;          // mode 2: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
-    int64_t tcap;          // mode 2: doubles available after the 2 L table entries
+    double* tens;          // mode 2 / fsolve: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
+    int64_t tcap;          // mode 2 / fsolve: doubles available after the 2 L table entries
     int lu_wave = 1;       // bonds with m, n <= 32: the one-wave rrLU (sw_lu_wave; env TCI_SW_LUWAVE=0: off)
 };
 // sweep1site! on the device (mode 2): the host's request and where the site tensors go
 struct SwSweep1 {
-    int forward, tensors;
+    int forward, tensors;  // (a fill with the solve: forward unused, tensors = 1)
     double reltol;
     int64_t tcap;      // doubles of tensor data the caller can take
     int64_t* table;    // [site] (offset, count) into data, 2 L entries (host)

@@ -68,11 +68,28 @@ static constexpr int32_t kBig = 0x7fffffff;
 // pure function of the committed pivot values, so the pass that writes the shadow and the passes
 // that read it derive the same s. 0 (search off) when B is outside [2^-100, 2^100] or not finite.
 constexpr bool kShHalf = TCI_SH_HALF != 0;
-#if TCI_SH_HALF
+// TCI_SH_U8: the narrow shadow in 8 bits instead of fp16 -- q = rint(s v) in [-127, 127] stored as
+// the offset-binary byte q + 128, with s = 127 / B per epoch (B the epoch's stale bound, below):
+// 1 B per element per read-only pass instead of 2. Read by the MFMA search only (the byte widened
+// into the fp32 accumulator, the offset -128 carried by one extra split slot of the MFMA, x = 1
+// against y = -128); error bound and certificate in sh_cert.
+#ifndef TCI_SH_U8
+#define TCI_SH_U8 1
+#endif
+constexpr bool kShU8 = TCI_SH_U8 != 0;
+#if TCI_SH_U8
+static_assert(TCI_SH_HALF && TCI_SH_MFMA, "the 8-bit shadow is read by the MFMA search only");
+static_assert(!TCI_EPOCH_GRID, "the persistent epoch grid reads the fp16 shadow only");
+typedef uint8_t shT;
+#elif TCI_SH_HALF
 typedef _Float16 shT;
 #else
 typedef float shT;
 #endif
+#ifndef TCI_SH_TIGHT_U8
+#define TCI_SH_TIGHT_U8 4  // 8-bit shadow: search only while its error bound is below 2^-TCI_SH_TIGHT_U8 |pivot k|
+#endif
+constexpr int kShTight = kShU8 ? TCI_SH_TIGHT_U8 : TCI_SH_TIGHT;
 
 // s = 2^(13 - ilogb B) maps the stale values below 2^14 and leaves one bit of headroom for the
 // pending updates: the certificate needs max |pivot_s| s <= 2^15 (the y's are split into fp16), i.e.
@@ -83,8 +100,22 @@ constexpr int kShExp = 13;
 __device__ __forceinline__ double sh_scale(double B) {
     if (!kShHalf) return 1.0;
     if (!(B >= 0x1p-100 && B <= 0x1p100)) return 0.0;
+    if constexpr (kShU8) return 127.0 / B;  // (the same fp64 quotient in every pass: deterministic)
     return ldexp(1.0, kShExp - ilogb(B));
 }
+// upper bound of 1 / sh_scale(B) (exact for the power-of-two fp16 scale)
+__device__ __forceinline__ double sh_rscale(double B) {
+    if constexpr (kShU8) return B * (1.0 / 127.0) * (1.0 + 0x1p-40);
+    return ldexp(1.0, ilogb(B) - kShExp);
+}
+// the 8-bit code of a scaled value f = s v: clamp to [-127, 127], round to nearest even (the add
+// of 1.5 2^23 + 128 leaves rint(f) + 128 in the low byte of the sum's bits; exact for |f| <= 127).
+// A NaN clamps to an end of the range (an exact examination then finds the NaN, never selected).
+__device__ __forceinline__ uint32_t sh_u8(float f) {
+    f = __builtin_fminf(__builtin_fmaxf(f, -127.0f), 127.0f);
+    return __float_as_uint(f + 12583040.0f) & 0xFFu;
+}
+constexpr uint32_t kShU8Zero = 0x80u;  // the code of 0
 
 // Bound on the stale trailing values of the epoch whose first pending pivot is t0. t0 = 0: the
 // stale values are A itself, bounded by |pivot 0| (the maximum of A). Otherwise they are the
@@ -810,7 +841,14 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                 // pass 0 of an fp16 shadow: the shadow of the stale values (A itself), whose bound
                 // |pivot 0| is known only now. Every row: the epoch starts at pivot 0, so pivot
                 // 0's own row counts as pivoted during it (see k_pass_mf)
-                if (rowok) {
+                if (rowok && kShU8) {
+                    uint8_t* ps = reinterpret_cast<uint8_t*>(g.S) + r0 + (int64_t)j * g.lds;
+                    const uint32_t c0 = sh_u8((float)(v.x * shs));
+                    if (pair)
+                        *reinterpret_cast<uint16_t*>(ps) = (uint16_t)(c0 | sh_u8((float)(v.y * shs)) << 8);
+                    else
+                        ps[0] = (uint8_t)c0;
+                } else if (rowok) {
                     _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
                     const _Float16 h0 = (_Float16)(float)(v.x * shs);
                     if (pair) {
@@ -845,7 +883,17 @@ __device__ __forceinline__ bool pass2_body(const PassK& g, const SelArgs& sel,
                     *pa = v;
                 }
             }
-            if constexpr (SH && kShHalf && FLUSH) {
+            if constexpr (SH && kShU8 && FLUSH) {
+                if (rowok) {  // rows outside the trailing block: 0 (the MFMA search masks by data)
+                    uint8_t* ps = reinterpret_cast<uint8_t*>(g.S) + r0 + (int64_t)j * g.lds;
+                    const uint32_t c0 = in0 ? sh_u8((float)(v.x * shs)) : kShU8Zero;
+                    if (pair)
+                        *reinterpret_cast<uint16_t*>(ps) =
+                            (uint16_t)(c0 | (in1 ? sh_u8((float)(v.y * shs)) : kShU8Zero) << 8);
+                    else
+                        ps[0] = (uint8_t)c0;
+                }
+            } else if constexpr (SH && kShHalf && FLUSH) {
                 if (rowok) {  // rows outside the trailing block: 0 (the MFMA search masks by data)
                     _Float16* ps = reinterpret_cast<_Float16*>(g.S) + r0 + (int64_t)j * g.lds;
                     const _Float16 h0 = in0 ? (_Float16)(float)(v.x * shs) : (_Float16)0.0f;
@@ -1403,6 +1451,9 @@ struct P2MfLds {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+// a lane's 16 shadow rows of one column: two h8v (fp16) or one u32x4v (8-bit codes)
+typedef std::conditional<kShU8, u32x4v, h8v>::type ShVec;
+constexpr int kShVecs = kShU8 ? 1 : 2;
 
 __device__ __forceinline__ void f16_split(double v, _Float16& hi, _Float16& lo) {
     hi = (_Float16)(float)v;
@@ -1459,15 +1510,27 @@ __device__ __forceinline__ ShCert sh_cert(double w, int k, int PS, int PE, int n
         }
         const double B = e == 0 ? fabs(at(0)) : 2.0 * fabs(at(e - 1));  // sh_bound(pv, e)
         const double s = sh_scale(B);
-        // 1 / s: s is a power of two (or 0, then unused), so x / s == x * rs exactly -- the two
-        // fp64 divisions per epoch had been ~1/3 of this function's time on the pass's critical path
-        const double rs = kShHalf ? (s > 0.0 ? ldexp(1.0, ilogb(B) - kShExp) : 0.0) : 1.0;
+        // >= 1 / s without a division: fp16, s is a power of two (or 0, then unused), so x / s ==
+        // x * rs exactly -- the two fp64 divisions per epoch had been ~1/3 of this function's time on
+        // the pass's critical path; u8, B / 127 rounded up
+        const double rs = kShHalf ? (s > 0.0 ? sh_rscale(B) : 0.0) : 1.0;
         const double Mfd = fabs(at(e)) + d;
         const double mag = Mfd + 2.0 * sumM;
-        const double ea = s > 0.0 ? d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 * rs + 0x1p-19 * sumM +
-                                        (double)P * 0x1p-24 * rs + (double)(3 * P + 4) * 0x1p-23 * mag
-                                  : 0.0;
-        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -TCI_SH_TIGHT);
+        double ea = 0.0;
+        if (s > 0.0) {
+            if constexpr (kShU8) {
+                // the 8-bit code: half a unit from the rounding to an integer (the clamp can only move
+                // a value towards the exact one: |s v| <= 127 for every stale value), 2^-14 for the
+                // fp32 scaling and rescaling products; the accumulator's partial sums also carry the
+                // byte offset (+-128 +- 255) and one more term (the offset slot)
+                ea = d + (0.5 + 0x1p-14) * rs + 0x1p-19 * sumM + (double)P * 0x1p-24 * rs +
+                     (double)(3 * P + 5) * 0x1p-23 * (mag + 384.0 * rs);
+            } else {
+                ea = d + 0x1p-11 * (1.0 + 0x1p-9) * Mfd + 0x1p-25 * rs + 0x1p-19 * sumM + (double)P * 0x1p-24 * rs +
+                     (double)(3 * P + 4) * 0x1p-23 * mag;
+            }
+        }
+        c.ok = s > 0.0 && mag < 0x1p100 && maxM * s <= 0x1p15 && ea * s < ldexp(fabs(at(ke)) * s, -kShTight);
         if (cur) {
             c.eps = ea * s;
             c.shs = s;
@@ -1566,7 +1629,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     const int gq = lane >> 4, lcol = lane & 15;  // lane's row quad / column within a chunk
     const int rl = sb + 16 * gq;                 // first of the lane's 16 loaded rows
     const bool rload = rl < lds;                 // lds is a multiple of 16
-    const _Float16* const sbase = reinterpret_cast<const _Float16*>(g.S) + (rload ? rl : 0);
+    const shT* const sbase = reinterpret_cast<const shT*>(g.S) + (rload ? rl : 0);
     auto col_of = [&](int g0, int lc) -> int {  // global column of staged local column lc
         const int it = g0 + (lc >> cbs);
         return ((q + (rev ? ntc - 1 - it : it) * nq) << cbs) + (lc & (cb - 1));
@@ -1586,12 +1649,13 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // Every chunk load is issued unconditionally (a lane past the last column reads the last one,
     // a lane past the last row tile row 0: approx() masks both), so that a fixed number of memory
     // instructions follows each chunk's loads and the compiler waits for that chunk alone.
-    auto load_chunk = [&](int g0, int gcols, int h, h8v (&v)[2]) {
+    // a lane's 16 rows of one column: 32 B of fp16 (two h8v) or 16 B of 8-bit codes (one u32x4v)
+    auto load_chunk = [&](int g0, int gcols, int h, ShVec (&v)[kShVecs]) {
         const int lc = h * 16 + lcol;
         const int j = lc < gcols ? col_of(g0, lc) : n;
-        const h8v* p = reinterpret_cast<const h8v*>(sbase + (int64_t)(j < n ? j : n - 1) * lds);
-        v[0] = p[0];
-        v[1] = p[1];
+        const ShVec* p = reinterpret_cast<const ShVec*>(sbase + (int64_t)(j < n ? j : n - 1) * lds);
+#pragma unroll
+        for (int i = 0; i < kShVecs; ++i) v[i] = p[i];
     };
     // staging: threads 0 .. 511 (one staged column each); the tile's rows: threads 512 .. 1023
     const bool stager = tx < kP2StageCols;
@@ -1616,7 +1680,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     }
     // refresh stores: the shadow as one buffer (the host keeps it below 4 GB for refreshes), the
     // second 16 B of a lane's 32 through a resource 16 B further on (an out-of-range offset stays so)
-    [[maybe_unused]] const int shb = (int)(unsigned)min((int64_t)lds * n * 2, (int64_t)0xFFFFFFF0);
+    [[maybe_unused]] const int shb = (int)(unsigned)min((int64_t)lds * n * (int64_t)sizeof(shT), (int64_t)0xFFFFFFF0);
     [[maybe_unused]] const auto rsS0 = buf_rsrc(g.S, shb);
     [[maybe_unused]] const auto rsS1 = buf_rsrc(reinterpret_cast<const char*>(g.S) + 16, shb - 16);
     int jst = ntc > 0 ? stage_col(0) : -1;
@@ -1628,7 +1692,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     const int prow = tx - kP2StageCols;  // this thread's tile row (row threads)
     const int rrow = tb + (prow >= 0 ? prow : 0);
     const int rpl = rowpos_of(min(rrow, m - 1));
-    h8v va[2], vb[2];
+    ShVec va[kShVecs], vb[kShVecs];
     const int gc0 = ntc > 0 ? min(G, ntc) * cb : 0;
     const int nch0 = (gc0 + 15) / 16;
     // unconditional (no columns: chunk 0 of an empty group reads column n - 1, never used)
@@ -1741,6 +1805,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
         }
 #pragma unroll
         for (int z = 3 * P; z < KS; ++z) sl[z] = (_Float16)0.0f;
+        if constexpr (kShU8) sl[3 * P] = (_Float16)1.0f;  // the 8-bit codes' offset: 1 x (-128)
 #pragma unroll
         for (int z = 0; z < KS / 8; ++z) {
             h8v w;
@@ -1776,7 +1841,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
     // chunk h: the lane's column's maximum |w| over its 16 rows and per 4-row block (-1: not a
     // trailing column)
     int g0r = 0;  // the staged group approx() works on (its columns, for the refresh stores)
-    auto approx = [&](int h, int gcols, const h8v (&v)[2], float (&mbs)[kMfBlk]) -> float {
+    auto approx = [&](int h, int gcols, const ShVec (&v)[kShVecs], float (&mbs)[kMfBlk]) -> float {
         const int lc = h * 16 + lcol;
         const int cp = lc < gcols ? L.cpos[lc] : -1;
         h8v bf[KSt];
@@ -1785,28 +1850,52 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
             bf[u] = *reinterpret_cast<const h8v*>(&L.yb[(lc < gcols ? lc : 0) * KSP + 32 * u + 8 * gq]);
         float c = 0.0f;
         [[maybe_unused]] h8v wout[2];
+        [[maybe_unused]] u32x4v wq;
 #pragma unroll
         for (int b = 0; b < kMfBlk; ++b) {
-            const h8v& hv = v[b >> 1];
-            const int o = 4 * (b & 1);
-            f4v acc = {(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
-            if (!rload) acc = f4v{0.0f, 0.0f, 0.0f, 0.0f};  // rows past the shadow: W = 0
+            f4v acc;
+            if constexpr (kShU8) {
+                // block b: rows 4 b .. 4 b + 3 = the bytes of dword b (v_cvt_f32_ubyte0..3); the offset
+                // -128 comes from the MFMA's constant slot
+                const uint32_t d = __builtin_bit_cast(u32x4v, v[0])[b];
+                acc = f4v{(float)(d & 0xFFu), (float)((d >> 8) & 0xFFu), (float)((d >> 16) & 0xFFu), (float)(d >> 24)};
+                if (!rload) acc = f4v{128.0f, 128.0f, 128.0f, 128.0f};  // rows past the shadow: W = 0
+            } else {
+                const h8v hv = __builtin_bit_cast(h8v, v[(b >> 1) % kShVecs]);
+                const int o = 4 * (b & 1);
+                acc = f4v{(float)hv[o], (float)hv[o + 1], (float)hv[o + 2], (float)hv[o + 3]};
+                if (!rload) acc = f4v{0.0f, 0.0f, 0.0f, 0.0f};  // rows past the shadow: W = 0
+            }
 #pragma unroll
             for (int u = 0; u < KSt; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[b][u], bf[u], acc, 0, 0, 0);
             mbs[b] = __builtin_fmaxf(__builtin_fmaxf(fabsf(acc[0]), fabsf(acc[1])),
                                      __builtin_fmaxf(fabsf(acc[2]), fabsf(acc[3])));
             c = __builtin_fmaxf(c, mbs[b]);
             if constexpr (RF) {  // rows rl + 4 b + t: the new epoch's shadow, 0 off the trailing block
+                if constexpr (kShU8) {
+                    uint32_t q = 0;
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    wout[b >> 1][o + t] = (tmask >> (4 * b + t)) & 1u ? (_Float16)(acc[t] * rscale) : (_Float16)0.0f;
+                    for (int t = 0; t < 4; ++t)
+                        q |= ((tmask >> (4 * b + t)) & 1u ? sh_u8(acc[t] * rscale) : kShU8Zero) << (8 * t);
+                    wq[b] = q;
+                } else {
+                    const int o = 4 * (b & 1);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        wout[b >> 1][o + t] = (tmask >> (4 * b + t)) & 1u ? (_Float16)(acc[t] * rscale) : (_Float16)0.0f;
+                }
             }
         }
         if constexpr (RF) {  // buffer stores, dropped out of range: a fixed count per chunk
             const int j = lc < gcols ? col_of(g0r, lc) : n;
-            const unsigned off = rload && j < n && cp > k ? (unsigned)(((int64_t)j * lds + rl) * 2) : 0xFFFFFFF0u;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[0]), rsS0, (int)off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[1]), rsS1, (int)off, 0, 0);
+            const unsigned off =
+                rload && j < n && cp > k ? (unsigned)(((int64_t)j * lds + rl) * (int64_t)sizeof(shT)) : 0xFFFFFFF0u;
+            if constexpr (kShU8) {
+                __builtin_amdgcn_raw_buffer_store_b128(wq, rsS0, (int)off, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[0]), rsS0, (int)off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, wout[1]), rsS1, (int)off, 0, 0);
+            }
         }
         if (cp <= k) {
 #pragma unroll
@@ -1977,6 +2066,7 @@ __device__ __forceinline__ int pass_mf_body(const PassK& g, const SelArgs& sel, 
                 }
 #pragma unroll
                 for (int z = 3 * P; z < KS; ++z) sl[z] = (_Float16)0.0f;
+                if constexpr (kShU8) sl[3 * P] = (_Float16)-128.0f;  // the 8-bit codes' offset
 #pragma unroll
                 for (int z = 0; z < KS / 8; ++z) {
                     h8v w;
@@ -2331,7 +2421,17 @@ __device__ __forceinline__ bool passx_body(const PassK& g, const SelArgs& sel, P
                             }
                         }
                     }
-                    if constexpr (MODE != 0 && kShHalf) {
+                    if constexpr (MODE != 0 && kShU8) {
+                        if (rowok) {
+                            uint8_t* ps = reinterpret_cast<uint8_t*>(g.S) + (int64_t)j * g.lds + roff;
+                            const uint32_t c0 = in0 ? sh_u8((float)(v[u].x * shs)) : kShU8Zero;
+                            if (pair)
+                                *reinterpret_cast<uint16_t*>(ps) =
+                                    (uint16_t)(c0 | (in1 ? sh_u8((float)(v[u].y * shs)) : kShU8Zero) << 8);
+                            else
+                                ps[0] = (uint8_t)c0;
+                        }
+                    } else if constexpr (MODE != 0 && kShHalf) {
                         if (rowok) {
                             _Float16* ps = reinterpret_cast<_Float16*>(g.S) + (int64_t)j * g.lds + roff;
                             const _Float16 h0 = in0 ? (_Float16)(float)(v[u].x * shs) : (_Float16)0.0f;
@@ -2676,7 +2776,7 @@ bool epoch_fits(int m, int n, int cb, int grid) {
 
 // tiles_r x nq workgroups: every row tile gets nq = min(tiles_c, max_grid / tiles_r) chunks of
 // column tiles (at least one; the host rejects tiles_r > kMaxPassGrid).
-int shadow_elem_bytes() { return kShHalf ? 2 : 4; }
+int shadow_elem_bytes() { return kShU8 ? 1 : kShHalf ? 2 : 4; }
 // the two-level epoch (refresh + EXT passes) exists only in the MFMA search (k_pass_mf): a build
 // without it (TCI_SH_MFMA=0) must write back after every shadow epoch
 bool shadow_two_level() { return kShHalf && TCI_SH_MFMA; }
@@ -2721,15 +2821,19 @@ static void launch_pass_p(hipStream_t s, bool flush, bool shadow, const PassArgs
                     hipLaunchKernelGGL((k_pass_mf<P, false, true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
                 else
                     hipLaunchKernelGGL((k_pass_mf<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            } else if constexpr (kShU8) {  // (k_pass_sh reads an fp16 / fp32 shadow: the exact pass)
+                hipLaunchKernelGGL((k_pass2<P, false, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
             } else {
                 hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
             }
         }
-    } else if (shadow) {
-        if (flush || P == 0)
-            hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
-        else if constexpr (P > 0)
-            hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+    } else if (shadow && !kShHalf) {  // (the fp32 shadow build, TCI_SH_HALF=0)
+        if constexpr (!kShHalf) {
+            if (flush || P == 0)
+                hipLaunchKernelGGL((k_pass2<P, (P > 0), true>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+            else if constexpr (P > 0)
+                hipLaunchKernelGGL((k_pass_sh<P>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
+        }
     } else if (flush) {
         hipLaunchKernelGGL((k_pass2<P, true, false>), dim3(grid), dim3(kP2Threads), 0, s, a, sel);
     } else {

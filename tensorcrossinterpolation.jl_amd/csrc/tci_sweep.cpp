@@ -329,8 +329,10 @@ namespace {
 // sweepstrategy: 0 = backandforth, 1 = forward, 2 = backward (sweepstrategies.jl:41-50). fill:
 // also fillsitetensors!'s maxsample update on the device after the iterations (*filled = 1 when
 // it was done there).
+// (solve: the fill also solves every site tensor, tensors / capacity / offsets as tci_tci2_sweep1site)
 int sweep2site_impl(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
-                    int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested, int fill, int* filled) {
+                    int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested, int fill, int* filled,
+                    const tci::SwSweep1* solve = nullptr) {
     if (!s || !f || niter < 0) return TCI_ERR_ARG;
     if (filled) *filled = 0;
     const int L = s->L;
@@ -342,7 +344,8 @@ int sweep2site_impl(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1
         const std::vector<char> in = sw_pack(s);
         std::vector<char> out;
         int st = tci_sweep_small_run(s->ctx, f, L, sw_capacity(s), in.data(), in.size(), 0, fill ? 1 : 0, niter,
-                                     iter1, sweepstrategy, strictlynested, abstol, maxbonddim, out);
+                                     iter1, sweepstrategy, strictlynested, abstol, maxbonddim, out,
+                                     fill ? solve : nullptr);
         if (st) return st;
         so = sw_unpack(s, out, 0);
         if (so.status == 0) {
@@ -426,6 +429,15 @@ int tci_tci2_sweep2site_fill(tci_tci2* s, const tci_func* f, int32_t niter, int3
     return sweep2site_impl(s, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested, 1, filled);
 }
 
+int tci_tci2_sweep2site_fillsolve(tci_tci2* s, const tci_func* f, int32_t niter, int32_t iter1, double abstol,
+                                  int64_t maxbonddim, int32_t sweepstrategy, int32_t strictlynested,
+                                  double* tensors, int64_t capacity, int64_t* offsets, int* filled) {
+    if (!s || !filled || !tensors || !offsets || capacity < 0) return TCI_ERR_ARG;
+    for (int i = 0; i < 2 * s->L; ++i) offsets[i] = 0;
+    const tci::SwSweep1 sv{0, 1, 1e-14, capacity, offsets, tensors};
+    return sweep2site_impl(s, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested, 1, filled, &sv);
+}
+
 
 // sweep1site! (tensorci2.jl:659-725) in one launch of the device-resident sweep (mode 2) when every
 // bond fits the one-workgroup rrLU; *handled = 0 (state untouched) otherwise or on any error, and the
@@ -454,7 +466,7 @@ int tci_tci2_sweep1site(tci_tci2* s, const tci_func* f, int32_t forward, double 
     return TCI_OK;
 }
 
-int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) {
+int fill_impl(tci_tci2* s, const tci_func* f, int* handled, const tci::SwSweep1* solve) {
     if (!s || !f || !handled) return TCI_ERR_ARG;
     *handled = 0;
     if (!tci_sweep_small_ok(s->ctx, f, s->L)) return TCI_OK;
@@ -462,7 +474,7 @@ int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) {
     std::vector<char> out;
     const double before = s->maxsample;
     int st = tci_sweep_small_run(s->ctx, f, s->L, sw_capacity(s), in.data(), in.size(), 1, 0, 0, 1, 0, 0, 0.0,
-                                 0, out);
+                                 0, out, solve);
     if (st) return st;
     const SwOut so = sw_unpack(s, out, 1);
     if (so.fstatus != 0) {  // the caller's loop reports it / evaluates the large site
@@ -471,6 +483,16 @@ int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) {
     }
     *handled = 1;
     return TCI_OK;
+}
+
+int tci_tci2_fill_maxsample(tci_tci2* s, const tci_func* f, int* handled) { return fill_impl(s, f, handled, nullptr); }
+
+int tci_tci2_fill_solve(tci_tci2* s, const tci_func* f, double* tensors, int64_t capacity, int64_t* offsets,
+                        int* handled) {
+    if (!s || !tensors || !offsets || capacity < 0) return TCI_ERR_ARG;
+    for (int i = 0; i < 2 * s->L; ++i) offsets[i] = 0;
+    const tci::SwSweep1 sv{0, 1, 1e-14, capacity, offsets, tensors};
+    return fill_impl(s, f, handled, &sv);
 }
 
 }  // extern "C"

@@ -690,6 +690,104 @@ __device__ __forceinline__ int sw_lu_wave_any(double* S, int ldS, int m, int n, 
 // current = slot 0, history = slot 1.
 __device__ __forceinline__ int sw_other(int h, int e) { return h != e ? 3 - h - e : (h + 1) % 3; }
 
+// ---- setsitetensor!'s solve (tensorci2.jl:620-627): T = transpose(transpose(P) \ transpose(Pi1)),
+// LAPACK getrf / getrs of P^T with partial pivoting, each element's operations in the order of the
+// oracle's restatement (oracle/tci_oracle.c orc_sitetensor_solve).
+// getrf of A = P^T (r x r, ld r, LDS; r <= 64) by one wave, lane i owning row i: per column k the
+// first maximal |a| at or below the diagonal (a NaN on the diagonal keeps k; NaNs below never win,
+// as the oracle's strict '>' scan), the interchange of whole rows, the column divided by the pivot,
+// the rank-1 update (a separate multiply and subtract). piv[k] (LDS): the row swapped with k.
+__device__ void sw_getrf_wave(double* A, int r, int* piv) {
+    const int i = threadIdx.x & 63;
+    for (int k = 0; k < r; ++k) {
+        const double v = (i >= k && i < r) ? fabs(A[i + k * r]) : -1.0;
+        const double vk = readlane_f64(v, k);
+        int p = k;
+        if (!isnan(vk)) {
+            double bv = (i >= k && i < r && !isnan(v)) ? v : -1.0, bx = 0.0;
+            unsigned bk = (unsigned)i;
+            wave_best(bv, bk, bx);  // the largest |a|, then the smallest row
+            p = (int)bk;
+        }
+        if (i == 0) piv[k] = p;
+        if (p != k && i < r) {  // lane i: column i of rows k and p
+            const double t = A[k + i * r];
+            A[k + i * r] = A[p + i * r];
+            A[p + i * r] = t;
+        }
+        wave_sync();
+        const double d = A[k + k * r];
+        if (i > k && i < r) {
+            const double l = A[i + k * r] / d;
+            A[i + k * r] = l;
+            for (int j = k + 1; j < r; ++j) A[i + j * r] = __dsub_rn(A[i + j * r], __dmul_rn(l, A[k + j * r]));
+        }
+        wave_sync();
+    }
+}
+
+// getrs with the factors of sw_getrf_wave: every right-hand side c (a row of Pi1, R x r, ld R, in
+// place -- it becomes the row of T) by one thread: the interchanges, the unit lower solve, the upper
+// solve with true division. RB >= r: the solution vector in registers (constant indices: the
+// interchanges as selects); RB = 0: in LDS (r > 32).
+template <int RB>
+__device__ void sw_getrs_rows(double* X, int R, int r, const double* A, const int* piv) {
+    for (int c = threadIdx.x; c < R; c += kSwThreads) {
+        double* x = X + c;
+        if constexpr (RB > 0) {
+            double v[RB];
+#pragma unroll
+            for (int i = 0; i < RB; ++i) v[i] = i < r ? x[(int64_t)i * R] : 0.0;
+#pragma unroll
+            for (int k = 0; k < RB; ++k) {
+                if (k >= r) break;
+                const int pk = piv[k];
+#pragma unroll
+                for (int i = k + 1; i < RB; ++i)
+                    if (i == pk) {
+                        const double t = v[k];
+                        v[k] = v[i];
+                        v[i] = t;
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < RB; ++k) {
+                if (k >= r) break;
+#pragma unroll
+                for (int i = k + 1; i < RB; ++i)
+                    if (i < r) v[i] = __dsub_rn(v[i], __dmul_rn(A[i + k * r], v[k]));
+            }
+#pragma unroll
+            for (int k = RB - 1; k >= 0; --k) {
+                if (k >= r) continue;
+                v[k] = v[k] / A[k + k * r];
+#pragma unroll
+                for (int i = 0; i < RB; ++i)
+                    if (i < k) v[i] = __dsub_rn(v[i], __dmul_rn(A[i + k * r], v[k]));
+            }
+#pragma unroll
+            for (int i = 0; i < RB; ++i)
+                if (i < r) x[(int64_t)i * R] = v[i];
+        } else {
+            for (int k = 0; k < r; ++k)
+                if (piv[k] != k) {
+                    const double t = x[(int64_t)k * R];
+                    x[(int64_t)k * R] = x[(int64_t)piv[k] * R];
+                    x[(int64_t)piv[k] * R] = t;
+                }
+            for (int k = 0; k < r; ++k) {
+                const double xk = x[(int64_t)k * R];
+                for (int i = k + 1; i < r; ++i) x[(int64_t)i * R] = __dsub_rn(x[(int64_t)i * R], __dmul_rn(A[i + k * r], xk));
+            }
+            for (int k = r - 1; k >= 0; --k) {
+                const double xk = x[(int64_t)k * R] / A[k + k * r];
+                x[(int64_t)k * R] = xk;
+                for (int i = 0; i < k; ++i) x[(int64_t)i * R] = __dsub_rn(x[(int64_t)i * R], __dmul_rn(A[i + k * r], xk));
+            }
+        }
+    }
+}
+
 template <int KIND>
 __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1239,8 +1337,15 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
         if (tid == 0) reinterpret_cast<int64_t*>(a.out)[10] = tused;
     }
     if ((a.mode == 1 || a.fill) && status == 0) {
-        // fillsitetensors!(tci, f) with the solve unobservable: updatemaxsample!(tci, Pi1) per site
+        // fillsitetensors!(tci, f) (globalsearch.jl:202-208): per site updatemaxsample!(tci, Pi1) and,
+        // with a.fsolve, setsitetensor!'s solve T = Pi1 P^-1 (tensorci2.jl:599-629) into a.tens as
+        // mode 2 stores its tensors ([site] (offset, count), then the data; header [10]: used).
+        // Without a.fsolve the solved tensors are unobservable (a later sweep overwrites them) and
+        // only the maxima are taken.
         fstatus = 0;
+        int64_t* ttab = reinterpret_cast<int64_t*>(a.tens);
+        double* tdat = a.tens + 2 * L;
+        int64_t tused = 0;
         for (int s = 0; s < L; ++s) {
             const int nI = set_cnt(0, 0, s), nJ = set_cnt(1, 0, s), d = ldm[s];
             if (s < L - 1 && set_cnt(0, 0, s + 1) != nJ) {
@@ -1253,6 +1358,66 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 fstatus = 5;  // too many states for LDS: the host evaluates it
                 fsite = s + 1;
                 break;
+            }
+            if (a.fsolve) {
+                const bool last = s == L - 1;
+                const int r = nJ;
+                const int64_t nT = (int64_t)R * r;
+                if (nT + (last ? 0 : (int64_t)r * r) > kSmallElems || (int64_t)R + r > kSmallPerm || r > 64 ||
+                    tused + nT > a.tcap) {
+                    fstatus = 5;  // the host redoes the fill
+                    fsite = s + 1;
+                    break;
+                }
+                double* Pi1 = S;       // R x r, ld R: T in place after the solve
+                double* Pt = S + nT;   // P^T, r x r
+                St* rs = reinterpret_cast<St*>(xy);
+                St* cs = rs + R;
+                const int wI = s, wJ = L - 1 - s;
+                const int32_t* Ib = set_ptr(0, 0, s);
+                const int32_t* Jb = set_ptr(1, 0, s);
+                for (int q = tid; q < R; q += kSwThreads) rs[q] = leg_state(f, Ib + (q % nI) * wI, wI, 0, q / nI + 1);
+                for (int j = tid; j < r; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, s + 1, 0);
+                __syncthreads();
+                double mx = 0.0;
+#pragma unroll 1
+                for (int64_t e = tid; e < nT; e += kSwThreads) {
+                    const double v = combine<KIND>(p, p0, rs[e % R], cs[e / R], wJ, L, nullptr, 0);
+                    Pi1[e] = v;
+                    const double av = fabs(v);
+                    mx = (isnan(av) || av > mx) ? av : mx;
+                }
+                mx = sw_maxabs(mx, &mxs);  // (its barriers order the states' reuse below)
+                maxsample = jl_max(fabs(maxsample), fabs(mx));
+                if (!last) {
+                    // P = f(Iset[s + 1] x Jset[s]) (the same column legs), stored transposed
+                    const int32_t* In = set_ptr(0, 0, s + 1);
+                    for (int q = tid; q < r; q += kSwThreads) rs[q] = leg_state(f, In + q * (s + 1), s + 1, 0, 0);
+                    __syncthreads();
+#pragma unroll 1
+                    for (int e = tid; e < r * r; e += kSwThreads) {
+                        const int q = e % r, j = e / r;  // P[q][j] -> Pt[j + q r]
+                        Pt[j + q * r] = combine<KIND>(p, p0, rs[q], cs[j], wJ, L, nullptr, 0);
+                    }
+                    __syncthreads();
+                    if (tid < 64) sw_getrf_wave(Pt, r, perm);
+                    __syncthreads();
+                    if (r <= 16)
+                        sw_getrs_rows<16>(Pi1, R, r, Pt, perm);
+                    else if (r <= 32)
+                        sw_getrs_rows<32>(Pi1, R, r, Pt, perm);
+                    else
+                        sw_getrs_rows<0>(Pi1, R, r, Pt, perm);
+                    __syncthreads();
+                }
+                for (int64_t e = tid; e < nT; e += kSwThreads) tdat[tused + e] = Pi1[e];
+                if (tid == 0) {
+                    ttab[2 * s] = tused;
+                    ttab[2 * s + 1] = nT;
+                }
+                tused += nT;
+                __syncthreads();
+                continue;
             }
             St* rs = reinterpret_cast<St*>(S);
             St* cs = rs + R;
@@ -1272,6 +1437,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
             mx = sw_maxabs(mx, &mxs);
             maxsample = jl_max(fabs(maxsample), fabs(mx));
         }
+        if (a.fsolve && tid == 0) reinterpret_cast<int64_t*>(a.out)[10] = fstatus == 0 ? tused : -1;
     }
     __syncthreads();
 

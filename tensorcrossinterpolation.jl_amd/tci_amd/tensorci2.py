@@ -348,11 +348,11 @@ class TensorCI2:
         self.invalidatesitetensors()
         n = len(self)
         if native is not False and NATIVE_SWEEP and _native_ok(f) and fillsitetensors:
-            # with lazy site tensors (solve unobservable) fillsitetensors! is only updatemaxsample!
-            # over every site's Pi1: the native object does it on the device in the same call
-            # sequence when it can (tci_tci2_fill_maxsample)
+            # fillsitetensors! in the same device launch when it can: with the solves (the
+            # reference's work, tci_tci2_sweep2site_fillsolve) or, lazy, only updatemaxsample! over
+            # every site's Pi1 (tci_tci2_sweep2site_fill)
             done = self._sweep2site_native(f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
-                                           fill_maxsample=lazy_sitetensors)
+                                           fill="max" if lazy_sitetensors else "solve")
             if not done:
                 self.fillsitetensors(f, solve=not lazy_sitetensors)
             return
@@ -418,29 +418,45 @@ class TensorCI2:
         return True
 
     def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
-                           fill_maxsample=False):
+                           fill=None):
         """The iterations in C++ / on the device (tci_tci2_sweep2site): the state goes in and comes
-        back bank by bank (a few ABI calls, not one per set). Returns whether fillsitetensors!'s
-        maxsample update was done natively too (fill_maxsample and tci_tci2_fill_maxsample handled it)."""
+        back bank by bank (a few ABI calls, not one per set). fill: None, "max" (fillsitetensors!'s
+        maxsample update only) or "solve" (fillsitetensors! with every site tensor solved, the
+        reference's work). Returns whether that fill was done natively too."""
         ctx = f.ctx
         lib = ctx.lib
         h = self._native_handle(ctx)
         self._native_push(ctx, h)
         strat = {"backandforth": 0, "forward": 1, "backward": 2}[sweepstrategy]
         handled = C.c_int(0)
+        mb = int(min(maxbonddim, INT64_MAX))
+        n = len(self)
+        if fill == "solve":
+            cap = n * 16384  # each site's tensor fits the small path's LDS
+            tens = np.empty(cap)
+            offs = np.zeros(2 * n, np.int64)
+            tp, op = tens.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p)
         with self._native_failure_sync(ctx, h, hist=niter > 0):
-            if fill_maxsample and niter > 0:
-                ctx.check(lib.tci_tci2_sweep2site_fill(h, f.h, int(niter), int(iter1), float(abstol),
-                                                       int(min(maxbonddim, INT64_MAX)), strat,
+            if fill == "max" and niter > 0:
+                ctx.check(lib.tci_tci2_sweep2site_fill(h, f.h, int(niter), int(iter1), float(abstol), mb, strat,
                                                        int(bool(strictlynested)), C.byref(handled)))
+            elif fill == "solve" and niter > 0:
+                ctx.check(lib.tci_tci2_sweep2site_fillsolve(h, f.h, int(niter), int(iter1), float(abstol), mb, strat,
+                                                            int(bool(strictlynested)), tp, cap, op, C.byref(handled)))
             else:
-                ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol),
-                                                  int(min(maxbonddim, INT64_MAX)), strat, int(bool(strictlynested))))
-                if fill_maxsample:
+                ctx.check(lib.tci_tci2_sweep2site(h, f.h, int(niter), int(iter1), float(abstol), mb, strat,
+                                                  int(bool(strictlynested))))
+                if fill == "max":
                     ctx.check(lib.tci_tci2_fill_maxsample(h, f.h, C.byref(handled)))
+                elif fill == "solve":
+                    ctx.check(lib.tci_tci2_fill_solve(h, f.h, tp, cap, op, C.byref(handled)))
         if niter > 0:
             self._native_has_hist = True  # every iteration starts a history
         self._native_pull(ctx, h)
+        if fill == "solve" and handled.value:
+            for p in range(n):
+                o, c = int(offs[2 * p]), int(offs[2 * p + 1])
+                self.setsitetensor_(p + 1, tens[o:o + c].copy())
         return bool(handled.value)
 
     @contextlib.contextmanager

@@ -131,12 +131,69 @@ def test_fill_maxsample_native_equals_loop():
     h = tci._native_h
     lib = ctx.lib
     # push the current state, run the native fill, compare with the Python loop
-    tci._sweep2site_native(f, 0, 1, 1e-8, TT.INT64_MAX, "backandforth", False, fill_maxsample=True)
+    tci._sweep2site_native(f, 0, 1, 1e-8, TT.INT64_MAX, "backandforth", False, fill="max")
     native = tci.maxsamplevalue
     tci.maxsamplevalue = 0.0
     tci.fillsitetensors(f, solve=False)
     assert native == tci.maxsamplevalue and native > 0.0
     assert h is not None and lib is not None
+
+
+@pytest.mark.parametrize("name", ["lorentz", "qosc40", "table", "gauss20", "qexp30", "sum"])
+def test_fill_solve_native_equals_oracle_solve(name):
+    """fillsitetensors! with the solves (globalsearch.jl:202-208, setsitetensor! tensorci2.jl:599-629)
+    in one device launch (tci_tci2_fill_solve): maxsamplevalue bitwise the per-site loop's; every
+    site tensor T = Pi1 P^-1 bitwise the oracle's getrf / getrs restatement (orc_sitetensor_solve) on
+    the same Pi1 and P (the kernel keeps its operation order), and within rtol 1e-10 of the host
+    loop's device solve (tci_sitetensor_h, K5: blocked, its own summation order)."""
+    ctx = T.context(0)
+    mk, ld, kw = CASES[name]
+    f = mk(ctx)
+    kw = dict(kw, maxiter=2)
+    kw.pop("sweepstrategy", None)
+    tci, _, _ = T.crossinterpolate2(f, ld, [T.optfirstpivot(f, ld)], nsearchglobalpivot=0, **kw)
+    tci.maxsamplevalue = 0.0
+    assert tci._sweep2site_native(f, 0, 1, 1e-8, TT.INT64_MAX, "backandforth", False, fill="solve")
+    native_ms = tci.maxsamplevalue
+    native_T = [t.copy() for t in tci.sitetensors]
+    tci.maxsamplevalue = 0.0
+    tci.fillsitetensors(f, solve=True)  # the host loop (tci_sitetensor_h per site)
+    assert native_ms == tci.maxsamplevalue and native_ms > 0.0
+    L = len(ld)
+    for p in range(L):
+        Ib, Jb = tci.Iset[p], tci.Jset[p]
+        Pi1 = f.pi(Ib, Jb, 1)[0].reshape((len(Ib) * ld[p], len(Jb)), order="F")
+        if p < L - 1:
+            P = f.pi(tci.Iset[p + 1], Jb, 0)[0]
+            ref = O.sitetensor_solve(P, Pi1)
+        else:
+            ref = Pi1
+        got = native_T[p].reshape(ref.shape, order="F")
+        assert np.array_equal(got, ref), (name, p)
+        host = tci.sitetensors[p].reshape(ref.shape, order="F")
+        assert np.allclose(got, host, rtol=1e-10, atol=1e-12 * native_ms), (name, p)
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_sweep2site_fill_solve_in_launch(lazy):
+    """crossinterpolate2 with the reference's work (fillsitetensors! solving every site tensor after
+    each sweep2site!, lazy=False: tci_tci2_sweep2site_fillsolve) and with the solves skipped
+    (lazy=True): identical ranks, errors, sets and final tensors; the device path equals the host
+    loop (tci_set_sweep_small 0) on ranks / errors / sets bit for bit."""
+    ctx = T.context(0)
+    ld = [2] * 30
+    f = T.quantics_osc(30, ctx=ctx)
+    p0 = [T.optfirstpivot(f, ld)]
+    out = []
+    for small in (1, 0):
+        ctx.check(ctx.lib.tci_set_sweep_small(ctx.h, small))
+        try:
+            out.append(T.crossinterpolate2(f, ld, p0, tolerance=1e-8, nsearchglobalpivot=0, lazy_sitetensors=lazy))
+        finally:
+            ctx.check(ctx.lib.tci_set_sweep_small(ctx.h, 1))
+    (t1, r1, e1), (t2, r2, e2) = out
+    assert r1 == r2 and list(e1) == list(e2)
+    _same(t1, t2)
 
 
 def test_bulk_set_transfer_roundtrip():
