@@ -34,14 +34,15 @@ def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1, pass0_a
     (the ones bench times), each over the (m-k-1) x (n-k-1) trailing block, following the host
     schedule of tci_abi.cpp rrlu_device. Exact passes: a read-only pass reads 8 B/element, every
     nb-th pass also writes 8 B/element back. With the certified shadow search (DESIGN.md K2;
-    sh_bytes = 2 for the fp16 shadow, 4 for fp32) a read-only pass streams the shadow instead; with
-    the fp16 shadow pass 0 is exact and writes the shadow of A (8 + 2), and the two-level epoch
-    ends every shadow epoch of nb pivots with a refresh (the shadow read and rewritten: 2 + 2) and
-    every epochs-th with a write-back (8 read + 8 + 2 written). The exact re-reads of candidate
+    sh_bytes = 1 for the 8-bit shadow, 2 for fp16, 4 for fp32) a read-only pass streams the shadow
+    instead; with the narrow shadows (1 or 2 B) pass 0 is exact and writes the shadow of A (8 + s),
+    and the two-level epoch ends every shadow epoch of nb pivots with a refresh (the shadow read and
+    rewritten: s + s) and every epochs-th with a write-back (8 read + 8 + s written). The exact re-reads of candidate
     elements and the pending x / y vectors are data-dependent / small and not counted.
     Returns (read_only, write_back, refresh) as (bytes, launches); with pass0_apart the exact pass 0
-    (fp16 shadow: 8 + 2 B/element) is left out of read_only and returned fourth."""
-    if not (shadow and sh_bytes == 2 and 2 <= nb <= 15):
+    (narrow shadow: 8 + s B/element) is left out of read_only and returned fourth."""
+    narrow = shadow and sh_bytes in (1, 2)  # the scaled narrow shadows (8-bit, fp16): two-level epoch
+    if not (narrow and 2 <= nb <= 15):
         epochs = 1
     epochs = max(1, min(epochs, 32 // nb))
     nbx = nb * epochs
@@ -67,11 +68,11 @@ def pass_bytes(m, n, r, nb, stride=1, shadow=True, sh_bytes=2, epochs=1, pass0_a
         elif refresh:
             rf_b += 2.0 * sh_bytes * elems
             rf_n += 1
-        elif shadow and sh_bytes == 2 and k == 0 and pass0_apart:
+        elif narrow and k == 0 and pass0_apart:
             p0_b += (8.0 + sh_bytes) * elems
             p0_n += 1
         else:
-            ro_b += (8.0 + sh_bytes if (shadow and sh_bytes == 2 and k == 0) else ro_per) * elems
+            ro_b += (8.0 + sh_bytes if (narrow and k == 0) else ro_per) * elems
             ro_n += 1
     if pass0_apart:
         return (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n), (p0_b, p0_n)
@@ -109,7 +110,7 @@ def main():
                     help="shadow epochs per fp64 write-back (two-level epoch; identical results; "
                          "0 = the library's choice by shape)")
     ap.add_argument("--no-shadow", action="store_true",
-                    help="exact fp64 read-only passes instead of the certified fp16 shadow search")
+                    help="exact fp64 read-only passes instead of the certified narrow-shadow search")
     args = ap.parse_args()
     # the result is ONE JSON line on stdout: native libraries' banners (RCCL prints its version
     # block to fd 1 when the sharded extras create a communicator) go to stderr instead
@@ -212,9 +213,9 @@ def main():
     if ro_n > 0 and ro_ms >= wb_ms:
         dom_key = "rrlu_read_only_pass"
         dom, dom_ms, dom_launches, dom_bytes, dom_n = (
-            (("k_pass_mf<P> (read-only: fp16 shadow streamed, pending updates applied by f16-split "
-              "MFMA with fp32 accumulation, certified abs2 argmax with exact fp64 re-reads of "
-              "candidate elements)") if sh_bytes == 2 else
+            (("k_pass_mf<P> (read-only: " + ("8-bit" if sh_bytes == 1 else "fp16") + " shadow streamed, "
+              "pending updates applied by f16-split MFMA with fp32 accumulation, certified abs2 argmax "
+              "with exact fp64 re-reads of candidate elements)") if sh_bytes in (1, 2) else
              ("k_pass_sh<P> (read-only: fp32 shadow streamed, pending updates applied in fp32, "
               "certified abs2 argmax with exact fp64 re-reads of candidate chunks)")) if shadow else
             "k_pass2<P,false> (read-only: pending updates applied on the fly + abs2 argmax)",
@@ -247,7 +248,7 @@ def main():
              "pass0": {"launches": p0_launches, "avg_ms": round(p0_ms / max(p0_launches, 1), 5),
                        "GBps": round(p0_b / max(p0_n, 1) / (p0_ms / max(p0_launches, 1) * 1e-3) / 1e9, 1)
                        if p0_launches else None,
-                       "note": "the exact pass after pivot 0 (reads A, writes the fp16 shadow: 10 B/element); "
+                       "note": f"the exact pass after pivot 0 (reads A, writes the shadow: {8 + sh_bytes} B/element); "
                                "its own family, not in read_only_pass"},
              "refresh_pass": {"launches": rf_launches, "avg_ms": round(rf_ms / max(rf_launches, 1), 5),
                               "GBps": round(rf_b / max(rf_n, 1) / (rf_ms / max(rf_launches, 1) * 1e-3) / 1e9, 1)

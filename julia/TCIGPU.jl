@@ -367,6 +367,29 @@ function sweep1site_device!(tci::TensorCI2{Float64}, f::GPUBatchEvaluator, sweep
     return true
 end
 
+# fillsitetensors! (globalsearch.jl:202-208) with every site tensor solved (setsitetensor!,
+# tensorci2.jl:599-629) in one device launch; false when the device path cannot take it
+function fillsitetensors_device!(tci::TensorCI2{Float64}, f::GPUBatchEvaluator)
+    s = DeviceState(f.ctx, tci.localdims)
+    push_sets!(f.ctx, s, tci)
+    tens = Vector{Float64}(undef, length(tci) * 16384)
+    offs = zeros(Int64, 2 * length(tci))
+    handled = Ref{Cint}(0)
+    check(f.ctx, ccall((:tci_tci2_fill_solve, libtci), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}, Int64, Ptr{Int64}, Ref{Cint}),
+        s.h, f.h, tens, length(tens), offs, handled))
+    handled[] == 1 || return false
+    ms = Ref(0.0)
+    check(f.ctx, ccall((:tci_tci2_errors, libtci), Cint, (Ptr{Cvoid}, Ref{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Int64}),
+                       s.h, ms, C_NULL, C_NULL, 0, C_NULL))
+    tci.maxsamplevalue = ms[]
+    for p in 1:length(tci)
+        o, len = offs[2p-1], offs[2p]
+        tci.sitetensors[p] = reshape(tens[o+1:o+len], length(tci.Iset[p]), tci.localdims[p], :)
+    end
+    return true
+end
+
 # ------------------------------------------------------------------ rrLU / MatrixLUCI
 # rrlu(A; ...) (matrixlu.jl:455-463) for Float64 and ComplexF64 (interleaved, Julia's own layout)
 function device_rrlu(A::Matrix{Float64}; maxrank::Int=typemax(Int), reltol::Number=1e-14,

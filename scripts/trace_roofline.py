@@ -4,11 +4,12 @@ Usage: python scripts/trace_roofline.py KERNEL_STATS_CSV OUT_JSON [--m 8192 --n 
 
 Sorts the rrLU kernels of the traced bench command into families -- the initial argmax (k_pass2<0>,
 one per factorisation, so it counts the factorisations), pass 0 (k_pass2<1,false,true>: reads A,
-writes the fp16 shadow), the read-only passes (per-pass k_pass_mf<P,EXT,false> launches and the
+writes the shadow), the read-only passes (per-pass k_pass_mf<P,EXT,false> launches and the
 persistent k_pass_mf_epoch launches, which run several passes each), refreshes, write-backs -- and
 prices the read-only passes by the kernel trace alone: their total device time / the number of
 read-only passes the schedule (bench.pass_bytes) gives per factorisation x the factorisations, against
-the algorithmic bytes of those passes (2 B of fp16 shadow per trailing element). This is
+the algorithmic bytes of those passes (--sh-bytes per trailing element: 1 for the 8-bit shadow of the
+default build, 2 for fp16). This is
 the rocprof counterpart of bench.py's HIP-event `roofline.frac`; bench.py reports it beside that one.
 """
 import argparse
@@ -51,6 +52,7 @@ def main():
     ap.add_argument("--r", type=int, default=256)
     ap.add_argument("--nb", type=int, default=10)
     ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--sh-bytes", type=int, default=1)
     a = ap.parse_args()
     import bench
     fam = {}
@@ -65,7 +67,7 @@ def main():
             "calls": int(row["Calls"]), "avg_us": round(float(row["AverageNs"]) * 1e-3, 2)}
     nfact = fam.get("initial_argmax", {}).get("launches", 0)
     (ro_b, ro_n), (wb_b, wb_n), (rf_b, rf_n), (p0_b, p0_n) = bench.pass_bytes(
-        a.m, a.n, a.r, a.nb, 1, True, 2, a.epochs, pass0_apart=True)
+        a.m, a.n, a.r, a.nb, 1, True, a.sh_bytes, a.epochs, pass0_apart=True)
     ro_us = sum(fam.get(f, {}).get("total_us", 0.0) for f in ("read_only_per_pass", "read_only_persistent"))
     passes = ro_n * nfact
     out = {"source": os.path.relpath(a.stats), "config": vars(a), "factorisations": nfact, "families": fam}

@@ -88,6 +88,11 @@ struct tci_ctx {
     size_t capSwOut = 0;
     double* sw_tens = nullptr;  // sweep1site's site tensors (device)
     size_t capSwTens = 0;
+    int32_t* sw_fmap = nullptr;  // the fill's map of the current sets (device; k_fill_sites)
+    size_t capSwFmap = 0;
+    char* sw_fmax = nullptr;     // the fill's per-site max |Pi1| bits (mapped host memory)
+    char* sw_fmax_d = nullptr;
+    size_t capSwFmax = 0;
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
@@ -1154,7 +1159,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->ev_ina) hipEventDestroy(c->ev_ina);
     if (c->hout) hipHostFree(c->hout);
     if (c->zbuf) hipHostFree(c->zbuf);
-    fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens);
+    fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens); fr(c->sw_fmap);
     if (c->sw_in) hipHostFree(c->sw_in);
     if (c->sw_out) hipHostFree(c->sw_out);
     if (c->hfn) hipHostFree(c->hfn);
@@ -2844,9 +2849,27 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
         a.tens = c->sw_tens;
         a.tcap = s1->tcap;
     }
+    // the fill (mode 0 with fill, mode 1): k_sweep_small checks and maps the sets, then
+    // k_fill_sites evaluates every site in parallel (one workgroup per site)
+    const bool filling = (mode == 0 && fill) || mode == 1;
+    if (filling) {
+        if ((st = ensure(c, &c->sw_fmap, &c->capSwFmap, (size_t)(4 * L + 4)))) return st;
+        if ((st = ensure_mapped_pair(c, &c->sw_fmax, &c->sw_fmax_d, &c->capSwFmax, (size_t)L * 8))) return st;
+        a.fmap = c->sw_fmap;
+    }
     HIPCHK(c, tci::launch_sweep_small(c->stream, a));
+    if (filling)
+        HIPCHK(c, tci::launch_fill_sites(c->stream, a, reinterpret_cast<unsigned long long*>(c->sw_fmax_d)));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t* hdr = reinterpret_cast<const int64_t*>(c->sw_out);
+    if (filling && hdr[0] == 0 && hdr[8] == 0) {
+        // updatemaxsample! over the sites: max of |Pi1| bits (Julia's NaN-propagating max, order-free
+        // on non-negative values) folded into the header's maxsample
+        unsigned long long b = (unsigned long long)reinterpret_cast<const int64_t*>(c->sw_out)[6] & 0x7fffffffffffffffull;
+        const unsigned long long* fm = reinterpret_cast<const unsigned long long*>(c->sw_fmax);
+        for (int q = 0; q < L; ++q) b = std::max(b, fm[q]);
+        reinterpret_cast<int64_t*>(c->sw_out)[6] = (int64_t)b;
+    }
     const int64_t* cn = reinterpret_cast<const int64_t*>(c->sw_out + io.counts);
     size_t bytes = io.sets;
     const int nb = (hdr[0] == 1 && hdr[4]) ? 6 : 4;

@@ -417,6 +417,9 @@ struct SweepSmallArgs {
                            // 2: sweep1site! (s1fwd, s1tens, reltol below)
     int fill;              // mode 0: the maxsample update after the iterations too (header [8] / [9])
     int fsolve = 0;        // modes 0 (fill) / 1: also setsitetensor!'s solve, the tensors into tens / tcap
+    int32_t* fmap = nullptr;  // modes 0 (fill) / 1: the per-site work of the fill is left to k_fill_sites
+                              // (one workgroup per site): [0] ok flag, then per site (bank of Iset[s],
+                              // bank of Jset[s], nI, nJ); the tensors' table entries written here
     int s1fwd, s1tens;     // mode 2: forward sweep; site tensors (MatrixLUCI factors) wanted
     double reltol;         // mode 2: the rrLU's reltol
     double* tens;          // mode 2 / fsolve: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
@@ -434,5 +437,9 @@ struct SwSweep1 {
 bool sweep_small_kind(int kind);
 size_t sweep_small_lds_bytes();
 hipError_t launch_sweep_small(hipStream_t s, const SweepSmallArgs& a);
+// fillsitetensors! after k_sweep_small (modes 0 with fill / 1): every site's Pi1 (max |Pi1| into
+// fmax[s] as |v| bits, Julia's NaN-propagating max) and, with a.fsolve, P and T = Pi1 P^-1 into the
+// table entries k_sweep_small wrote -- one workgroup per site, all sites at once
+hipError_t launch_fill_sites(hipStream_t s, const SweepSmallArgs& a, unsigned long long* fmax);
 
 }  // namespace tci

@@ -294,6 +294,7 @@ __device__ __forceinline__ CandR load_cand_sc1(const Cand* src) {
 __device__ unsigned long long g_pprof[kMaxPassGrid * 8 + 8];
 __device__ unsigned long long g_pprof_x[kMaxPassGrid * 4];  // thread 0's prologue sub-phases (k_pass_mf)
 __shared__ unsigned g_exam_lds;  // exact examinations of this workgroup (k_pass_mf)
+__device__ unsigned g_cert_fails;  // read-only / refresh passes whose certificate failed (exact body ran)
 #define PPROF(i) (pt[i] = wall_clock64())
 #define PPROFX(i)                                                                                   \
     do {                                                                                            \
@@ -464,6 +465,17 @@ __device__ __forceinline__ void pass_tail(CandR best, const SelArgs& sel, Cand* 
         unsigned long long* gp = g_pprof;
         const unsigned long long prev5 = gp[kMaxPassGrid * 8];
         gp[kMaxPassGrid * 8] = pt[5];
+#ifdef TCI_EXAM_CENSUS
+        {  // every pass: the grid's exact examinations (k_pass_mf; 0 for the exact bodies) and the
+           // running count of certificate failures -- one line per pass
+            unsigned long long tot = 0;
+            if (!flush)
+                for (int i = 0; i < (int)gridDim.x; ++i)
+                    tot += __hip_atomic_load(&gp[i * 8 + 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            printf("[census k=%d P=%d flush=%d grid=%d] exams %llu cert_fails %u\n", sel.selk, P, flush, (int)gridDim.x,
+                   tot, __hip_atomic_load(&g_cert_fails, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+#endif
         if (sel.selk == TCI_PASS_PROF || sel.selk == TCI_PASS_PROF + 1) {
             unsigned long long t0min = ~0ull, t0max = 0, t3max = 0, t3min = ~0ull;
             double s01 = 0, s12 = 0, s23 = 0, s06 = 0, s61 = 0, s17 = 0, s72 = 0;
@@ -2530,6 +2542,10 @@ __global__ __launch_bounds__(kP2Threads) void k_pass_mf(PassK g, SelArgs sel) {
     CandR best = cand_none();
     const int r = pass_mf_body<P, EXT, RF>(g, sel, L.f, best, pt, RT ? g.ps : P);
     bool go = r == kMfDone;
+#if TCI_PASS_PROF
+    if (r == kMfExact && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_cert_fails, 1u);
+    if (r != kMfDone && threadIdx.x == 0) g_exam_lds = 0;  // (the exact bodies examine everything)
+#endif
     if (r == kMfExact) {  // uniform: every workgroup derives the same certificate
         if constexpr (RF)
             go = passx_body<2>(g, sel, L.px, best, pt);

@@ -738,10 +738,10 @@ __device__ void sw_getrs_rows(double* X, int R, int r, const double* A, const in
             double v[RB];
 #pragma unroll
             for (int i = 0; i < RB; ++i) v[i] = i < r ? x[(int64_t)i * R] : 0.0;
+            // (guards instead of break / continue: the loops must unroll for v[] to stay in registers)
 #pragma unroll
             for (int k = 0; k < RB; ++k) {
-                if (k >= r) break;
-                const int pk = piv[k];
+                const int pk = k < r ? piv[k] : k;
 #pragma unroll
                 for (int i = k + 1; i < RB; ++i)
                     if (i == pk) {
@@ -752,18 +752,18 @@ __device__ void sw_getrs_rows(double* X, int R, int r, const double* A, const in
             }
 #pragma unroll
             for (int k = 0; k < RB; ++k) {
-                if (k >= r) break;
 #pragma unroll
                 for (int i = k + 1; i < RB; ++i)
                     if (i < r) v[i] = __dsub_rn(v[i], __dmul_rn(A[i + k * r], v[k]));
             }
 #pragma unroll
             for (int k = RB - 1; k >= 0; --k) {
-                if (k >= r) continue;
-                v[k] = v[k] / A[k + k * r];
+                if (k < r) {
+                    v[k] = v[k] / A[k + k * r];
 #pragma unroll
-                for (int i = 0; i < RB; ++i)
-                    if (i < k) v[i] = __dsub_rn(v[i], __dmul_rn(A[i + k * r], v[k]));
+                    for (int i = 0; i < RB; ++i)
+                        if (i < k) v[i] = __dsub_rn(v[i], __dmul_rn(A[i + k * r], v[k]));
+                }
             }
 #pragma unroll
             for (int i = 0; i < RB; ++i)
@@ -1337,14 +1337,12 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
         if (tid == 0) reinterpret_cast<int64_t*>(a.out)[10] = tused;
     }
     if ((a.mode == 1 || a.fill) && status == 0) {
-        // fillsitetensors!(tci, f) (globalsearch.jl:202-208): per site updatemaxsample!(tci, Pi1) and,
-        // with a.fsolve, setsitetensor!'s solve T = Pi1 P^-1 (tensorci2.jl:599-629) into a.tens as
-        // mode 2 stores its tensors ([site] (offset, count), then the data; header [10]: used).
-        // Without a.fsolve the solved tensors are unobservable (a later sweep overwrites them) and
-        // only the maxima are taken.
+        // fillsitetensors!(tci, f) (globalsearch.jl:202-208): the checks here -- the pivot matrices
+        // square ("Pivot matrix at bond b is not square!", fstatus 4), every site within one
+        // workgroup's LDS (else fstatus 5: the host loop runs the fill) -- and the map of the
+        // current sets for k_fill_sites, which evaluates every site's Pi1 (updatemaxsample!) and, with
+        // a.fsolve, setsitetensor!'s solve T = Pi1 P^-1 (tensorci2.jl:599-629), one workgroup per site
         fstatus = 0;
-        int64_t* ttab = reinterpret_cast<int64_t*>(a.tens);
-        double* tdat = a.tens + 2 * L;
         int64_t tused = 0;
         for (int s = 0; s < L; ++s) {
             const int nI = set_cnt(0, 0, s), nJ = set_cnt(1, 0, s), d = ldm[s];
@@ -1353,91 +1351,34 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 fsite = s + 1;
                 break;
             }
-            const int R = nI * d;
-            if ((int64_t)R + nJ > kSmallElems) {
-                fstatus = 5;  // too many states for LDS: the host evaluates it
+            const int64_t R = (int64_t)nI * d, nT = R * nJ;
+            const bool fits = a.fsolve ? (nT + (s == L - 1 ? 0 : (int64_t)nJ * nJ) <= kSmallElems &&
+                                          R + nJ <= kSmallPerm && nJ <= 64 && tused + nT <= a.tcap)
+                                       : R + nJ <= kSmallPerm;
+            if (!fits) {
+                fstatus = 5;  // the host evaluates it
                 fsite = s + 1;
                 break;
             }
-            if (a.fsolve) {
-                const bool last = s == L - 1;
-                const int r = nJ;
-                const int64_t nT = (int64_t)R * r;
-                if (nT + (last ? 0 : (int64_t)r * r) > kSmallElems || (int64_t)R + r > kSmallPerm || r > 64 ||
-                    tused + nT > a.tcap) {
-                    fstatus = 5;  // the host redoes the fill
-                    fsite = s + 1;
-                    break;
+            if (tid == 0) {
+                int32_t* fm = a.fmap + 4 + 4 * s;
+                fm[0] = bank_of(0, 0, s);
+                fm[1] = bank_of(1, 0, s);
+                fm[2] = nI;
+                fm[3] = nJ;
+                if (a.fsolve) {
+                    reinterpret_cast<int64_t*>(a.tens)[2 * s] = tused;
+                    reinterpret_cast<int64_t*>(a.tens)[2 * s + 1] = nT;
                 }
-                double* Pi1 = S;       // R x r, ld R: T in place after the solve
-                double* Pt = S + nT;   // P^T, r x r
-                St* rs = reinterpret_cast<St*>(xy);
-                St* cs = rs + R;
-                const int wI = s, wJ = L - 1 - s;
-                const int32_t* Ib = set_ptr(0, 0, s);
-                const int32_t* Jb = set_ptr(1, 0, s);
-                for (int q = tid; q < R; q += kSwThreads) rs[q] = leg_state(f, Ib + (q % nI) * wI, wI, 0, q / nI + 1);
-                for (int j = tid; j < r; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, s + 1, 0);
-                __syncthreads();
-                double mx = 0.0;
-#pragma unroll 1
-                for (int64_t e = tid; e < nT; e += kSwThreads) {
-                    const double v = combine<KIND>(p, p0, rs[e % R], cs[e / R], wJ, L, nullptr, 0);
-                    Pi1[e] = v;
-                    const double av = fabs(v);
-                    mx = (isnan(av) || av > mx) ? av : mx;
-                }
-                mx = sw_maxabs(mx, &mxs);  // (its barriers order the states' reuse below)
-                maxsample = jl_max(fabs(maxsample), fabs(mx));
-                if (!last) {
-                    // P = f(Iset[s + 1] x Jset[s]) (the same column legs), stored transposed
-                    const int32_t* In = set_ptr(0, 0, s + 1);
-                    for (int q = tid; q < r; q += kSwThreads) rs[q] = leg_state(f, In + q * (s + 1), s + 1, 0, 0);
-                    __syncthreads();
-#pragma unroll 1
-                    for (int e = tid; e < r * r; e += kSwThreads) {
-                        const int q = e % r, j = e / r;  // P[q][j] -> Pt[j + q r]
-                        Pt[j + q * r] = combine<KIND>(p, p0, rs[q], cs[j], wJ, L, nullptr, 0);
-                    }
-                    __syncthreads();
-                    if (tid < 64) sw_getrf_wave(Pt, r, perm);
-                    __syncthreads();
-                    if (r <= 16)
-                        sw_getrs_rows<16>(Pi1, R, r, Pt, perm);
-                    else if (r <= 32)
-                        sw_getrs_rows<32>(Pi1, R, r, Pt, perm);
-                    else
-                        sw_getrs_rows<0>(Pi1, R, r, Pt, perm);
-                    __syncthreads();
-                }
-                for (int64_t e = tid; e < nT; e += kSwThreads) tdat[tused + e] = Pi1[e];
-                if (tid == 0) {
-                    ttab[2 * s] = tused;
-                    ttab[2 * s + 1] = nT;
-                }
-                tused += nT;
-                __syncthreads();
-                continue;
             }
-            St* rs = reinterpret_cast<St*>(S);
-            St* cs = rs + R;
-            const int wI = s, wJ = L - 1 - s;
-            const int32_t* Ib = set_ptr(0, 0, s);
-            const int32_t* Jb = set_ptr(1, 0, s);
-            for (int r = tid; r < R; r += kSwThreads) rs[r] = leg_state(f, Ib + (r % nI) * wI, wI, 0, r / nI + 1);
-            for (int j = tid; j < nJ; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, s + 1, 0);
-            __syncthreads();
-            double mx = 0.0;
-#pragma unroll 1
-            for (int64_t e = tid; e < (int64_t)R * nJ; e += kSwThreads) {
-                const double v = combine<KIND>(p, p0, rs[e % R], cs[e / R], wJ, L, nullptr, 0);
-                const double av = fabs(v);
-                mx = (isnan(av) || av > mx) ? av : mx;
-            }
-            mx = sw_maxabs(mx, &mxs);
-            maxsample = jl_max(fabs(maxsample), fabs(mx));
+            tused += a.fsolve ? nT : 0;
         }
-        if (a.fsolve && tid == 0) reinterpret_cast<int64_t*>(a.out)[10] = fstatus == 0 ? tused : -1;
+        if (tid == 0) {
+            a.fmap[0] = fstatus == 0 ? 1 : 0;
+            if (a.fsolve) reinterpret_cast<int64_t*>(a.out)[10] = fstatus == 0 ? tused : -1;
+        }
+    } else if (tid == 0 && a.fmap) {
+        a.fmap[0] = 0;  // (no fill: k_fill_sites does nothing)
     }
     __syncthreads();
 
@@ -1471,6 +1412,100 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
             [&](int i, int) { const int lb = i / L; return (const int32_t*)set_ptr(lb & 1, lb >> 1, i % L); },
             [&](int, int off) { return dst + off; });
     }
+}
+
+// fillsitetensors! for k_sweep_small's map, one workgroup per site (the sites are independent):
+// Pi1 = f(kronecker(Iset[s], d) x Jset[s]) with the assembly's arithmetic, max |Pi1| (fmax[s], |v|
+// bits), and with a.fsolve P = f(Iset[s + 1] x Jset[s]) stored transposed, getrf by one wave and
+// getrs per row of Pi1 (sw_getrf_wave / sw_getrs_rows: the oracle's operation order), T in place
+template <int KIND>
+__global__ __launch_bounds__(kSwThreads) void k_fill_sites(SweepSmallArgs a, unsigned long long* fmax) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* S = reinterpret_cast<double*>(smem);
+    int* piv = reinterpret_cast<int*>(smem + kSwLdsS);
+    St* rs = reinterpret_cast<St*>(smem + kSwLdsS + kSwLdsPerm);
+    __shared__ unsigned long long mxs;
+    if (a.fmap[0] != 1) return;  // the sweep stopped, or the fill did not fit (the host runs it)
+    const int tid = threadIdx.x, s = blockIdx.x, L = a.L;
+    const FuncDev& f = a.f;
+    const double* p = f.params;
+    const double p0 = (KIND == F_SUM || KIND == F_TABLE) ? 0.0 : p[0];
+    const int32_t* fm = a.fmap + 4 + 4 * s;
+    const int bI = fm[0], bJ = fm[1], nI = fm[2], nJ = fm[3];
+    const int d = f.localdims[s];
+    const int64_t half = (int64_t)L * (L - 1) / 2;
+    auto bank_ptr = [&](int bank, int site) -> const int32_t* {  // (k_sweep_small's layout)
+        const int64_t pre = (bank & 1) ? (int64_t)site * (L - 1) - (int64_t)site * (site - 1) / 2
+                                       : (int64_t)site * (site - 1) / 2;
+        return a.ws + a.cap * (bank * half + pre);
+    };
+    const int R = nI * d, r = nJ, wI = s, wJ = L - 1 - s;
+    const int64_t nT = (int64_t)R * r;
+    St* cs = rs + R;
+    const int32_t* Ib = bank_ptr(bI, s);
+    const int32_t* Jb = bank_ptr(bJ, s);
+    for (int q = tid; q < R; q += kSwThreads) rs[q] = leg_state(f, Ib + (q % nI) * wI, wI, 0, q / nI + 1);
+    for (int j = tid; j < r; j += kSwThreads) cs[j] = leg_state(f, Jb + j * wJ, wJ, s + 1, 0);
+    __syncthreads();
+    double mx = 0.0;
+    double* Pi1 = S;  // R x r, ld R (T in place after the solve)
+#pragma unroll 1
+    for (int64_t e = tid; e < nT; e += kSwThreads) {
+        const double v = combine<KIND>(p, p0, rs[e % R], cs[e / R], wJ, L, nullptr, 0);
+        if (a.fsolve) Pi1[e] = v;
+        const double av = fabs(v);
+        mx = (isnan(av) || av > mx) ? av : mx;
+    }
+    mx = sw_maxabs(mx, &mxs);
+    if (tid == 0) fmax[s] = (unsigned long long)__double_as_longlong(fabs(mx));
+    if (!a.fsolve) return;
+    if (s < L - 1) {
+        // P = f(Iset[s + 1] x Jset[s]) (the same column legs), stored transposed
+        double* Pt = S + nT;
+        const int32_t* In = bank_ptr(a.fmap[4 + 4 * (s + 1)], s + 1);
+        for (int q = tid; q < r; q += kSwThreads) rs[q] = leg_state(f, In + q * (s + 1), s + 1, 0, 0);
+        __syncthreads();
+#pragma unroll 1
+        for (int e = tid; e < r * r; e += kSwThreads) {
+            const int q = e % r, j = e / r;  // P[q][j] -> Pt[j + q r]
+            Pt[j + q * r] = combine<KIND>(p, p0, rs[q], cs[j], wJ, L, nullptr, 0);
+        }
+        __syncthreads();
+        if (tid < 64) sw_getrf_wave(Pt, r, piv);
+        __syncthreads();
+        if (r <= 16)
+            sw_getrs_rows<16>(Pi1, R, r, Pt, piv);
+        else if (r <= 32)
+            sw_getrs_rows<32>(Pi1, R, r, Pt, piv);
+        else
+            sw_getrs_rows<0>(Pi1, R, r, Pt, piv);
+        __syncthreads();
+    }
+    double* T = a.tens + 2 * L + reinterpret_cast<const int64_t*>(a.tens)[2 * s];
+    for (int64_t e = tid; e < nT; e += kSwThreads) T[e] = Pi1[e];
+}
+
+hipError_t launch_fill_sites(hipStream_t s, const SweepSmallArgs& a, unsigned long long* fmax) {
+    const void* fn = nullptr;
+    switch (a.f.kind) {
+    case F_SUM: fn = reinterpret_cast<const void*>(&k_fill_sites<F_SUM>); break;
+    case F_LORENTZ: fn = reinterpret_cast<const void*>(&k_fill_sites<F_LORENTZ>); break;
+    case F_TABLE: fn = reinterpret_cast<const void*>(&k_fill_sites<F_TABLE>); break;
+    case F_GAUSS: fn = reinterpret_cast<const void*>(&k_fill_sites<F_GAUSS>); break;
+    case F_QOSC: fn = reinterpret_cast<const void*>(&k_fill_sites<F_QOSC>); break;
+    case F_QEXP: fn = reinterpret_cast<const void*>(&k_fill_sites<F_QEXP>); break;
+    default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSwLds);
+    if (e != hipSuccess) return e;
+    switch (a.f.kind) {
+#define TCI_FS(K)                                                                                    \
+    case K: hipLaunchKernelGGL(k_fill_sites<K>, dim3(a.L), dim3(kSwThreads), kSwLds, s, a, fmax); break;
+        TCI_FS(F_SUM) TCI_FS(F_LORENTZ) TCI_FS(F_TABLE) TCI_FS(F_GAUSS) TCI_FS(F_QOSC) TCI_FS(F_QEXP)
+#undef TCI_FS
+    default: break;
+    }
+    return hipGetLastError();
 }
 
 size_t sweep_small_lds_bytes() { return kSwLds; }
