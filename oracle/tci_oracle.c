@@ -746,6 +746,41 @@ int orc_rrlu(const double* A, i64 m, i64 n, i64 maxrank, double reltol, double a
     return ORC_OK;
 }
 
+/* ----------------------------------------------------- shared-divisor division check
+ * Test support for the device's div_shared (tensorcrossinterpolation.jl_amd/csrc/tci_sweep_small.hip):
+ * y = 1 / p once, then q = x y, r = fma(-p, q, x), q' = fma(r, y, q) must equal x / p bit for bit
+ * (Markstein) for |x|, |p| in [2^-400, 2^400]. n random pairs (uniform exponents in a few ranges,
+ * significands near all-ones / all-zeros); returns the number of mismatches. */
+static uint64_t orc_xs(uint64_t* s) { *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17; return *s; }
+static double orc_bits_dbl(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
+i64 orc_div_shared_check(i64 n, uint64_t seed) {
+    uint64_t s = seed ? seed : 88172645463325252ull;
+    i64 bad = 0;
+    for (i64 i = 0; i < n; ++i) {
+        double x, p;
+        const int mode = (int)(i % 4);
+        uint64_t mx = orc_xs(&s) & 0xFFFFFFFFFFFFFull, mp = orc_xs(&s) & 0xFFFFFFFFFFFFFull;
+        int ex, ep;
+        if (mode >= 2) {  /* significands near all-ones or all-zeros */
+            mp = (orc_xs(&s) & 1) ? 0xFFFFFFFFFFFFFull - (orc_xs(&s) & 0xFF) : (orc_xs(&s) & 0xFF);
+            if (mode == 3) mx = (orc_xs(&s) & 1) ? 0xFFFFFFFFFFFFFull - (orc_xs(&s) & 0xFF) : (orc_xs(&s) & 0xFF);
+        }
+        const int span = mode == 1 ? 400 : 30;
+        ex = (int)(orc_xs(&s) % (uint64_t)(2 * span + 1)) - span;
+        ep = (int)(orc_xs(&s) % (uint64_t)(2 * span + 1)) - span;
+        if (mode == 1) { ex = ex < -399 ? -399 : ex; ep = ep < -399 ? -399 : ep; }
+        x = orc_bits_dbl(((uint64_t)(ex + 1023) << 52) | mx | ((orc_xs(&s) & 1) << 63));
+        p = orc_bits_dbl(((uint64_t)(ep + 1023) << 52) | mp | ((orc_xs(&s) & 1) << 63));
+        const double y = 1.0 / p;
+        const double q = x * y;
+        const double r = fma(-p, q, x);
+        const double q2 = fma(r, y, q);
+        const double t = x / p;
+        if (memcmp(&q2, &t, 8)) ++bad;
+    }
+    return bad;
+}
+
 /* ----------------------------------------------------- partial-pivot solve
  * Tmat = transpose(transpose(P) \ transpose(Pi1)) (tensorci2.jl:626): LAPACK getrf/getrs on
  * P^T with partial pivoting (first maximal |a| in the column, like idamax). P: r x r,

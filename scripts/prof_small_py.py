@@ -1,0 +1,40 @@
+"""Host-side profile of the small TCI2 configs (C3 gauss20d, C4 qosc40): cProfile of one
+crossinterpolate2 after a warm-up, the top functions by own time, and a per-phase wall split
+(the native sweep's ABI call vs the Python around it).
+
+  python scripts/prof_small_py.py [C3|C4]
+"""
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tensorcrossinterpolation.jl_amd"))
+
+import tci_amd as T  # noqa: E402
+
+which = sys.argv[1:] or ["C3", "C4"]
+cases = {}
+if "C4" in which:
+    fq = T.quantics_osc(40)
+    cases["C4"] = (fq, [2] * 40, [T.optfirstpivot(fq, [2] * 40)], dict(tolerance=1e-8, nsearchglobalpivot=0))
+if "C3" in which:
+    cases["C3"] = (T.gauss([16] * 20, 0.05, 8.5), [16] * 20, [[8] * 20],
+                   dict(tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0))
+for name, (f, ld, p0, kw) in cases.items():
+    for _ in range(3):
+        T.crossinterpolate2(f, ld, p0, **kw)
+    t0 = time.perf_counter()
+    T.crossinterpolate2(f, ld, p0, **kw)
+    wall = time.perf_counter() - t0
+    pr = cProfile.Profile()
+    pr.enable()
+    T.crossinterpolate2(f, ld, p0, **kw)
+    pr.disable()
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+    print(f"== {name}: wall {wall * 1e3:.3f} ms (unprofiled)")
+    print(s.getvalue())

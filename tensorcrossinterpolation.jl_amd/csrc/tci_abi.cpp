@@ -451,9 +451,14 @@ struct StopPoll {
 // trade pays where a write-back streams long, i.e. on large trailing blocks. Measured on MI355X
 // (profiles/r04_ab_epochs_shapes.jsonl, r = 256): 2048^2 / 4096^2 fastest at 1, 8192^2 / 16384^2 at
 // 3; the break-even (2 write-backs' 14 B/element saved ~ 20 EXT prologues) is near 2.4e7 elements.
+// Round 6, 8-bit shadow (refresh 1 + 1 B/element, read-only passes 1 B): the EXT passes' extra start-up
+// now weighs more against the write-backs they save, so the middle sizes prefer two shadow epochs
+// (profiles/r06_d2_sched_*.jsonl, r06_e2_sched_*.jsonl: 4096^2 fastest at 1 (6.40 vs 6.66 ms), 8192^2
+// at 2 (12.05 vs 12.32), 16384^2 2 ~ 3 (36.69 / 36.64), 32768^2 r = 1024 at 3 (508.7 vs 555.9)).
 int rrlu_epochs(const tci_ctx* c, int64_t m, int64_t n) {
     if (c->epochs > 0) return c->epochs;
-    return (double)m * (double)n >= 2.4e7 ? 3 : 1;
+    const double mn = (double)m * (double)n;
+    return mn >= 2.0e8 ? 3 : mn >= 2.4e7 ? 2 : 1;
 }
 
 // dsrc (optional): the input, ld ldsrc; dA is then the work matrix it is copied into (rrlu's copy,

@@ -508,6 +508,27 @@ __device__ int sw_lu_regs(double* S, int ldS, int m, int n, int mr, double relto
 // pivots and bits. The other waves wait at the closing barrier.
 constexpr int kSwWaveN = 64;
 
+// x / p for a divisor p shared by many x, bitwise the IEEE quotient: with y = RN(1 / p) computed
+// once, q = RN(x y), r = x - p q (exact, one fma) and RN(q + r y) is the correctly rounded x / p
+// (Markstein's theorem) while no intermediate is subnormal or overflows -- |x|, |p| in
+// [2^-400, 2^400], x != 0 (pok: the test on p, once per pivot); otherwise the true division. No
+// v_div_scale / v_div_fmas, hence no VCC chain: a lane's divisions overlap (the normalisation of a
+// pivot column was ~0.57 us of a C4 pivot's ~1.6 us). oracle/tci_oracle.c orc_div_shared_check
+// compares the sequence with x / p on random and edge-case operands (tests/test_oracle_kats.py).
+__device__ __forceinline__ bool div_shared_ok(double p) {
+    const double ap = fabs(p);
+    return ap >= 0x1p-400 && ap <= 0x1p400;
+}
+__device__ __forceinline__ double div_shared(double x, double p, double y, bool pok) {
+    const double ax = fabs(x);
+    if (pok && ax >= 0x1p-400 && ax <= 0x1p400) {  // (false for NaN and 0)
+        const double q = __dmul_rn(x, y);
+        const double r = __fma_rn(-p, q, x);
+        return __fma_rn(r, y, q);
+    }
+    return x / p;
+}
+
 template <int TILE>
 __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double reltol, double abstol, int leftorth,
                           int* rowphys, int* colphys, double* xv, double* yv, SmallCand* red, double* pvl,
@@ -586,6 +607,8 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
             // normalisation (true division) of the pivot column / row by their owners: lane column
             // pc mod 8 holds physical column pc in slot pc / 8 (uniform), lane row pr mod 8 row pr
             const double piv = val;
+            const bool pok = div_shared_ok(piv);
+            const double rpiv = 1.0 / piv;  // (uniform; used only when pok)
             const int bsel = pc >> 3, asel = pr >> 3;
             if (tc == (pc & 7)) {
 #pragma unroll
@@ -594,7 +617,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
 #pragma unroll
                         for (int a = 0; a < TILE; ++a)
                             if (rpos[a] > k) {
-                                const double x = leftorth ? v[a][b] / piv : v[a][b];
+                                const double x = leftorth ? div_shared(v[a][b], piv, rpiv, pok) : v[a][b];
                                 v[a][b] = x;
                                 xv[tr + 8 * a] = x;
                                 fl |= isnan(x) ? 1 : 0;
@@ -608,7 +631,7 @@ __device__ int sw_lu_wave(double* S, int ldS, int m, int n, int mr, double relto
 #pragma unroll
                         for (int b = 0; b < TILE; ++b)
                             if (cpos[b] > k) {
-                                const double y = leftorth ? v[a][b] : v[a][b] / piv;
+                                const double y = leftorth ? v[a][b] : div_shared(v[a][b], piv, rpiv, pok);
                                 v[a][b] = y;
                                 yv[tc + 8 * b] = y;
                                 fl |= isnan(y) ? 2 : 0;

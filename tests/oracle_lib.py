@@ -58,6 +58,8 @@ def _bind(path):
         L.orc_feval.argtypes = [C.c_int, f64p, C.c_int64, i32p, C.c_int, i32p]
         L.orc_feval.restype = C.c_double
         L.orc_sitetensor_solve.argtypes = [f64p, C.c_int64, f64p, C.c_int64, f64p]
+        L.orc_div_shared_check.argtypes = [C.c_int64, C.c_uint64]
+        L.orc_div_shared_check.restype = C.c_int64
         L.orc_convergencecriterion.argtypes = [i64p, f64p, i64p, C.c_int, C.c_double, C.c_int64,
                                                C.c_int, C.c_int]
         L.orc_tci_new.argtypes = [C.c_int, f64p, C.c_int64, i32p, C.c_int, i32p, C.c_int,

@@ -351,3 +351,12 @@ def test_omp_baseline_ties_and_nan():
             assert r1[0] == r2[0]
             assert np.array_equal(r1[2], r2[2]) and np.array_equal(r1[3], r2[3])
             assert np.array_equal(a1, a2, equal_nan=True)
+
+
+def test_shared_divisor_division_is_ieee():
+    """The device's div_shared (tci_sweep_small.hip, the one-wave bond rrLU's normalisation):
+    y = 1 / p once per pivot, then RN(q + (x - p q) y) with q = RN(x y) must be the IEEE quotient x / p
+    bit for bit in its domain (|x|, |p| in [2^-400, 2^400]) -- Markstein's theorem, checked on 2e7
+    random pairs incl. significands next to all-ones / all-zeros and exponents across the domain."""
+    lib = O.lib()
+    assert lib.orc_div_shared_check(20_000_000, 7) == 0
