@@ -24,12 +24,50 @@ if "C4" in which:
 if "C3" in which:
     cases["C3"] = (T.gauss([16] * 20, 0.05, 8.5), [16] * 20, [[8] * 20],
                    dict(tolerance=1e-10, maxbonddim=512, nsearchglobalpivot=0))
+
+
+class _TimedLib:
+    """ctx.lib proxy: wall time and calls per ABI entry"""
+
+    def __init__(self, lib):
+        self._lib, self.acc = lib, {}
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if not callable(fn):
+            return fn
+
+        def call(*a, _fn=fn, _n=name):
+            t = time.perf_counter()
+            try:
+                return _fn(*a)
+            finally:
+                c = self.acc.setdefault(_n, [0, 0.0])
+                c[0] += 1
+                c[1] += time.perf_counter() - t
+        return call
+
+
+from tci_amd import _lib as L  # noqa: E402
+ctx = L.context()
+timed = _TimedLib(ctx.lib)
 for name, (f, ld, p0, kw) in cases.items():
     for _ in range(3):
         T.crossinterpolate2(f, ld, p0, **kw)
     t0 = time.perf_counter()
     T.crossinterpolate2(f, ld, p0, **kw)
     wall = time.perf_counter() - t0
+    ctx.lib = timed
+    timed.acc.clear()
+    t0 = time.perf_counter()
+    T.crossinterpolate2(f, ld, p0, **kw)
+    wt = time.perf_counter() - t0
+    ctx.lib = timed._lib
+    abi = sum(v[1] for v in timed.acc.values())
+    print(f"== {name}: ABI split (one run, {wt * 1e3:.3f} ms with the proxy): ABI {abi * 1e3:.3f} ms, "
+          f"Python {(wt - abi) * 1e3:.3f} ms")
+    for k, (n, t) in sorted(timed.acc.items(), key=lambda kv: -kv[1][1])[:14]:
+        print(f"   {k:40s} {n:4d} calls {t * 1e3:8.3f} ms")
     pr = cProfile.Profile()
     pr.enable()
     T.crossinterpolate2(f, ld, p0, **kw)

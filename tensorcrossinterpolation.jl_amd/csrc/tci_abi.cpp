@@ -76,6 +76,7 @@ struct tci_ctx {
     char* zdev = nullptr;  // its device address
     int small_sweep = 1;   // device-resident small sweeps (tci_sweep_small.hip; env TCI_SWEEP_SMALL=0)
     int sw_lu_wave = 1;    // their bonds with m, n <= 32 on the one-wave rrLU (env TCI_SW_LUWAVE=0: off)
+    int sw_lazy_union = 1;  // their unions without materialised kronecker products (env TCI_SW_LAZYU=0: off)
     int32_t* sw_ws = nullptr;   // their six banks of index sets
     size_t capSwWs = 0;
     char* sw_inbuf = nullptr;   // device copy of the input image
@@ -1104,6 +1105,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
     if (const char* e = getenv("TCI_SW_LUWAVE")) c->sw_lu_wave = atoi(e) != 0;
+    if (const char* e = getenv("TCI_SW_LAZYU")) c->sw_lazy_union = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_MID")) c->mid_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_RRLU_PERSIST")) c->persist = tci::kEpochGrid && atoi(e) != 0;
     if (const char* e = getenv("TCI_SHARD_EXCHANGE")) c->sh_exchange = std::max(0, std::min(atoi(e), 2));
@@ -2846,6 +2848,7 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
     a.s1tens = s1 ? s1->tensors : 0;
     a.reltol = s1 ? s1->reltol : 1e-14;
     a.lu_wave = c->sw_lu_wave;
+    a.lazy_union = c->sw_lazy_union;
     a.tens = nullptr;
     a.tcap = 0;
     a.fsolve = mode != 2 && s1 && s1->tensors ? 1 : 0;  // a fill that also solves the site tensors

@@ -89,6 +89,60 @@ __device__ __forceinline__ St leg_state(const FuncDev& f, const int32_t* e, int 
     return s;
 }
 
+// The state of the legs [lead (if > 0), e[0 .. w-1], cval (if > 0)] at global positions toff, ...
+// in that order -- a kronecker(Iset, d) row [I..., j] (cval = j) or kronecker(d, Jset) column
+// [i, J...] (lead = i), tensorci2.jl:512-529, without materialising it; the same operations in the
+// same order as leg_state over the materialised entry. One code path for every entry, so that the
+// lanes of a wave holding kron entries and extras do not diverge into two copies of it.
+__device__ __forceinline__ St leg_state_x(const FuncDev& f, int lead, const int32_t* e, int w, int toff, int cval) {
+    St s;
+    s.i = 0;
+    const int o = lead > 0 ? 1 : 0;  // e[t] sits at position toff + o + t
+    switch (f.kind) {
+    case F_SUM:
+        if (lead > 0) s.i += lead;
+        for_legs(e, w, [&](int, int32_t x) { s.i += x; });
+        if (cval > 0) s.i += cval;
+        break;
+    case F_LORENTZ:
+        if (lead > 0) s.i += (int64_t)lead * lead;
+        for_legs(e, w, [&](int, int32_t x) { s.i += (int64_t)x * x; });
+        if (cval > 0) s.i += (int64_t)cval * cval;
+        break;
+    case F_TABLE:
+        if (lead > 0) s.i += (int64_t)(lead - 1) * f.strides[toff];
+        for_legs(e, w, [&](int t, int32_t x) { s.i += (int64_t)(x - 1) * f.strides[toff + o + t]; });
+        if (cval > 0) s.i += (int64_t)(cval - 1) * f.strides[toff + o + w];
+        break;
+    case F_GAUSS: {
+        double a = 0.0;
+        const double c = f.params[1];
+        if (lead > 0) {
+            const double u = (double)lead - c;
+            a = __dadd_rn(a, __dmul_rn(u, u));
+        }
+        for_legs(e, w, [&](int, int32_t x) {
+            const double u = (double)x - c;
+            a = __dadd_rn(a, __dmul_rn(u, u));
+        });
+        if (cval > 0) {
+            const double u = (double)cval - c;
+            a = __dadd_rn(a, __dmul_rn(u, u));
+        }
+        s.d = a;
+    } break;
+    case F_QOSC:
+    case F_QEXP: {
+        uint64_t idx = 0;
+        if (lead > 0) idx = (uint64_t)(lead - 1);
+        for_legs(e, w, [&](int, int32_t x) { idx = (idx << 1) | (uint64_t)(x - 1); });
+        if (cval > 0) idx = (idx << 1) | (uint64_t)(cval - 1);
+        s.i = (int64_t)idx;
+    } break;
+    }
+    return s;
+}
+
 // value of one Pi element from its row and column states. Lorentzian: the quotient
 // p0 / (s + 1) of the integer sum of squares s, from a table of the same quotients when one is
 // given (s < ntab): bitwise the same division.

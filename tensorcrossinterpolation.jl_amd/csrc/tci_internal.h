@@ -425,6 +425,7 @@ struct SweepSmallArgs {
     double* tens;          // mode 2 / fsolve: [site] (offset, count) int64 pairs, then the tensors (header [10]: used)
     int64_t tcap;          // mode 2 / fsolve: doubles available after the 2 L table entries
     int lu_wave = 1;       // bonds with m, n <= 32: the one-wave rrLU (sw_lu_wave; env TCI_SW_LUWAVE=0: off)
+    int lazy_union = 1;    // mode 0: the union without materialising the kronecker products (env TCI_SW_LAZYU=0: off)
 };
 // sweep1site! on the device (mode 2): the host's request and where the site tensors go
 struct SwSweep1 {

@@ -828,6 +828,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     __shared__ unsigned long long mxs;
     __shared__ int nanflag;
     __shared__ int mn[2];
+    __shared__ int xsel[2][64];  // lazy union: the kept extras (I / J side), in order
     __shared__ double dslot;
     __shared__ int64_t hdr[16];
 
@@ -959,28 +960,82 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int32_t* Ic = reinterpret_cast<int32_t*>(R + kSwLdsS - bI - bJ);
                 int32_t* Jc = reinterpret_cast<int32_t*>(R + kSwLdsS - bJ);
                 int m = 0, n = 0;
-                if (room) {
-                    // the four source sets into LDS in one batched round of loads
-                    {
-                        const int32_t* s0 = set_ptr(0, 0, b - 1);
-                        const int32_t* s1 = set_ptr(1, 0, b);
-                        const int32_t* s2 = set_ptr(0, 2, b);
-                        const int32_t* s3 = set_ptr(1, 2, b - 1);
-                        const int n01 = gI + gJ, n012 = n01 + gEI, tot = n012 + gEJ;
-                        for (int base = 0; base < tot; base += kSwCopyB * kSwThreads) {
-                            int32_t v[kSwCopyB];
+                // Lazy union (round 6): the kronecker products are not materialised. Their entries are
+                // distinct (Iset / Jset are sets), so union(kron, extra) keeps every kron entry in order
+                // and appends the extras that are neither in the kron product nor earlier extras: only
+                // the <= 64 extras are hashed and compared (an extra [I..., j] is a kron entry iff
+                // 1 <= j <= d and its prefix is an Iset entry; [i, J...] likewise), and rows, states
+                // and the new sets are read from the staged sources by descriptor. The sources stay
+                // staged (top of S) until the selection; Pi lives below them. Same entries in the
+                // same order as the materialised union, hence the same Pi and pivots. Taken where a leg
+                // has d >= 4: with d = 2 (quantics) the materialised kron is a couple of row copies and
+                // the materialised path was faster (C4 9.2 vs 9.85 ms; C1 d = 10 6.0 -> 5.1 ms).
+                const bool lzu = a.lazy_union && max(dI, dJ) >= 4 && nI <= 64 && neI <= 64 && nJ <= 64 && neJ <= 64 && bG <= kSwLdsS / 2;
+                const int KI = nI * dI, KJ = nJ * dJ;
+                int32_t* const gsl = reinterpret_cast<int32_t*>(R + kSwLdsS - bG);
+                // the four source sets into LDS (dst) in one batched round of loads
+                auto stage = [&](int32_t* dst) {
+                    const int32_t* s0 = set_ptr(0, 0, b - 1);
+                    const int32_t* s1 = set_ptr(1, 0, b);
+                    const int32_t* s2 = set_ptr(0, 2, b);
+                    const int32_t* s3 = set_ptr(1, 2, b - 1);
+                    const int n01 = gI + gJ, n012 = n01 + gEI, tot = n012 + gEJ;
+                    for (int base = 0; base < tot; base += kSwCopyB * kSwThreads) {
+                        int32_t v[kSwCopyB];
 #pragma unroll
-                            for (int u = 0; u < kSwCopyB; ++u) {
-                                const int e = base + tid + u * kSwThreads;
-                                v[u] = e < gI ? s0[e] : e < n01 ? s1[e - gI] : e < n012 ? s2[e - n01] : e < tot ? s3[e - n012] : 0;
-                            }
+                        for (int u = 0; u < kSwCopyB; ++u) {
+                            const int e = base + tid + u * kSwThreads;
+                            v[u] = e < gI ? s0[e] : e < n01 ? s1[e - gI] : e < n012 ? s2[e - n01] : e < tot ? s3[e - n012] : 0;
+                        }
 #pragma unroll
-                            for (int u = 0; u < kSwCopyB; ++u) {
-                                const int e = base + tid + u * kSwThreads;
-                                if (e < tot) gs[e] = v[u];
-                            }
+                        for (int u = 0; u < kSwCopyB; ++u) {
+                            const int e = base + tid + u * kSwThreads;
+                            if (e < tot) dst[e] = v[u];
                         }
                     }
+                };
+                if (lzu) {
+                    stage(gsl);
+                    __syncthreads();
+                    SWP(5);
+                    const int wv = tid >> 6, ln = tid & 63;
+                    if (wv < 2) {  // wave 0: the I side, wave 1: the J side
+                        const bool sideI = wv == 0;
+                        const int nk = sideI ? nI : nJ, ne = sideI ? neI : neJ, dk = sideI ? dI : dJ;
+                        const int wk = sideI ? wI0 : wJ0, we = wk + 1;
+                        const int32_t* K = sideI ? gsl : gsl + gI;                   // Iset[b-1] / Jset[b]
+                        const int32_t* E = sideI ? gsl + gI + gJ : gsl + gI + gJ + gEI;  // the extras
+                        const int32_t* et = E + ln * we;
+                        bool keep = ln < ne;
+                        // the extra's leg on the kron side (last for I, first for J) and its other legs
+                        const int leg = keep ? (sideI ? et[wk] : et[0]) : 0;
+                        const int32_t* rest = sideI ? et : et + 1;
+                        const uint32_t hr = keep ? sw_hash(rest, wk) : 0u;         // vs the kron sources
+                        const uint32_t hf = (hr ^ (uint32_t)leg) * 16777619u;      // (rest, leg): vs earlier extras
+                        const uint32_t hk = ln < nk ? sw_hash(K + ln * wk, wk) : 0u;
+                        // in the kron product? (readlane reads lane s2 whatever the exec mask)
+                        const bool kin = keep && leg >= 1 && leg <= dk;
+                        for (int s2 = 0; s2 < nk; ++s2) {
+                            const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)hk, s2);
+                            if (kin && keep && h2 == hr && sw_rows_equal(K + s2 * wk, rest, wk)) keep = false;
+                        }
+                        for (int s2 = 0; s2 < ne - 1; ++s2) {  // an equal earlier extra
+                            const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)hf, s2);
+                            if (keep && s2 < ln && h2 == hf && sw_rows_equal(E + s2 * we, et, we)) keep = false;
+                        }
+                        const uint64_t bal = __ballot(keep);
+                        if (keep) {
+                            const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                            (sideI ? xsel[0] : xsel[1])[pos] = ln;
+                        }
+                        if (ln == 0) mn[wv] = __popcll(bal);
+                    }
+                    __syncthreads();
+                    m = KI + mn[0];
+                    n = KJ + mn[1];
+                } else if (room) {
+                    stage(gs);
                     __syncthreads();
                     SWP(5);
                     const int32_t* Ib = gs;
@@ -1032,7 +1087,8 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 }
                 const bool fits = m > 0 && n > 0 && (int64_t)(m | 1) * n <= kSmallElems && m + n <= kSmallPerm;  // rrlu_small_fits
                 const int ldS = m | 1;
-                if (!room || !fits || a.maxbonddim <= 0 || (size_t)ldS * n * 8 > kSwLdsS - bI - bJ) {
+                if (!(room || lzu) || !fits || a.maxbonddim <= 0 ||
+                    (size_t)ldS * n * 8 > (lzu ? kSwLdsS - bG : kSwLdsS - bI - bJ)) {
                     status = 1;  // resume on the host at (it, q)
                     s_it = it;
                     s_q = q;
@@ -1045,18 +1101,52 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 // then one compact loop over the elements (one inlined copy of f, for the I-cache)
                 St* rs = reinterpret_cast<St*>(xy);
                 St* cs = rs + m;
-                for (int i = tid; i < m; i += kSwThreads) rs[i] = leg_state(f, Ic + i * wI, wI, 0, 0);
-                for (int j = tid; j < n; j += kSwThreads) cs[j] = leg_state(f, Jc + j * wJ, wJ, wI, 0);
+                const int32_t* const Ibl = gsl;                      // (lazy union) Iset[b-1], Jset[b], the extras
+                const int32_t* const Jbl = gsl + gI;
+                const int32_t* const Exl = gsl + gI + gJ;
+                const int32_t* const Eyl = gsl + gI + gJ + gEI;
+                // rows and columns in ONE pass over the m + n entries (one leg_state per thread, not a
+                // row pass then a column pass); lazily one leg_state_x per entry (kron rows and extras
+                // in one code path)
+                for (int t = tid; t < m + n; t += kSwThreads) {
+                    const bool row = t < m;
+                    const int i = row ? t : t - m;
+                    if (lzu) {
+                        const bool kr = i < (row ? KI : KJ);
+                        const int32_t* e;
+                        int w, lead = 0, cv = 0;
+                        if (row) {
+                            e = kr ? Ibl + (i % nI) * wI0 : Exl + xsel[0][i - KI] * wI;
+                            w = kr ? wI0 : wI;
+                            cv = kr ? i / nI + 1 : 0;
+                        } else {
+                            e = kr ? Jbl + (i / dJ) * wJ0 : Eyl + xsel[1][i - KJ] * wJ;
+                            w = kr ? wJ0 : wJ;
+                            lead = kr ? i % dJ + 1 : 0;
+                        }
+                        (row ? rs : cs)[i] = leg_state_x(f, lead, e, w, row ? 0 : wI, cv);
+                    } else {
+                        (row ? rs : cs)[i] = leg_state(f, row ? Ic + i * wI : Jc + i * wJ, row ? wI : wJ, row ? 0 : wI, 0);
+                    }
+                }
                 __syncthreads();
                 SWP(6);
                 double mx = 0.0, error, maxerror;
+                // (i, j) = (e mod m, e / m) stepped incrementally: no integer division per element
+                const int di = kSwThreads % m, dj = kSwThreads / m;
+                int i = tid % m, j = tid / m;
 #pragma unroll 1
                 for (int e = tid; e < m * n; e += kSwThreads) {
-                    const int i = e % m, j = e / m;
                     const double v = combine<KIND>(p, p0, rs[i], cs[j], wJ, L, nullptr, 0);
                     S[i + j * ldS] = v;
                     const double av = fabs(v);
                     mx = (isnan(av) || av > mx) ? av : mx;
+                    i += di;
+                    j += dj;
+                    if (i >= m) {
+                        i -= m;
+                        j += 1;
+                    }
                 }
                 SWP(7);
                 mx = sw_maxabs(mx, &mxs);
@@ -1090,8 +1180,30 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 const int tJs = sw_other(rol[1][1][b - 1], rol[1][2][b - 1]);
                 int32_t* Io = bank_ptr(2 * tIs, b);
                 int32_t* Jo = bank_ptr(2 * tJs + 1, b - 1);
-                for (int e = tid; e < np * wI; e += kSwThreads) Io[e] = Ic[rp[e / wI] * wI + e % wI];
-                for (int e = tid; e < np * wJ; e += kSwThreads) Jo[e] = Jc[cp[e / wJ] * wJ + e % wJ];
+                // a wave per row / column of the new set, a lane per leg (L <= 64): the row's source
+                // (kron entry or kept extra) decoded once per row, no division per element
+                {
+                    const int wv = tid >> 6, l = tid & 63;
+                    for (int rr = wv; rr < 2 * np; rr += kSwWaves) {
+                        const bool sI = rr < np;
+                        const int k = sI ? rr : rr - np;
+                        const int w = sI ? wI : wJ;
+                        if (l >= w) continue;
+                        int32_t v;
+                        if (lzu) {
+                            if (sI) {
+                                const int r = rp[k];
+                                v = r < KI ? (l < wI0 ? Ibl[(r % nI) * wI0 + l] : r / nI + 1) : Exl[xsel[0][r - KI] * wI + l];
+                            } else {
+                                const int c = cp[k];
+                                v = c < KJ ? (l == 0 ? c % dJ + 1 : Jbl[(c / dJ) * wJ0 + l - 1]) : Eyl[xsel[1][c - KJ] * wJ + l];
+                            }
+                        } else {
+                            v = sI ? Ic[rp[k] * wI + l] : Jc[cp[k] * wJ + l];
+                        }
+                        (sI ? Io : Jo)[k * w + l] = v;
+                    }
+                }
                 // updateerrors!(tci, b, pivoterrors(lu)): elementwise max over zero-padded vectors
                 const int ne = max(npe, np + 1);
                 for (int i = tid; i < ne; i += kSwThreads) {

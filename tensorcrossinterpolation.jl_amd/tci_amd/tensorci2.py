@@ -412,10 +412,20 @@ class TensorCI2:
             return False
         self._native_pull(ctx, h)  # sweep1site! leaves the history alone (so does the kernel)
         if updatetensors:
-            for p in range(n):
-                o, c = int(offs[2 * p]), int(offs[2 * p + 1])
-                self.setsitetensor_(p + 1, tens[o:o + c].copy())
+            self._native_set_tensors(tens, offs)
         return True
+
+    def _native_set_tensors(self, tens, offs):
+        """setsitetensor! for every site from a native fill's packed output: the shapes from the
+        native set counts, so the (still native-side) index sets are neither pulled nor marked as
+        modified -- the next sweep does not have to push them back."""
+        nI, nJ = self._native_counts(0), self._native_counts(1)
+        for p in range(len(self)):
+            o, c = int(offs[2 * p]), int(offs[2 * p + 1])
+            shape = (int(nI[p]), int(self.localdims[p]), int(nJ[p]))
+            if shape[0] * shape[1] * shape[2] != c:
+                raise RuntimeError(f"native site tensor {p + 1}: {c} values for shape {shape}")
+            self.sitetensors[p] = tens[o:o + c].reshape(shape, order="F")
 
     def _sweep2site_native(self, f, niter, iter1, abstol, maxbonddim, sweepstrategy, strictlynested,
                            fill=None):
@@ -454,9 +464,7 @@ class TensorCI2:
             self._native_has_hist = True  # every iteration starts a history
         self._native_pull(ctx, h)
         if fill == "solve" and handled.value:
-            for p in range(n):
-                o, c = int(offs[2 * p]), int(offs[2 * p + 1])
-                self.setsitetensor_(p + 1, tens[o:o + c].copy())
+            self._native_set_tensors(tens, offs)
         return bool(handled.value)
 
     @contextlib.contextmanager
