@@ -1,10 +1,16 @@
-# rocprofv3 kernel trace of the dense bench (K3 / K4 / K5) for one TCI_GETRF_NT setting: per-kernel
-# times of the getrf panel chain.   gpurun -- bash scripts/k5_trace.sh TAG NT
+#!/bin/bash
+# kernel trace of the K5 solve at the C5 shape (scripts/k5_prof.py)
 set -o pipefail
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-T=${1:-k5t}; NT=${2:-256}
-( cd /tmp && export TMPDIR=/tmp && export TCI_GETRF_NT=$NT && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d $GRAFT_REPO_ROOT/gpurun_out/${T}_trace -o run -- python3 $GRAFT_REPO_ROOT/scripts/dense_bench.py ) \
-    > gpurun_out/${T}_trace.log 2>&1 || { tail -20 gpurun_out/${T}_trace.log; exit 1; }
-f=$(ls gpurun_out/${T}_trace/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -z "$f" ] && f=$(ls gpurun_out/${T}_trace/run_kernel_stats.csv)
-cut -d, -f1-4 "$f" | head -30
+cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
+R=$PWD
+mkdir -p gpurun_out
+T=$1
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${T}_k5" -o run \
+    -- python3 "$R/scripts/k5_prof.py" 1024 32768 3 ) > gpurun_out/${T}_k5.log 2>&1 || { tail -20 gpurun_out/${T}_k5.log; exit 1; }
+grep "per solve" gpurun_out/${T}_k5.log
+f=$(find gpurun_out/${T}_k5 -name '*kernel_stats.csv' | sed -n 1p)
+python3 - "$f" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    print(f'{r["Name"][:70]:72s} {int(r["Calls"]):6d} {float(r["TotalDurationNs"]) / 4e6:9.3f} ms/solve {float(r["AverageNs"]) / 1e3:9.2f} us avg')
+PY

@@ -10,6 +10,7 @@
 #include <cstddef>
 #include <cmath>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -72,6 +73,9 @@ struct tci_ctx {
     size_t capHin = 0;
     char* hout = nullptr;
     size_t capHout = 0;
+    char* hd2h = nullptr;  // d2h_large's two pinned chunk slots
+    size_t capHd2h = 0;
+    hipEvent_t d2h_ev[2] = {nullptr, nullptr};
     char* zbuf = nullptr;  // mapped pinned host memory the small path's kernels write into
     char* zdev = nullptr;  // its device address
     int small_sweep = 1;   // device-resident small sweeps (tci_sweep_small.hip; env TCI_SWEEP_SMALL=0)
@@ -351,6 +355,57 @@ int ensure_pinned(tci_ctx* c, char** p, size_t* cap, size_t bytes) {
                                              " bytes failed");
     }
     *cap = want;
+    return TCI_OK;
+}
+
+// host memcpy over up to 8 threads (page faults of fresh destination pages and the copy itself
+// spread over cores): large device -> pageable host results only
+static void par_memcpy(char* dst, const char* src, size_t n) {
+    const size_t per = 4u << 20;
+    const int nt = (int)std::min<size_t>(8, n / per);
+    if (nt <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t blk = ((n / nt) + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const size_t o = (size_t)t * blk;
+        if (o < n) th.emplace_back([=] { memcpy(dst + o, src + o, std::min(blk, n - o)); });
+    }
+    memcpy(dst, src, std::min(blk, n));
+    for (auto& x : th) x.join();
+}
+
+// n bytes of device memory into pageable host memory (then synchronised). Small copies go straight
+// to hipMemcpyAsync; large ones (the site tensors and MatrixLUCI factors of config 5: up to 268 MB)
+// in 32-MB chunks through two pinned slots -- chunk k + 1's DMA in flight while the host threads copy
+// chunk k out -- instead of the runtime's pageable path (~20 GB/s with one host thread).
+static int d2h_large(tci_ctx* c, void* dst, const void* src, size_t n) {
+    constexpr size_t kCh = 32u << 20;
+    if (n < 2 * kCh) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return TCI_OK;
+    }
+    int st;
+    if ((st = ensure_pinned(c, &c->hd2h, &c->capHd2h, 2 * kCh))) return st;
+    for (auto& e : c->d2h_ev)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t nch = (n + kCh - 1) / kCh;
+    auto issue = [&](size_t k) -> int {
+        const size_t len = std::min(kCh, n - k * kCh);
+        HIPCHK(c, hipMemcpyAsync(c->hd2h + (k & 1) * kCh, static_cast<const char*>(src) + k * kCh, len,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->d2h_ev[k & 1], c->stream));
+        return TCI_OK;
+    };
+    if ((st = issue(0))) return st;
+    for (size_t k = 0; k < nch; ++k) {
+        if (k + 1 < nch && (st = issue(k + 1))) return st;  // slot (k + 1) & 1 was drained at step k - 1
+        HIPCHK(c, hipEventSynchronize(c->d2h_ev[k & 1]));
+        par_memcpy(static_cast<char*>(dst) + k * kCh, c->hd2h + (k & 1) * kCh, std::min(kCh, n - k * kCh));
+    }
     return TCI_OK;
 }
 
@@ -1165,6 +1220,9 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->dIa); fr(c->dJa);
     if (c->ev_ina) hipEventDestroy(c->ev_ina);
     if (c->hout) hipHostFree(c->hout);
+    if (c->hd2h) hipHostFree(c->hd2h);
+    for (auto e : c->d2h_ev)
+        if (e) hipEventDestroy(e);
     if (c->zbuf) hipHostFree(c->zbuf);
     fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens); fr(c->sw_fmap);
     if (c->sw_in) hipHostFree(c->sw_in);
@@ -1969,12 +2027,8 @@ static int luci_outputs(tci_ctx* c, int64_t m, int64_t n, int leftorth, int64_t 
                                  right ? c->dF2 : nullptr, c->dense);
         ev_end(c);
         HIPCHK(c, hipGetLastError());
-        if (left)
-            HIPCHK(c, hipMemcpyAsync(left, c->dF1, m * np * sizeof(double), hipMemcpyDeviceToHost,
-                                     c->stream));
-        if (right)
-            HIPCHK(c, hipMemcpyAsync(right, c->dF2, np * n * sizeof(double), hipMemcpyDeviceToHost,
-                                     c->stream));
+        if (left && (st = d2h_large(c, left, c->dF1, (size_t)(m * np) * sizeof(double)))) return st;
+        if (right && (st = d2h_large(c, right, c->dF2, (size_t)(np * n) * sizeof(double)))) return st;
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     return TCI_OK;
@@ -2150,16 +2204,15 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
         ev_end(c);
         HIPCHK(c, hipGetLastError());
     }
-    // T (and maxabs) down through one pinned stage
+    // maxabs through the pinned stage, T by d2h_large (chunked through pinned slots, host copy threaded)
     const size_t bt = (size_t)(R * nJb) * 8;
-    if ((st = ensure_pinned(c, &c->hout, &c->capHout, bt + 16))) return st;
+    if ((st = ensure_pinned(c, &c->hout, &c->capHout, 16))) return st;
     HIPCHK(c, hipMemcpyAsync(c->hout, c->maxbits, 8, hipMemcpyDeviceToHost, c->stream));
-    if (bt && (solve || !Inext))
-        HIPCHK(c, hipMemcpyAsync(c->hout + 16, solve ? c->dA : c->dF1, bt, hipMemcpyDeviceToHost,
-                                 c->stream));
+    if (bt && (solve || !Inext)) {
+        if ((st = d2h_large(c, T, solve ? c->dA : c->dF1, bt))) return st;
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (maxabs) memcpy(maxabs, c->hout, 8);
-    if (bt && (solve || !Inext)) memcpy(T, c->hout + 16, bt);
     return TCI_OK;
 }
 
