@@ -280,8 +280,8 @@ def main():
                      "deferred_depth_nb": nb, "epochs": args.epochs, "shadow_search": shadow, "shadow_bytes": sh_bytes,
                      "step_algorithmic_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                      "step_note": "all passes' algorithmic bytes + initial pass + copy, per measured step; "
-                                  "frac above is the dominant (read-only) kernel alone, half of whose "
-                                  "~40 us is fixed per-pass cost (DESIGN.md K2)"},
+                                  "frac above is the dominant (read-only) kernel alone, most of whose "
+                                  "~34 us is fixed per-pass cost (DESIGN.md K2)"},
     }
     # HBM bytes per launch from the committed PMC summary of this configuration (FETCH_SIZE x 2 +
     # WRITE_SIZE, scripts/profile_round.sh); null when none matches
@@ -348,9 +348,9 @@ def main():
         sys.exit(3)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_z3_pmc_summary.json")
-TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r05_z3_trace_roofline.json")  # scripts/trace_roofline.py
-PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 3, "shadow": True, "sh_bytes": 2}  # the profiled command
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_i1_pmc_summary.json")
+TRACE_ROOFLINE = os.path.join(ROOT, "profiles", "r06_i1_trace_roofline.json")  # scripts/trace_roofline.py
+PMC_CONFIG = {"m": 8192, "n": 8192, "r": 256, "nb": 10, "epochs": 2, "shadow": True, "sh_bytes": 1}  # the profiled command
 
 
 def pmc_traffic(fam, m, n, r, nb, epochs, shadow, sh_bytes):

@@ -11,7 +11,6 @@ are (count, width) int32 arrays of 1-based local indices.
 """
 import contextlib
 import ctypes as C
-
 import numpy as np
 
 from . import _lib
@@ -21,6 +20,58 @@ INT64_MAX = np.iinfo(np.int64).max
 
 
 # ------------------------------------------------------------------ helpers
+_BIG_FREE = 16 << 20  # site tensors at least this large are recycled
+
+
+class _BufferPool:
+    """Flat float64 buffers of large device -> host site tensors, recycled. Config 5 replaces 12
+    tensors of up to 268 MB every iteration: freeing them (munmap) and faulting fresh pages in for
+    the next ones cost ~0.3 s of its 21 s. A replaced tensor's buffer is taken back only when
+    nothing else can see it -- the buffer came from this pool, the replaced array is a view whose
+    only owner was the TensorCI2, and no other view of the buffer is alive -- so recycling is never
+    observable. Bounded (_CAP bytes); anything else is simply dropped."""
+    _CAP = 16 << 30
+
+    def __init__(self):
+        self.free = {}  # size -> [buffers]
+        self.bytes = 0
+        self.ids = set()  # ids of live buffers handed out by take()
+
+    def take(self, n):
+        lst = self.free.get(n)
+        if lst:
+            buf = lst.pop()
+            self.bytes -= buf.nbytes
+        else:
+            buf = np.empty(max(n, 1))
+        if buf.nbytes >= _BIG_FREE:
+            self.ids.add(id(buf))
+        return buf
+
+    def give_back(self, arrays):
+        import sys
+        for i in range(len(arrays)):
+            a = arrays[i]
+            arrays[i] = None
+            if not isinstance(a, np.ndarray) or a.nbytes < _BIG_FREE:
+                continue
+            root = a.base
+            # the array (this local, getrefcount's argument) and its buffer (the array's .base, this
+            # local, getrefcount's argument): any further reference means someone else holds it
+            if (not isinstance(root, np.ndarray) or root.base is not None or id(root) not in self.ids
+                    or sys.getrefcount(a) > 2 or sys.getrefcount(root) > 3):
+                continue
+            del a
+            if self.bytes + root.nbytes > self._CAP:
+                self.ids.discard(id(root))
+                continue
+            self.free.setdefault(root.size, []).append(root)
+            self.bytes += root.nbytes
+
+
+_POOL = _BufferPool()
+
+
 def jl_max(x, y):
     """Base.max for Float64 (NaN-propagating, max(-0.0, 0.0) == 0.0)."""
     if (y > x) or (np.signbit(y) < np.signbit(x)):
@@ -193,8 +244,10 @@ class TensorCI2:
         return max(self.linkdims()) if len(self) > 1 else 0
 
     def invalidatesitetensors(self):
+        old = list(self.sitetensors)
         for b in range(len(self)):
             self.sitetensors[b] = np.zeros((0, 0, 0))
+        _POOL.give_back(old)
 
     def issitetensorsavailable(self):
         return all(t.size != 0 for t in self.sitetensors)
@@ -241,8 +294,10 @@ class TensorCI2:
 
     def setsitetensor_(self, b, T):
         """setsitetensor!(tci, b, T) (tensorci2.jl:536-545); b is 1-based."""
+        old = [self.sitetensors[b - 1]]
         self.sitetensors[b - 1] = np.asarray(T).reshape(
             (len(self.Iset[b - 1]), self.localdims[b - 1], len(self.Jset[b - 1])), order="F")
+        _POOL.give_back(old)
 
     # -- hot path
     def updatepivots(self, b, f, leftorthogonal, reltol=1e-14, abstol=0.0, maxbonddim=INT64_MAX,
@@ -764,8 +819,9 @@ def update_pivots_device(f, rows, cols, maxrank, reltol, abstol, leftorth, want_
     pe = np.zeros(mr + 1)
     npv = C.c_int64()
     mx = C.c_double()
-    left = np.zeros(max(m * mr, 1)) if (want_factors and want_left) else None
-    right = np.zeros(max(mr * n, 1)) if (want_factors and want_right) else None
+    # (large factor buffers recycled from replaced site tensors: every value read back is written)
+    left = _POOL.take(m * mr) if (want_factors and want_left) else None
+    right = _POOL.take(mr * n) if (want_factors and want_right) else None
     ctx.check(ctx.lib.tci_update_pivots_h(ctx.h, f.h, _lib.ptr(rows), m, nl, _lib.ptr(cols), n, nr,
                                           int(min(maxrank, INT64_MAX)), float(reltol), float(abstol),
                                           int(bool(leftorth)), int(bool(want_factors)), _lib.ptr(rowidx),
@@ -895,12 +951,12 @@ def sitetensor_device(f, Ib, Jb, Inext, solve=True):
     R = nI * d
     mx = C.c_double()
     if Inext is None:
-        T = np.zeros(max(R * nJ, 1)) if solve else None
+        T = _POOL.take(R * nJ) if solve else None  # (written in full by the device copy)
         nxt, nn = None, 0
     else:
         Inext = np.ascontiguousarray(Inext, np.int32)
         nn = len(Inext)
-        T = np.zeros(max(R * nn, 1)) if solve else None
+        T = _POOL.take(R * nn) if solve else None
         nxt = Inext
     if not solve:
         # only max|Pi1| is observable: evaluate Pi1 on the device, no solve, no copy back
