@@ -46,6 +46,7 @@ struct tci_ctx {
     int serpentine = 1;    // alternate the pass's tile order (env TCI_RRLU_SERP=0 disables)
     int shadow = 1;        // certified fp32 search in read-only passes (env TCI_RRLU_SHADOW=0)
     int pass_gridx = 1;    // rrLU pass workgroups per CU (env TCI_PASS_GRIDX; 1 = all resident at once)
+    int pass_griddiv = 1;  // A/B: the pass grid over this many fewer CUs (env TCI_PASS_GRIDDIV)
     float* sbuf = nullptr; // its fp32 shadow of the matrix
     size_t capS = 0;
     int small_path = 1;    // single-workgroup LDS rrLU for small matrices (env TCI_RRLU_SMALL=0)
@@ -642,7 +643,7 @@ int rrlu_device(tci_ctx* c, double* dA, int64_t m, int64_t n, int64_t lda, int64
         if ((st = zero_shadow_pad(c, g.lds, m, n))) return st;
     }
     const int grid = tci::argmax_grid(mi, ni, -1, g.cb,
-                                      std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
+                                      std::min(std::max(std::max(c->ncu, 1) * c->pass_gridx / c->pass_griddiv, 8), kMaxGrid));
     // two-level epoch: shadow epochs of nb pivots end with a refresh of the fp16
     // shadow by the MFMA search itself, and only every `epochs`-th of them with a write-back of the
     // fp64 values (exact pending updates up to nb * epochs <= kMaxPendR). epochs = 1: every shadow
@@ -1058,7 +1059,7 @@ int rrlu_sharded_device(tci_ctx* c, tci_comm* comm, tci_exchange_fn exch, void* 
         g.S = c->sbuf;
         if ((st = zero_shadow_pad(c, g.lds, m, nl1))) return st;
     }
-    const int grid = tci::argmax_grid(mi, nl1, -1, g.cb, std::min(std::max(c->ncu, 1) * c->pass_gridx, kMaxGrid));
+    const int grid = tci::argmax_grid(mi, nl1, -1, g.cb, std::min(std::max(std::max(c->ncu, 1) * c->pass_gridx / c->pass_griddiv, 8), kMaxGrid));
     // candidates: own record at lout[0], the all-gathered ones at lout[1..nranks]
     tci::Cand* recvC = multi ? c->lout + 1 : c->lout;
     uint64_t* colsend = reinterpret_cast<uint64_t*>(c->shsend);
@@ -1157,6 +1158,7 @@ int tci_ctx_create(int device, tci_ctx** out) {
     if (const char* e = getenv("TCI_RRLU_EPOCHS")) c->epochs = std::max(0, std::min(atoi(e), tci::kMaxPendR));
     if (const char* e = getenv("TCI_RRLU_SHADOW")) c->shadow = atoi(e) != 0;
     if (const char* e = getenv("TCI_PASS_GRIDX")) c->pass_gridx = std::max(1, std::min(atoi(e), 8));
+    if (const char* e = getenv("TCI_PASS_GRIDDIV")) c->pass_griddiv = std::max(1, std::min(atoi(e), 16));
     if (const char* e = getenv("TCI_RRLU_SMALL")) c->small_path = atoi(e) != 0;
     if (const char* e = getenv("TCI_SWEEP_SMALL")) c->small_sweep = atoi(e) != 0;
     if (const char* e = getenv("TCI_SW_LUWAVE")) c->sw_lu_wave = atoi(e) != 0;
