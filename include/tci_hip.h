@@ -537,6 +537,9 @@ int tci_diag_mfma_f64_ex(tci_ctx* ctx, int waves_per_simd, double* tflops, doubl
 int tci_malloc_d(tci_ctx* ctx, void** p, int64_t bytes);
 int tci_free_d(tci_ctx* ctx, void* p);
 int tci_memcpy_h2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
+/* device -> pageable host, synchronous; from 64 MB up in 32-MB chunks through two pinned slots (one
+ * chunk's DMA in flight while host threads copy the previous one out). The site tensors and
+ * MatrixLUCI factors of tci_sitetensor_h / tci_update_pivots_h come back the same way. */
 int tci_memcpy_d2h(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int tci_memcpy_d2d(tci_ctx* ctx, void* dst, const void* src, int64_t bytes);
 /* bytes bytes of dst set to (unsigned char)value, stream-ordered on the context stream (no host

@@ -2506,9 +2506,9 @@ int tci_memset_d(tci_ctx* c, void* dst, int value, int64_t bytes) {
     return TCI_OK;
 }
 int tci_memcpy_d2h(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
-    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return TCI_OK;
+    if (!c || bytes < 0 || (bytes > 0 && (!dst || !src))) return TCI_ERR_ARG;
+    if (bytes == 0) return TCI_OK;
+    return d2h_large(c, dst, src, (size_t)bytes);  // (synchronous; chunked through pinned slots when large)
 }
 int tci_memcpy_d2d(tci_ctx* c, void* dst, const void* src, int64_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
