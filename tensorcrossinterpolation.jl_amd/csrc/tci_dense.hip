@@ -214,6 +214,10 @@ static void dgemm_go(hipStream_t s, DgemmArgs g) {
     // trip dominates and four times as many 64 x 64 tiles keep more of it in flight (8192^2, nb 32:
     // 0.268 vs 0.289 ms, profiles/r04_s6_k3_tile*.json)
     if (ov == 0 && g.k <= 32 && t64 >= 1024) ov = 3;
+    // n <= 64 (the getrs updates of 64-column blocks of T, R x 64 x jb): a 128-wide tile would run
+    // half its MFMAs on zero padding; 64 x 64 tiles: the r = 1024, R = 32768 solve 8.97 -> 8.05 ms
+    // (scripts/k5_tiles.sh, profiles/r06_m2_k5_tiles.txt)
+    if (ov == 0 && g.n <= 64 && t64 >= 256) ov = 3;
     if (ov == 1 || (ov == 0 && t128 >= 256)) {
         g.tm = (g.m + 127) / 128;
         g.tn = (g.n + 127) / 128;
@@ -766,15 +770,39 @@ void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv, bool reg) {
 // T (R x r) = Pi1 P^-1 given A = LU(P^T) and its interchanges: T's columns permuted as the rows of
 // P^T were (k_gather_cols), then T <- T L^-T (forward, unit) and T <- T U^-T (backward), each as
 // kTrsmNB-wide diagonal solves (one thread per row of T) and K3 updates.
-__global__ void k_piv_to_perm(const int* __restrict__ piv, int r, int* __restrict__ perm) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    for (int a = 0; a < r; ++a) perm[a] = a;
-    for (int k = 0; k < r; ++k) {
-        const int p = piv[k];
-        const int t = perm[k];
-        perm[k] = perm[p];
-        perm[p] = t;
+// (the interchanges composed in LDS by one thread -- the sequence is inherently serial -- with the
+// interchange list and the permutation staged through LDS by the whole workgroup: each step is two
+// LDS round trips instead of two global ones; 160 us -> tens of us at r = 1024)
+constexpr int kPermLds = 4096;
+__global__ __launch_bounds__(256) void k_piv_to_perm(const int* __restrict__ piv, int r, int* __restrict__ perm) {
+    if (blockIdx.x != 0) return;
+    __shared__ int sp[kPermLds], spv[kPermLds];
+    if (r > kPermLds) {  // (not the solve's sizes: r <= 8192 / 2; the global fallback)
+        if (threadIdx.x != 0) return;
+        for (int a = 0; a < r; ++a) perm[a] = a;
+        for (int k = 0; k < r; ++k) {
+            const int p = piv[k];
+            const int t = perm[k];
+            perm[k] = perm[p];
+            perm[p] = t;
+        }
+        return;
     }
+    for (int a = threadIdx.x; a < r; a += blockDim.x) {
+        sp[a] = a;
+        spv[a] = piv[a];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < r; ++k) {
+            const int p = spv[k];
+            const int t = sp[k];
+            sp[k] = sp[p];
+            sp[p] = t;
+        }
+    }
+    __syncthreads();
+    for (int a = threadIdx.x; a < r; a += blockDim.x) perm[a] = sp[a];
 }
 
 __global__ void k_gather_cols(const double* __restrict__ Pi1, int R, int r, const int* __restrict__ perm,
@@ -789,7 +817,7 @@ __global__ void k_gather_cols(const double* __restrict__ Pi1, int R, int r, cons
 
 void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv, const double* Pi1,
                           int R, double* T, int* perm) {
-    hipLaunchKernelGGL(k_piv_to_perm, dim3(1), dim3(1), 0, s, piv, r, perm);
+    hipLaunchKernelGGL(k_piv_to_perm, dim3(1), dim3(256), 0, s, piv, r, perm);
     const long long work = (long long)R * r;
     hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)std::min<long long>(8192, (work + 255) / 256)), dim3(256),
                        0, s, Pi1, R, r, perm, T);
