@@ -380,6 +380,21 @@ int tci_tci2_fill_maxsample(tci_tci2* tci, const tci_func* f, int* handled);
  * runs tci_sitetensor_h per site. */
 int tci_tci2_fill_solve(tci_tci2* tci, const tci_func* f, double* tensors, int64_t capacity, int64_t* offsets,
                         int* handled);
+/* optimize!(tci, f; tolerance, maxbonddim, maxiter, ncheckhistory, normalizeerror, strictlynested,
+ * nsearchglobalpivot = 0, sweepstrategy = :backandforth, pivotsearch = :full) (tensorci2.jl:1018-1172)
+ * for a TCI2 whose bonds fit the device-resident small sweep: every iteration (sweep2site! with
+ * fillsitetensors! -- solved when solvefill -- then pivoterror / rank / convergencecriterion) runs as
+ * a chain of launches that keeps the state on the device, then sweep1site!(forward, abstol =
+ * tolerance * maxsample) with its site tensors (tensors / capacity / offsets as tci_tci2_sweep1site).
+ * errors[i] / ranks[i]: iteration i + 1's pivoterror / rank, *niter of them (maxiter < 64).
+ * *handled = 0: nothing done; otherwise the state is the one after *niter iterations and, when
+ * *ended and *s1done, after the closing sweep too (*errnorm: the maxsample it normalised with). A
+ * bond, fill or sweep the device cannot run ends the chain early (*ended = 0: the caller continues
+ * the loop; *ended = 1, *s1done = 0: the caller runs the closing sweep). */
+int tci_tci2_optimize_small(tci_tci2* t, const tci_func* f, double tolerance, int64_t maxbonddim, int32_t maxiter,
+                            int32_t ncheckhistory, int32_t normalizeerror, int32_t strictlynested, int32_t solvefill,
+                            double* tensors, int64_t capacity, int64_t* offsets, double* errors, int64_t* ranks,
+                            int32_t* niter, int32_t* ended, int32_t* s1done, double* errnorm, int* handled);
 /* tci_tci2_sweep2site followed by tci_tci2_fill_solve's work in the same device launch when the
  * device-resident path runs; *filled = 0: the caller runs its own fill loop. */
 int tci_tci2_sweep2site_fillsolve(tci_tci2* tci, const tci_func* f, int32_t niter, int32_t iter1,

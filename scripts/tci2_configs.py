@@ -39,12 +39,12 @@ def run(name, f, localdims, initialpivots=None, oracle_ok=False, reps=None, **kw
     reps = REPS if reps is None else reps
     T.crossinterpolate2(f, localdims, initialpivots, **dict(kw, maxiter=1))  # warm the kernels
     wall, (tci, ranks, errors) = _timed(f, localdims, initialpivots, kw, reps)
-    res = {"config": name, "wall_s": round(wall, 4), "lazy_sitetensors": False, "iterations": len(ranks),
+    res = {"config": name, "wall_s": round(wall, 5), "lazy_sitetensors": False, "iterations": len(ranks),
            "ranks": ranks, "final_error": errors[-1], "linkdims": tci.linkdims(),
            "kwargs": {k: v for k, v in kw.items() if k != "rng"}}
     if kw.get("nsearchglobalpivot", 5) == 0:
         wl, (tl, rl, el) = _timed(f, localdims, initialpivots, dict(kw, lazy_sitetensors=True), reps)
-        res["wall_s_lazy"] = round(wl, 4)
+        res["wall_s_lazy"] = round(wl, 5)
         res["lazy_identical"] = bool(rl == ranks and list(el) == list(errors) and tl.linkdims() == tci.linkdims())
     if ORACLE and oracle_ok and kw.get("nsearchglobalpivot", 5) == 0:
         # the CPU oracle (1 core, deterministic mode) on the same integrand, initial pivots and kwargs
@@ -53,7 +53,7 @@ def run(name, f, localdims, initialpivots=None, oracle_ok=False, reps=None, **kw
         okw = {k: v for k, v in kw.items() if k in ("tolerance", "maxbonddim", "maxiter")}
         t0 = time.perf_counter()
         _, oranks, oerrors = O.crossinterpolate2(f.kind, f.params, localdims, initialpivots, **okw)
-        res["oracle_wall_s"] = round(time.perf_counter() - t0, 4)
+        res["oracle_wall_s"] = round(time.perf_counter() - t0, 5)
         res["oracle_ranks_equal"] = list(oranks) == list(ranks)
         res["oracle_final_error"] = oerrors[-1]
     return res

@@ -99,6 +99,12 @@ struct tci_ctx {
     char* sw_fmax = nullptr;     // the fill's per-site max |Pi1| bits (mapped host memory)
     char* sw_fmax_d = nullptr;
     size_t capSwFmax = 0;
+    char* sw_img[2] = {nullptr, nullptr};  // chained optimize!: the iterations' images (device, ping-pong)
+    size_t capSwImg[2] = {0, 0};
+    unsigned long long* sw_ctl = nullptr;  // chained optimize!: control words (SweepSmallArgs.ctl)
+    size_t capSwCtl = 0;
+    char* hctl = nullptr;                  // their pinned host copy
+    size_t capHctl = 0;
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
@@ -1226,7 +1232,9 @@ int tci_ctx_destroy(tci_ctx* c) {
     for (auto e : c->d2h_ev)
         if (e) hipEventDestroy(e);
     if (c->zbuf) hipHostFree(c->zbuf);
-    fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens); fr(c->sw_fmap);
+    fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens); fr(c->sw_fmap); fr(c->sw_img[0]); fr(c->sw_img[1]); fr(c->sw_ctl);
+    if (c->hctl) hipHostFree(c->hctl);
+    if (c->sw_fmax) hipHostFree(c->sw_fmax);
     if (c->sw_in) hipHostFree(c->sw_in);
     if (c->sw_out) hipHostFree(c->sw_out);
     if (c->hfn) hipHostFree(c->hfn);
@@ -2949,6 +2957,179 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
             HIPCHK(c, hipMemcpyAsync(s1->data, c->sw_tens + 2 * L, (size_t)used * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
+    return TCI_OK;
+}
+
+// Chained optimize! for the device-resident small sweep: the iterations of optimize!
+// (tensorci2.jl:1018-1172 with no global pivot search) as back-to-back launches that hand the state
+// over in device memory -- iteration i reads iteration i-1's output image, folds its fill maxima and
+// derives its abstol on the device, and records pivoterror / rank / the convergence test in ctl
+// (SweepSmallArgs) -- with one host synchronisation per chunk of iterations (the first chunk is
+// ncheckhistory long: no earlier iteration can converge), then the closing sweep1site! launch.
+// Launches after the stop return at once. Results:
+//   *ended = 1: the loop ended on the device at iteration *niter (converged or maxiter); with
+//     *s1done the closing sweep ran too (out = its image, tensors as tci_sweep_small_run mode 2;
+//     *errnorm = the maxsample it normalised with), else out = iteration *niter's image.
+//   *ended = 0: iteration *niter + 1 could not run on the device (a bond outgrew the workgroup, a NaN,
+//     a fill that does not fit): out = iteration *niter's image (empty when *niter = 0); the caller
+//     continues from there on the ordinary path, which raises the reference's errors.
+//   errors[i] / ranks[i], i = 1 .. *niter: pivoterror and rank after iteration i.
+// Iteration images carry the sweep's maxsample; the fill maxima are folded into `out`'s header here.
+int tci_sweep_small_optimize(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
+                             double tol, int norm, int maxiter, int ncheck, int strictlynested, int64_t maxbonddim,
+                             int fsolve, int64_t fill_tcap, const tci::SwSweep1* s1, std::vector<char>& out,
+                             int* niter, int* ended, int* s1done, double* errors, int64_t* ranks, double* errnorm) {
+    auto width = [&](int bank, int p) { return (bank & 1) ? L - 1 - p : p; };
+    const int64_t tot = 6 * cap * ((int64_t)L * (L - 1) / 2);
+    const tci::SwIO io = tci::sw_io(L);
+    const size_t outcap = io.sets + (size_t)tot * 4;
+    const size_t nctl = 8 + 2 * (size_t)tci::kSwOptMax;
+    *niter = 0;
+    *ended = 0;
+    *s1done = 0;
+    out.clear();
+    if (maxiter < 1 || maxiter >= tci::kSwOptMax || ncheck < 1) return set_err(c, TCI_ERR_ARG, "optimize chain: maxiter");
+    int st;
+    if ((st = ensure(c, &c->sw_ws, &c->capSwWs, (size_t)std::max<int64_t>(tot, 1)))) return st;
+    if ((st = ensure(c, &c->sw_inbuf, &c->capSwInbuf, inbytes))) return st;
+    for (int i = 0; i < 2; ++i)
+        if ((st = ensure(c, &c->sw_img[i], &c->capSwImg[i], outcap))) return st;
+    if ((st = ensure(c, &c->sw_ctl, &c->capSwCtl, nctl))) return st;
+    if ((st = ensure_pinned(c, &c->hctl, &c->capHctl, nctl * 8))) return st;
+    if ((st = ensure_mapped_pair(c, &c->sw_in, &c->sw_in_d, &c->capSwIn, inbytes))) return st;
+    if ((st = ensure_mapped_pair(c, &c->sw_out, &c->sw_out_d, &c->capSwOut, outcap))) return st;
+    if ((st = ensure(c, &c->sw_fmap, &c->capSwFmap, (size_t)(4 * L + 4)))) return st;
+    if ((st = ensure_mapped_pair(c, &c->sw_fmax, &c->sw_fmax_d, &c->capSwFmax, (size_t)L * 8))) return st;
+    const int64_t tcap = std::max<int64_t>(fsolve ? fill_tcap : 0, s1 && s1->tensors ? s1->tcap : 0);
+    if (tcap > 0 && (st = ensure(c, &c->sw_tens, &c->capSwTens, (size_t)(2 * L + tcap)))) return st;
+    memcpy(c->sw_in, in, inbytes);
+    HIPCHK(c, hipMemcpyAsync(c->sw_inbuf, c->sw_in, inbytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sw_ctl, 0, nctl * 8, c->stream));
+    unsigned long long* fmax_d = reinterpret_cast<unsigned long long*>(c->sw_fmax_d);
+    tci::SweepSmallArgs a;
+    a.f = f->view();
+    a.L = L;
+    a.ws = c->sw_ws;
+    a.cap = cap;
+    a.niter = 2;  // sweep2site!(tci, f, 2; iter1 = 1): one back-and-forth pair per iteration
+    a.iter1 = 1;
+    a.strategy = 0;
+    a.strictlynested = strictlynested;
+    a.abstol = 0.0;  // (derived on the device)
+    a.maxbonddim = maxbonddim;
+    a.mode = 0;
+    a.fill = 1;
+    a.fsolve = fsolve ? 1 : 0;
+    a.fmap = c->sw_fmap;
+    a.s1fwd = 0;
+    a.s1tens = 0;
+    a.reltol = 1e-14;
+    a.tens = fsolve ? c->sw_tens : nullptr;
+    a.tcap = fsolve ? fill_tcap : 0;
+    a.lu_wave = c->sw_lu_wave;
+    a.lazy_union = c->sw_lazy_union;
+    a.ctl = c->sw_ctl;
+    a.opt_maxiter = maxiter;
+    a.opt_ncheck = ncheck;
+    a.opt_norm = norm ? 1 : 0;
+    a.opt_tol = tol;
+    const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(c->hctl);
+    // the closing sweep1site! (mode 2), enqueued after every chunk: it runs only once the loop has
+    // ended (ctl[0] = 1), from the stop iteration's image, with that iteration's fill folded on the
+    // device -- so a loop that ends inside a chunk costs no further round trip
+    tci::SweepSmallArgs z = a;
+    if (s1) {
+        z.mode = 2;
+        z.fill = 0;
+        z.fsolve = 0;
+        z.fmap = nullptr;
+        z.opt_it = -1;
+        z.inbuf = c->sw_img[0];
+        z.img_sel[0] = c->sw_img[0];
+        z.img_sel[1] = c->sw_img[1];
+        z.out = c->sw_out_d;
+        z.fmax_in = fmax_d;
+        z.s1fwd = s1->forward;
+        z.s1tens = s1->tensors;
+        z.reltol = s1->reltol;
+        z.tens = s1->tensors ? c->sw_tens : nullptr;
+        z.tcap = s1->tensors ? s1->tcap : 0;
+    }
+    const char* prev = c->sw_inbuf;
+    int it = 1;
+    unsigned long long stop = 0, stop_it = 0;
+    while (it <= maxiter) {
+        const int chunk = it == 1 ? std::min(ncheck, maxiter) : std::min(2, maxiter - it + 1);
+        for (int j = 0; j < chunk; ++j, ++it) {
+            a.opt_it = it;
+            a.inbuf = prev;
+            a.out = c->sw_img[it & 1];
+            a.fmax_in = it > 1 ? fmax_d : nullptr;
+            HIPCHK(c, tci::launch_sweep_small(c->stream, a));
+            HIPCHK(c, tci::launch_fill_sites(c->stream, a, fmax_d));
+            prev = c->sw_img[it & 1];
+        }
+        if (s1) HIPCHK(c, tci::launch_sweep_small(c->stream, z));
+        HIPCHK(c, hipMemcpyAsync(c->hctl, c->sw_ctl, nctl * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        stop = hc[0];
+        stop_it = hc[1];
+        if (stop) break;
+    }
+    if (stop != 1 && stop != 2) return set_err(c, TCI_ERR_DEVICE, "optimize chain: no stop after maxiter");
+    const int n = stop == 1 ? (int)stop_it : (int)stop_it - 1;  // iterations completed on the device
+    for (int i = 1; i <= n; ++i) {
+        errors[i] = __builtin_bit_cast(double, hc[8 + i]);
+        ranks[i] = (int64_t)hc[8 + tci::kSwOptMax + i];
+    }
+    *niter = n;
+    // iteration n's image (device) -> out, with its fill's maxima folded into the header
+    auto take_iteration = [&]() -> int {
+        if (n == 0) return TCI_OK;
+        const char* img = c->sw_img[n & 1];
+        std::vector<char> head(io.sets);
+        HIPCHK(c, hipMemcpyAsync(head.data(), img, io.sets, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const int64_t* cn = reinterpret_cast<const int64_t*>(head.data() + io.counts);
+        size_t bytes = io.sets;
+        for (int b = 0; b < 4; ++b)
+            for (int p = 0; p < L; ++p) bytes += (size_t)cn[(size_t)b * L + p] * width(b, p) * 4;
+        if (bytes > outcap) return set_err(c, TCI_ERR_DEVICE, "optimize chain: image overflow");
+        out.assign(head.begin(), head.end());
+        out.resize(bytes);
+        if (bytes > io.sets)
+            HIPCHK(c, hipMemcpyAsync(out.data() + io.sets, img + io.sets, bytes - io.sets, hipMemcpyDeviceToHost,
+                                     c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        int64_t* hdr = reinterpret_cast<int64_t*>(out.data());
+        unsigned long long b = (unsigned long long)hdr[6] & 0x7fffffffffffffffull;
+        const unsigned long long* fm = reinterpret_cast<const unsigned long long*>(c->sw_fmax);
+        for (int q = 0; q < L; ++q) b = std::max(b, fm[q]);
+        hdr[6] = (int64_t)b;
+        return TCI_OK;
+    };
+    if (stop == 2) return take_iteration();
+    *ended = 1;
+    if (!s1) return take_iteration();
+    // (the closing sweep ran behind the chunk that stopped the loop)
+    *errnorm = __builtin_bit_cast(double, hc[2]);
+    const int64_t* hdr = reinterpret_cast<const int64_t*>(c->sw_out);
+    if (hdr[0] != 0) return take_iteration();  // the host loop runs sweep1site! (and raises its errors)
+    const int64_t* cn = reinterpret_cast<const int64_t*>(c->sw_out + io.counts);
+    size_t bytes = io.sets;
+    for (int b = 0; b < 4; ++b)
+        for (int p = 0; p < L; ++p) bytes += (size_t)cn[(size_t)b * L + p] * width(b, p) * 4;
+    if (bytes > outcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: output image overflow");
+    out.assign(c->sw_out, c->sw_out + bytes);
+    if (s1->tensors && s1->table) {
+        const int64_t used = hdr[10];
+        if (used < 0 || used > s1->tcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: tensor overflow");
+        HIPCHK(c, hipMemcpyAsync(s1->table, c->sw_tens, (size_t)(2 * L) * 8, hipMemcpyDeviceToHost, c->stream));
+        if (used > 0)
+            HIPCHK(c, hipMemcpyAsync(s1->data, c->sw_tens + 2 * L, (size_t)used * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    *s1done = 1;
     return TCI_OK;
 }
 

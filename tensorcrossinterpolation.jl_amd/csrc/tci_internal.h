@@ -426,7 +426,20 @@ struct SweepSmallArgs {
     int64_t tcap;          // mode 2 / fsolve: doubles available after the 2 L table entries
     int lu_wave = 1;       // bonds with m, n <= 32: the one-wave rrLU (sw_lu_wave; env TCI_SW_LUWAVE=0: off)
     int lazy_union = 1;    // mode 0: the union without materialising the kronecker products (env TCI_SW_LAZYU=0: off)
+    // Chained optimize! (tci_sweep_small_optimize): opt_it > 0, this launch is optimize! iteration
+    // opt_it (its abstol = opt_tol * maxsample, or opt_tol without normalizeerror); opt_it < 0, the
+    // closing sweep1site! (mode 2). ctl (device): [0] stop (0 running, 1 the loop ended -- converged or
+    // maxiter --, 2 iteration ctl[1] could not run on the device), [1] that iteration, [2] / [3] the
+    // closing sweep's errornormalization / abstol bits, [8 + i] / [8 + kSwOptMax + i] iteration i's
+    // pivot error bits / rank. A launch after the stop does nothing. fmax_in: the previous iteration's
+    // fill maxima, folded into maxsample first.
+    unsigned long long* ctl = nullptr;
+    const unsigned long long* fmax_in = nullptr;
+    int opt_it = 0, opt_maxiter = 0, opt_ncheck = 3, opt_norm = 1;
+    double opt_tol = 0.0;
+    const char* img_sel[2] = {nullptr, nullptr};  // the closing sweep: iteration i's image is img_sel[i & 1]
 };
+constexpr int kSwOptMax = 64;  // optimize! iterations a chain takes
 // sweep1site! on the device (mode 2): the host's request and where the site tensors go
 struct SwSweep1 {
     int forward, tensors;  // (a fill with the solve: forward unused, tensors = 1)

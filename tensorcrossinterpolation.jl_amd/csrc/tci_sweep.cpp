@@ -23,6 +23,10 @@ int tci_sweep_small_run(tci_ctx* c, const tci_func* f, int L, int64_t cap, const
                         int mode, int fill, int niter, int iter1, int strategy, int strictlynested, double abstol,
                         int64_t maxbonddim, std::vector<char>& out, const tci::SwSweep1* s1 = nullptr);
 int tci_sweep_small_error(tci_ctx* c, int status, int64_t bond);
+int tci_sweep_small_optimize(tci_ctx* c, const tci_func* f, int L, int64_t cap, const char* in, size_t inbytes,
+                             double tol, int norm, int maxiter, int ncheck, int strictlynested, int64_t maxbonddim,
+                             int fsolve, int64_t fill_tcap, const tci::SwSweep1* s1, std::vector<char>& out,
+                             int* niter, int* ended, int* s1done, double* errors, int64_t* ranks, double* errnorm);
 
 namespace {
 
@@ -462,6 +466,51 @@ int tci_tci2_sweep1site(tci_tci2* s, const tci_func* f, int32_t forward, double 
     const int64_t status = reinterpret_cast<const int64_t*>(out.data())[0];
     if (status != 0) return TCI_OK;  // the host loop redoes it (and raises the reference's errors)
     sw_unpack(s, out, 0);
+    *handled = 1;
+    return TCI_OK;
+}
+
+// optimize! (tensorci2.jl:1018-1172) without a global pivot search, as one chain of device launches
+// (tci_sweep_small_optimize): the sweep2site! iterations with fillsitetensors! after each (solved
+// when solvefill, else the maxsample update only), the convergence test on the device, then
+// sweep1site!(forward, abstol = tolerance * maxsample) with its site tensors. *handled: 0 nothing
+// done (state untouched); 1 with *ended = 1 and *s1done = 1 everything done; otherwise the state
+// after the first *niter iterations -- the caller continues the loop (*ended = 0) or runs the closing
+// sweep1site! (*ended = 1) on its own path. errors / ranks: iteration i at [i - 1]; *errnorm: the
+// maxsample the closing sweep normalised with.
+int tci_tci2_optimize_small(tci_tci2* s, const tci_func* f, double tolerance, int64_t maxbonddim, int32_t maxiter,
+                            int32_t ncheckhistory, int32_t normalizeerror, int32_t strictlynested, int32_t solvefill,
+                            double* tensors, int64_t capacity, int64_t* offsets, double* errors, int64_t* ranks,
+                            int32_t* niter, int32_t* ended, int32_t* s1done, double* errnorm, int* handled) {
+    if (!s || !f || !handled || !niter || !ended || !s1done || !errnorm || !errors || !ranks || !tensors ||
+        !offsets || capacity < 0)
+        return TCI_ERR_ARG;
+    *handled = 0;
+    *niter = *ended = *s1done = 0;
+    if (maxiter < 1 || maxiter >= tci::kSwOptMax || ncheckhistory < 1 || !tci_sweep_small_ok(s->ctx, f, s->L))
+        return TCI_OK;
+    const std::vector<char> in = sw_pack(s);
+    std::vector<char> out;
+    for (int i = 0; i < 2 * s->L; ++i) offsets[i] = 0;
+    const tci::SwSweep1 s1{1, 1, 1e-14, capacity, offsets, tensors};
+    std::vector<double> e(tci::kSwOptMax + 1, 0.0);
+    std::vector<int64_t> r(tci::kSwOptMax + 1, 0);
+    int n = 0, en = 0, sd = 0;
+    double norm = 0.0;
+    int st = tci_sweep_small_optimize(s->ctx, f, s->L, sw_capacity(s), in.data(), in.size(), tolerance,
+                                      normalizeerror, maxiter, ncheckhistory, strictlynested, maxbonddim, solvefill,
+                                      capacity, &s1, out, &n, &en, &sd, e.data(), r.data(), &norm);
+    if (st) return st;
+    if (n == 0 && !en) return TCI_OK;  // nothing ran on the device
+    sw_unpack(s, out, 0);
+    for (int i = 0; i < n; ++i) {
+        errors[i] = e[i + 1];
+        ranks[i] = r[i + 1];
+    }
+    *niter = n;
+    *ended = en;
+    *s1done = sd;
+    *errnorm = norm;
     *handled = 1;
     return TCI_OK;
 }

@@ -838,6 +838,13 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     const double* p = f.params;
     const double p0 = (KIND == F_SUM || KIND == F_TABLE) ? 0.0 : p[0];
     const SwIO io = sw_io(L);
+    if (a.ctl) {  // chained optimize!: nothing after the stop (the closing sweep only after a clean end)
+        const unsigned long long stop = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.opt_it > 0 ? stop != 0 : stop != 1) {
+            if (tid == 0 && a.fmap) a.fmap[0] = 0;
+            return;
+        }
+    }
 #ifdef TCI_SW_PROF
     unsigned long long lu_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define SWP_ACC lu_acc
@@ -898,11 +905,16 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
         }
     };
 
-    // ---- input (DMA'd to a.inbuf by the host): header, counts, bond errors, the four banks
-    if (tid < 16) hdr[tid] = reinterpret_cast<const int64_t*>(a.inbuf)[tid];
+    // ---- input (DMA'd to a.inbuf by the host): header, counts, bond errors, the four banks. The
+    // closing sweep of a chain, enqueued before the host knows where the loop stops, takes the image
+    // of the stop iteration ctl[1] (iteration i's image is img_sel[i & 1]).
+    const char* inb = a.inbuf;
+    if (a.ctl && a.opt_it < 0 && a.img_sel[0])
+        inb = a.img_sel[__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1];
+    if (tid < 16) hdr[tid] = reinterpret_cast<const int64_t*>(inb)[tid];
     for (int i = tid; i < 6 * L; i += kSwThreads)
-        cnt[(i / L) * kSwMaxL + i % L] = i < 4 * L ? (int)reinterpret_cast<const int64_t*>(a.inbuf + io.counts)[i] : 0;
-    for (int i = tid; i < L - 1; i += kSwThreads) bonderr[i] = reinterpret_cast<const double*>(a.inbuf + io.bonderr)[i];
+        cnt[(i / L) * kSwMaxL + i % L] = i < 4 * L ? (int)reinterpret_cast<const int64_t*>(inb + io.counts)[i] : 0;
+    for (int i = tid; i < L - 1; i += kSwThreads) bonderr[i] = reinterpret_cast<const double*>(inb + io.bonderr)[i];
     for (int i = tid; i < L; i += kSwThreads) {
         ldm[i] = f.localdims[i];
         for (int k = 0; k < 2; ++k)
@@ -910,13 +922,27 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
     }
     __syncthreads();
     {
-        const int32_t* src = reinterpret_cast<const int32_t*>(a.inbuf + io.sets);
+        const int32_t* src = reinterpret_cast<const int32_t*>(inb + io.sets);
         copy_segments(
             4 * L, [&](int i) { return cnt[(i / L) * kSwMaxL + i % L] * width(i / L, i % L); },
             [&](int, int off) { return src + off; }, [&](int i, int) { return bank_ptr(i / L, i % L); });
     }
     int has_history = (int)hdr[3];
     double maxsample = __longlong_as_double((long long)hdr[6]);
+    if (a.fmax_in) {  // chained: the previous iteration's fill (|v| bits: Julia's NaN-propagating max)
+        unsigned long long mb = (unsigned long long)hdr[6] & 0x7fffffffffffffffull;
+        for (int q = 0; q < L; ++q) {
+            const unsigned long long v = a.fmax_in[q];
+            mb = v > mb ? v : mb;
+        }
+        maxsample = __longlong_as_double((long long)mb);
+    }
+    // optimize!'s abstol = tol * errornormalization (tensorci2.jl:1049-1050) in a chain
+    const double abstol = a.ctl ? (a.opt_norm ? a.opt_tol * maxsample : a.opt_tol) : a.abstol;
+    if (a.ctl && a.opt_it < 0 && tid == 0) {
+        a.ctl[2] = (unsigned long long)__double_as_longlong(maxsample);
+        a.ctl[3] = (unsigned long long)__double_as_longlong(abstol);
+    }
     int npe = 0;
     int status = 0, s_it = 0, s_q = 0, esite = 0, extra_valid = 0, fstatus = -1, fsite = 0;
     __syncthreads();
@@ -1155,13 +1181,13 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
                 int* cp = perm + m;
                 int np, fl;
                 if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {  // one-wave rrLU
-                    np = sw_lu_wave_any(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                    np = sw_lu_wave_any(S, ldS, m, n, mr, 1e-14, abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                     &nanflag, &dslot, error, maxerror, fl, false, SWP_ACC);
                 } else if (m <= kSwRegN && n <= kSwRegN) {  // register-tile rrLU, its tile read from S
-                    np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                    np = sw_lu_regs(S, ldS, m, n, mr, 1e-14, abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                     &nanflag, &dslot, error, maxerror, fl, SWP_ACC);
                 } else {
-                    np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, 1e-14, a.abstol, fwd ? 1 : 0, rp, cp, red, xy,
+                    np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, 1e-14, abstol, fwd ? 1 : 0, rp, cp, red, xy,
                                                    xy + m, pvl, error, maxerror);
                     fl = small_lu_nanflags<kSwThreads>(S, ldS, m, n, np, &nanflag);
                 }
@@ -1351,13 +1377,13 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
             int* cp = perm + m;
             int np, fl;
             if (m <= kSwWaveN && n <= kSwWaveN && a.lu_wave) {
-                np = sw_lu_wave_any(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                np = sw_lu_wave_any(S, ldS, m, n, mr, a.reltol, abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                 &nanflag, &dslot, error, maxerror, fl, a.s1tens != 0);
             } else if (m <= kSwRegN && n <= kSwRegN) {
-                np = sw_lu_regs(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
+                np = sw_lu_regs(S, ldS, m, n, mr, a.reltol, abstol, fwd ? 1 : 0, rp, cp, xy, xy + kSwRegN, red, pvl,
                                 &nanflag, &dslot, error, maxerror, fl, SWP_ACC, a.s1tens != 0);
             } else {
-                np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, a.reltol, a.abstol, fwd ? 1 : 0, rp, cp, red, xy,
+                np = small_lu_core<kSwThreads>(S, ldS, m, n, mr, a.reltol, abstol, fwd ? 1 : 0, rp, cp, red, xy,
                                                xy + m, pvl, error, maxerror);
                 fl = small_lu_nanflags<kSwThreads>(S, ldS, m, n, np, &nanflag);
             }
@@ -1514,6 +1540,40 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_small(SweepSmallArgs a) {
         }
     } else if (tid == 0 && a.fmap) {
         a.fmap[0] = 0;  // (no fill: k_fill_sites does nothing)
+    }
+    if (a.ctl && a.opt_it > 0 && tid == 0) {
+        // chained optimize!: errors[it] = pivoterror(tci) (maxbonderror, tensorci2.jl:223-232), ranks[it]
+        // = rank(tci) (max linkdims), then convergencecriterion (tensorci2.jl:947-966) over the last
+        // ncheckhistory iterations with this iteration's abstol (no global pivots are added)
+        const int it = a.opt_it;
+        if (status != 0 || fstatus != 0) {
+            a.ctl[1] = (unsigned long long)it;
+            a.ctl[0] = 2;
+        } else {
+            double e = bonderr[0];
+            for (int b = 1; b < L - 1; ++b) e = jl_max(e, bonderr[b]);
+            int rk = 0;
+            for (int b = 1; b < L; ++b) rk = max(rk, set_cnt(0, 0, b));
+            a.ctl[8 + it] = (unsigned long long)__double_as_longlong(e);
+            a.ctl[8 + kSwOptMax + it] = (unsigned long long)rk;
+            bool conv = false;
+            if (it >= a.opt_ncheck) {
+                bool allerr = true, allmax = true;
+                int mn = rk;
+                for (int j = it - a.opt_ncheck + 1; j <= it; ++j) {
+                    const double ej = __longlong_as_double((long long)a.ctl[8 + j]);
+                    const int rj = (int)a.ctl[8 + kSwOptMax + j];
+                    allerr = allerr && ej < abstol;
+                    mn = min(mn, rj);
+                    allmax = allmax && (int64_t)rj >= a.maxbonddim;
+                }
+                conv = (allerr && mn == rk) || allmax;
+            }
+            if (conv || it >= a.opt_maxiter) {
+                a.ctl[1] = (unsigned long long)it;
+                a.ctl[0] = 1;
+            }
+        }
     }
     __syncthreads();
 

@@ -118,6 +118,9 @@ SIGNATURES = {
     "tci_tci2_get_sets": ([vp, C.c_int, vp, vp, i64], C.c_int),
     "tci_tci2_fill_maxsample": ([vp, vp, C.POINTER(C.c_int)], C.c_int),
     "tci_tci2_fill_solve": ([vp, vp, vp, i64, vp, C.POINTER(C.c_int)], C.c_int),
+    "tci_tci2_optimize_small": ([vp, vp, dbl, i64, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_double), C.POINTER(C.c_int)], C.c_int),
     "tci_tci2_sweep2site_fillsolve": ([vp, vp, i32, i32, dbl, i64, i32, i32, vp, i64, vp, C.POINTER(C.c_int)],
                                       C.c_int),
     "tci_tci2_sweep2site_fill": ([vp, vp, i32, i32, dbl, i64, i32, i32, C.POINTER(C.c_int)], C.c_int),

@@ -11,6 +11,8 @@ are (count, width) int32 arrays of 1-based local indices.
 """
 import contextlib
 import ctypes as C
+import os
+
 import numpy as np
 
 from . import _lib
@@ -470,6 +472,42 @@ class TensorCI2:
             self._native_set_tensors(tens, offs)
         return True
 
+    def _optimize_native(self, f, tol, maxbonddim, maxiter, ncheckhistory, normalizeerror, strictlynested, lazy):
+        """optimize!'s loop and closing sweep1site! as one chain of device launches
+        (tci_tci2_optimize_small). None when nothing ran on the device; else (iterations done, their
+        errors, their ranks, loop ended, closing sweep done, the maxsample it normalised with)."""
+        ctx = f.ctx
+        lib = ctx.lib
+        n = len(self)
+        h = self._native_handle(ctx)
+        self._native_push(ctx, h)
+        cap = n * 16384
+        tens = np.empty(cap)
+        offs = np.zeros(2 * n, np.int64)
+        errs = np.zeros(maxiter)
+        rks = np.zeros(maxiter, np.int64)
+        nd, ended, s1done = C.c_int32(), C.c_int32(), C.c_int32()
+        errnorm, handled = C.c_double(), C.c_int(0)
+        with self._native_failure_sync(ctx, h, hist=True):
+            ctx.check(lib.tci_tci2_optimize_small(h, f.h, float(tol), int(min(maxbonddim, INT64_MAX)), int(maxiter),
+                                                  int(ncheckhistory), int(bool(normalizeerror)),
+                                                  int(bool(strictlynested)), int(not lazy),
+                                                  tens.ctypes.data_as(C.c_void_p), cap,
+                                                  offs.ctypes.data_as(C.c_void_p), errs.ctypes.data_as(C.c_void_p),
+                                                  rks.ctypes.data_as(C.c_void_p), C.byref(nd), C.byref(ended),
+                                                  C.byref(s1done), C.byref(errnorm), C.byref(handled)))
+        if not handled.value:
+            return None
+        k = nd.value
+        if k > 0:
+            self._native_has_hist = True
+        self._native_pull(ctx, h)
+        self.invalidatesitetensors()
+        if s1done.value:
+            self._native_set_tensors(tens, offs)
+        return (k, [float(x) for x in errs[:k]], [int(x) for x in rks[:k]], bool(ended.value), bool(s1done.value),
+                float(errnorm.value))
+
     def _native_set_tensors(self, tens, offs):
         """setsitetensor! for every site from a native fill's packed output: the shapes from the
         native set counts, so the (still native-side) index sets are neither pulled nor marked as
@@ -677,7 +715,26 @@ class TensorCI2:
         # with no search they are unobservable (sweep1site! below rebuilds all of them).
         searches = getattr(finder, "nsearch", 1) > 0
         lazy = bool(lazy_sitetensors) and not searches
-        for it in range(1, maxiter + 1):
+        it0, loop_done = 1, False
+        if (OPTIMIZE_CHAIN and NATIVE_SWEEP and _native_ok(f) and not searches and sweepstrategy == "backandforth"
+                and pivotsearch == "full" and verbosity == 0 and 1 <= maxiter < 64 and ncheckhistory >= 1):
+            # the whole loop (and sweep1site!) as one chain of device launches when every bond fits
+            # the device-resident small sweep; the same iterations, tests and results as below
+            r = self._optimize_native(f, tol, maxbonddim, maxiter, ncheckhistory, normalizeerror, strictlynested,
+                                      lazy)
+            if r is not None:
+                nd, errs_d, rks_d, ended, s1done, errnorm = r
+                errors.extend(errs_d)
+                ranks.extend(rks_d)
+                nglobalpivots.extend([0] * nd)
+                if s1done:
+                    self._sanitycheck()
+                    en = errnorm if normalizeerror else 1.0
+                    return ranks, [e / en for e in errors]
+                it0, loop_done = nd + 1, ended
+        for it in range(it0, maxiter + 1):
+            if loop_done:
+                break
             errornormalization = self.maxsamplevalue if normalizeerror else 1.0
             abstol = tol * errornormalization
             self.sweep2site(f, 2, iter1=1, abstol=abstol, maxbonddim=maxbonddim, pivotsearch=pivotsearch,
@@ -782,6 +839,9 @@ class _NativeTCI2:
 
 # the native per-bond loop for device integrands (set False to run sweep2site's Python loop)
 NATIVE_SWEEP = True
+# optimize!'s whole loop as one chain of device launches where the small sweep takes every bond
+# (set False, or TCI_OPT_CHAIN=0, for the per-iteration native calls)
+OPTIMIZE_CHAIN = os.environ.get("TCI_OPT_CHAIN", "1") != "0"
 
 
 def _ctx_of(f):
