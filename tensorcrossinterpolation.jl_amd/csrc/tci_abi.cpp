@@ -105,6 +105,9 @@ struct tci_ctx {
     size_t capSwCtl = 0;
     char* hctl = nullptr;                  // their pinned host copy
     size_t capHctl = 0;
+    char* sw_s1t = nullptr;                // chained optimize!: the closing sweep's site tensors (mapped host)
+    char* sw_s1t_d = nullptr;
+    size_t capSwS1t = 0;
     size_t capZ = 0;
     int* hflag = nullptr;  // pinned
     RrluState* hpoll = nullptr;  // pinned, two slots: rrLU stop-flag polling (StopPoll)
@@ -1234,6 +1237,7 @@ int tci_ctx_destroy(tci_ctx* c) {
     if (c->zbuf) hipHostFree(c->zbuf);
     fr(c->sw_ws); fr(c->sw_inbuf); fr(c->sw_tens); fr(c->sw_fmap); fr(c->sw_img[0]); fr(c->sw_img[1]); fr(c->sw_ctl);
     if (c->hctl) hipHostFree(c->hctl);
+    if (c->sw_s1t) hipHostFree(c->sw_s1t);
     if (c->sw_fmax) hipHostFree(c->sw_fmax);
     if (c->sw_in) hipHostFree(c->sw_in);
     if (c->sw_out) hipHostFree(c->sw_out);
@@ -3000,8 +3004,13 @@ int tci_sweep_small_optimize(tci_ctx* c, const tci_func* f, int L, int64_t cap, 
     if ((st = ensure_mapped_pair(c, &c->sw_out, &c->sw_out_d, &c->capSwOut, outcap))) return st;
     if ((st = ensure(c, &c->sw_fmap, &c->capSwFmap, (size_t)(4 * L + 4)))) return st;
     if ((st = ensure_mapped_pair(c, &c->sw_fmax, &c->sw_fmax_d, &c->capSwFmax, (size_t)L * 8))) return st;
-    const int64_t tcap = std::max<int64_t>(fsolve ? fill_tcap : 0, s1 && s1->tensors ? s1->tcap : 0);
-    if (tcap > 0 && (st = ensure(c, &c->sw_tens, &c->capSwTens, (size_t)(2 * L + tcap)))) return st;
+    if (fsolve && fill_tcap > 0 && (st = ensure(c, &c->sw_tens, &c->capSwTens, (size_t)(2 * L + fill_tcap))))
+        return st;
+    // the closing sweep writes its (small) site tensors straight into mapped host memory: no copy
+    // and no second synchronisation after the chain
+    if (s1 && s1->tensors &&
+        (st = ensure_mapped_pair(c, &c->sw_s1t, &c->sw_s1t_d, &c->capSwS1t, (size_t)(2 * L + s1->tcap) * 8)))
+        return st;
     memcpy(c->sw_in, in, inbytes);
     HIPCHK(c, hipMemcpyAsync(c->sw_inbuf, c->sw_in, inbytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->sw_ctl, 0, nctl * 8, c->stream));
@@ -3052,7 +3061,7 @@ int tci_sweep_small_optimize(tci_ctx* c, const tci_func* f, int L, int64_t cap, 
         z.s1fwd = s1->forward;
         z.s1tens = s1->tensors;
         z.reltol = s1->reltol;
-        z.tens = s1->tensors ? c->sw_tens : nullptr;
+        z.tens = s1->tensors ? reinterpret_cast<double*>(c->sw_s1t_d) : nullptr;
         z.tcap = s1->tensors ? s1->tcap : 0;
     }
     const char* prev = c->sw_inbuf;
@@ -3124,10 +3133,9 @@ int tci_sweep_small_optimize(tci_ctx* c, const tci_func* f, int L, int64_t cap, 
     if (s1->tensors && s1->table) {
         const int64_t used = hdr[10];
         if (used < 0 || used > s1->tcap) return set_err(c, TCI_ERR_DEVICE, "device sweep: tensor overflow");
-        HIPCHK(c, hipMemcpyAsync(s1->table, c->sw_tens, (size_t)(2 * L) * 8, hipMemcpyDeviceToHost, c->stream));
-        if (used > 0)
-            HIPCHK(c, hipMemcpyAsync(s1->data, c->sw_tens + 2 * L, (size_t)used * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const double* tm = reinterpret_cast<const double*>(c->sw_s1t);
+        memcpy(s1->table, tm, (size_t)(2 * L) * 8);
+        if (used > 0) memcpy(s1->data, tm + 2 * L, (size_t)used * 8);
     }
     *s1done = 1;
     return TCI_OK;

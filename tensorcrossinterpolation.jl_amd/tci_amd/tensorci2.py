@@ -758,9 +758,15 @@ class TensorCI2:
         return ranks, [e / errornormalization for e in errors]
 
     def _sanitycheck(self):
-        """_sanitycheck (globalsearch.jl:226-233)."""
-        for b in range(1, len(self)):
-            if len(self.Iset[b]) != len(self.Jset[b - 1]):
+        """_sanitycheck (globalsearch.jl:226-233). (With the sets still native-side, their counts
+        are read without pulling the sets.)"""
+        if self._py_stale:
+            nI, nJ = self._native_counts(0), self._native_counts(1)
+            lens = [(int(nI[b]), int(nJ[b - 1])) for b in range(1, len(self))]
+        else:
+            lens = [(len(self.Iset[b]), len(self.Jset[b - 1])) for b in range(1, len(self))]
+        for b, (i, j) in enumerate(lens, start=1):
+            if i != j:
                 raise RuntimeError(f"Pivot matrix at bond {b} is not square!")
         return True
 
