@@ -14,14 +14,6 @@ from tci_amd import tensorci2 as T2  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _gpu():
-    import torch
-
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-
-
 def _run(chain, make, ld, p0, kw):
     old = T2.OPTIMIZE_CHAIN
     T2.OPTIMIZE_CHAIN = chain
