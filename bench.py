@@ -822,7 +822,11 @@ def dense_extras(T, ctx, only_k3=False):
         Pi1.fill_uniform(seed=7)
         Tm = T.DeviceMatrix(R, r, ctx=ctx, ld=R)
         rec = {"r": r, "R": R}
-        for tag, mask in (("mfma", 15), ("mfma_lds_panel", 7), ("round1_scalar", 0), ("mfma_getrs_only", 4)):
+        # mfma: the default (31: one cooperative getrf launch for r <= 1024); mfma_r5: round 5's
+        # form (15: four launches per panel); mfma_lds_panel / round1_scalar / mfma_getrs_only:
+        # older A/B points
+        for tag, mask in (("mfma", 31), ("mfma_r5", 15), ("mfma_lds_panel", 7), ("round1_scalar", 0),
+                          ("mfma_getrs_only", 4)):
             ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
             P.copy_from(P0)
             T.sitetensor_solve_device(P, Pi1, Tm)
@@ -836,7 +840,7 @@ def dense_extras(T, ctx, only_k3=False):
             fl = 2.0 / 3.0 * r ** 3 + 2.0 * R * r * r
             rec[tag] = {"ms": round(sec * 1e3, 3), "TFLOPs": round(fl / sec / 1e12, 2),
                         "frac_of_spec": round(fl / sec / 1e12 / MFMA_F64_SPEC_TFLOPS, 4)}
-        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
         solves.append(rec)
         for x in (P0, P, Pi1, Tm):
             x.free()
@@ -851,14 +855,14 @@ def dense_extras(T, ctx, only_k3=False):
         # GEMM with K = np over the full np x n (or m x np) block + TRSM m np^2 (or n np^2)
         fl = 2.0 * npv * npv * 8192 + 1.0 * (8192 - npv) * npv * npv
         rec = {"m": 8192, "n": 8192, "np": npv, "leftorthogonal": lo}
-        for tag, mask in (("mfma", 15), ("round1_scalar", 0)):
+        for tag, mask in (("mfma", 31), ("round1_scalar", 0)):
             ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
             ctx.set_timing(True)
             T.MatrixLUCI(Ah, maxrank=npv, leftorthogonal=lo, ctx=ctx).left()
             kms, kn = ctx.kernel_stats(21)
             ctx.set_timing(False)
             rec[tag] = {"ms": round(kms / max(kn, 1), 3), "TFLOPs": round(fl / (kms / max(kn, 1) * 1e-3) / 1e12, 2)}
-        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
         lucis.append(rec)
     out["luci_factors_k4"] = lucis
     return out

@@ -158,10 +158,11 @@ int tci_rrlu_shadow_bytes(void);
 int tci_set_c128_shadow(tci_ctx* ctx, int enabled);
 
 /* fp64 MFMA forms of the MatrixLUCI factors (bit 1), the site-tensor getrf
- * (bit 2) and getrs (bit 4), and the getrf's panels held in registers (bit 8; without it the
- * panels are factorised in LDS -- bitwise the same factors); default 15 (env TCI_DENSE_MFMA). 0
- * restores the round-1 scalar kernels (A/B). Factors / solutions agree to the parity tolerances
- * either way. */
+ * (bit 2) and getrs (bit 4), the getrf's panels held in registers (bit 8; without it the
+ * panels are factorised in LDS -- bitwise the same factors) and the getrf as one cooperative
+ * launch for r <= 1024 (bit 16, with bits 2 and 8; without it: four launches per panel); default
+ * 31 (env TCI_DENSE_MFMA). 0 restores the round-1 scalar kernels
+ * (A/B). Factors / solutions agree to the parity tolerances either way. */
 int tci_set_dense_mfma(tci_ctx* ctx, int mask);
 
 /* ------------------------------------------------------------ integrands */

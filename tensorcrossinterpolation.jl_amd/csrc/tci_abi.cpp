@@ -142,6 +142,10 @@ struct tci_ctx {
     size_t capDiag = 0;
     int* dPiv = nullptr;
     size_t capPiv = 0;
+    double* dPbak = nullptr;  // P kept for a cooperative getrf that gave up (solve_launch)
+    size_t capPbak = 0;
+    int* hCoop = nullptr;     // pinned: the fault word read back
+    int coop_faults = 0;      // cooperative getrfs that gave up (diagnostic)
     // rrLU results (tci_rrlu.hip): position maps, pivot values, physical-order L / U, and the
     // position-order L / U extracted from them
     int32_t* rowpos = nullptr;
@@ -1218,9 +1222,10 @@ int tci_ctx_destroy(tci_ctx* c) {
     fr(c->ticket); fr(c->esync); fr(c->bar); fr(c->fault); fr(c->colbuf);
     fr(c->maxbits); fr(c->scratch); fr(c->scratch2); fr(c->dI); fr(c->dJ); fr(c->dI2); fr(c->dF1); fr(c->dF2);
     fr(c->dDiag);
-    fr(c->dPiv); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
+    fr(c->dPiv); fr(c->dPbak); fr(c->rowpos); fr(c->colpos); fr(c->pivv); fr(c->Lp); fr(c->Up); fr(c->dL);
     fr(c->dU); fr(c->cws); fr(c->dRe); fr(c->colposL); fr(c->shsend); fr(c->shrecv); fr(c->lout);
     if (c->hst) hipHostFree(c->hst);
+    if (c->hCoop) hipHostFree(c->hCoop);
     if (c->hflag) hipHostFree(c->hflag);
     if (c->hpoll) hipHostFree(c->hpoll);
     for (auto e : c->pollev)
@@ -2174,6 +2179,34 @@ int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int6
                         want_factors ? left : nullptr, want_factors ? right : nullptr);
 }
 
+
+// setsitetensor!'s solve on device buffers (piv: c->dPiv, 2 r + 2 ints). The cooperative getrf
+// (tci_dense.hip k_getrf_coop) needs its workgroups co-resident; if one of them waited past its
+// timeout (another stream or process holding the CUs) every workgroup left and the fault word is
+// set: the solve is then redone from a copy of P on the launch-per-panel path. One host
+// synchronisation more per cooperative solve (the fault word), ~10 us against ms of solve.
+static int solve_launch(tci_ctx* c, double* P, int64_t r, double* Pi1, int64_t R, double* T) {
+    const int coopmask = tci::kDenseGetrf | tci::kDenseGetrfReg | tci::kDenseGetrfCoop;
+    const bool coop = (c->dense & coopmask) == coopmask && tci::getrf_coop_fits((int)r);
+    int st;
+    if (coop) {
+        if ((st = ensure(c, &c->dPbak, &c->capPbak, (size_t)(r * r)))) return st;
+        if (!c->hCoop) HIPCHK(c, hipHostMalloc((void**)&c->hCoop, 64, hipHostMallocDefault));
+        HIPCHK(c, hipMemcpyAsync(c->dPbak, P, (size_t)(r * r) * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    }
+    tci::launch_sitetensor_solve(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense);
+    HIPCHK(c, hipGetLastError());
+    if (!coop) return TCI_OK;
+    HIPCHK(c, hipMemcpyAsync(c->hCoop, c->dPiv + 2 * r + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (*c->hCoop == 0) return TCI_OK;
+    ++c->coop_faults;
+    HIPCHK(c, hipMemcpyAsync(P, c->dPbak, (size_t)(r * r) * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    tci::launch_sitetensor_solve(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense & ~tci::kDenseGetrfCoop);
+    HIPCHK(c, hipGetLastError());
+    return TCI_OK;
+}
+
 int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t nIb, int32_t wI,
                      const int32_t* Jb, int64_t nJb, int32_t wJ, const int32_t* Inext,
                      int64_t nInext, double* T, double* maxabs) {
@@ -2203,7 +2236,7 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
         // Pi1), tensorci2.jl:609), and each evaluation resets c->maxbits
         if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
         if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
-        if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
+        if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r + 2)))) return st;
         if ((st = ensure(c, &c->dI2, &c->capI2, (size_t)std::max<int64_t>(nInext * (wI + 1), 1))))
             return st;
         if (bn)
@@ -2214,9 +2247,8 @@ int tci_sitetensor_h(tci_ctx* c, const tci_func* f, const int32_t* Ib, int64_t n
     if ((st = batcheval_launch(c, f, c->dI, nIb, wI, c->dJ, nJb, wJ, 1, c->dF1, ldR))) return st;
     if (solve) {
         ev_begin(c, 20);
-        tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv, c->dense);
+        if ((st = solve_launch(c, c->dF2, r, c->dF1, R, c->dA))) return st;
         ev_end(c);
-        HIPCHK(c, hipGetLastError());
     }
     // maxabs through the pinned stage, T by d2h_large (chunked through pinned slots, host copy threaded)
     const size_t bt = (size_t)(R * nJb) * 8;
@@ -2240,13 +2272,12 @@ int tci_sitetensor_solve_h(tci_ctx* c, const double* P, int64_t r, const double*
     if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(r * r)))) return st;
     if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(R * r)))) return st;
     if ((st = ensure(c, &c->dA, &c->capA, (size_t)(R * r)))) return st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r + 2)))) return st;
     HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * sizeof(double), hipMemcpyHostToDevice, c->stream));
     ev_begin(c, 20);
-    tci::launch_sitetensor_solve(c->stream, c->dF2, (int)r, c->dF1, (int)R, c->dA, c->dPiv, c->dense);
+    if ((st = solve_launch(c, c->dF2, r, c->dF1, R, c->dA))) return st;
     ev_end(c);
-    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(T, c->dA, R * r * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
@@ -2281,11 +2312,10 @@ int tci_sitetensor_solve_d(tci_ctx* c, double* d_P, int64_t r, const double* d_P
     if (r > INT32_MAX / 2 || R > INT32_MAX / 2 || r * R > INT32_MAX * 64LL)
         return set_err(c, TCI_ERR_ARG, "matrix too large");
     int st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r + 2)))) return st;
     ev_begin(c, 20);
-    tci::launch_sitetensor_solve(c->stream, d_P, (int)r, const_cast<double*>(d_Pi1), (int)R, d_T, c->dPiv, c->dense);
+    if ((st = solve_launch(c, d_P, r, const_cast<double*>(d_Pi1), R, d_T))) return st;
     ev_end(c);
-    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return TCI_OK;
 }
@@ -2438,7 +2468,7 @@ int tci_sitetensor_solve_c128_h(tci_ctx* c, const double* P, int64_t r, const do
     if ((st = ensure(c, &c->dF2, &c->capF2, (size_t)(2 * r * r)))) return st;
     if ((st = ensure(c, &c->dF1, &c->capF1, (size_t)(2 * R * r)))) return st;
     if ((st = ensure(c, &c->dA, &c->capA, (size_t)(2 * (R * r + r * r))))) return st;
-    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r)))) return st;
+    if ((st = ensure(c, &c->dPiv, &c->capPiv, (size_t)(2 * r + 2)))) return st;
     HIPCHK(c, hipMemcpyAsync(c->dF2, P, r * r * 16, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->dF1, Pi1, R * r * 16, hipMemcpyHostToDevice, c->stream));
     double2* dT = reinterpret_cast<double2*>(c->dA);

@@ -244,6 +244,7 @@ void launch_dgemm(hipStream_t s, bool tb, int m, int n, int k, double alpha, con
     else dgemm_go<false>(s, g);
 }
 
+
 // ------------------------------------------------------------- diagonal-block triangular solve
 // For every right-hand side q < nrhs, the nb-vector x_q(j) = X[q * rs + j * es] (j < nb <= NB) is
 // replaced by the solution of its nb x nb triangular system, M(j, t) = Mb[j * mj + t * mt]:
@@ -765,6 +766,304 @@ void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv, bool reg) {
                          A + je + (int64_t)je * r, r, nullptr, nullptr);
         jb = je;
     }
+}
+
+// Round 6: the whole getrf (rows <= 1024) as ONE cooperative launch. launch_getrf_blocked issues
+// four dependent launches per 24-column panel (panel, interchanges, U12 solve, K = 24 update): at
+// r = 1024 that is 172 launches and ~6.5 ms, of which the panels' own column steps are ~2. Here G
+// workgroups (one per 8-column block group, at most 64, all co-resident) loop over the panels:
+//  1. every workgroup loads the panel (rows jb..r-1) and factorises it in registers with the
+//     k_getrf_panel_reg column step -- redundantly, bitwise the same everywhere, so no hand-off of
+//     the factored panel is needed;
+//  2. workgroup 0 stores the interchanges;
+//  3. each workgroup applies the panel to the 8-column blocks it owns (block b: workgroup b mod G):
+//     blocks left of the panel take the composed interchanges (<= 48 rows); blocks right of it are
+//     staged in LDS, permuted, their U12 rows solved against L11 (column-oriented substitution, one
+//     wave per column, readlane broadcasts) and their rows below updated by L21 U12 with L21 still
+//     in the registers of step 1 (sequential separate multiply and subtract);
+//  4. one grid barrier (release fence, agent counter, acquire fence: MI355X_MICROARCH.md's
+//     barrier-counter row) before the next panel reads its columns;
+//  5. the owners of the panel's column blocks store them (after the barrier: every workgroup has
+//     read the panel by then).
+// Same pivot rule and panel arithmetic as the blocked path; the trailing updates sum in another
+// order than K3's MFMAs (rounding). Co-residency is not assumed blindly: a workgroup that waits
+// more than 4 ms for the others sets the fault word and every workgroup leaves; the host then
+// redoes the solve from a copy of P on the launch-per-panel path (tci_abi.cpp solve_launch).
+constexpr int kCoopNBP = 24, kCoopRPT = 4, kCoopNT = 256, kCoopCW = 8, kCoopMaxG = 64;
+
+bool getrf_coop_fits(int r) { return r >= 1 && r <= kCoopNT * kCoopRPT; }
+
+// Cross-workgroup data of the cooperative getrf is stored and loaded write-through (agent-scope
+// relaxed atomics: global_store / global_load sc1), so the barrier needs no L2 write-back: every
+// wave drains its stores, one lane adds to the counter, polls it, and invalidates the CU's L1
+// (MI355X_MICROARCH.md hand-off table, row 1, with the acquire kept). The release fence of round
+// 6's first build (buffer_wbl2 from every workgroup) made the barrier ~32 us per panel.
+__device__ __forceinline__ double ld_wt(const double* p) {
+    return __longlong_as_double(
+        __hip_atomic_load(reinterpret_cast<const long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_wt(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool coop_grid_sync(unsigned* count, unsigned target, int* fault, int* lflag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int bad = 0;
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > 400000ull || __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                bad = 1;
+                __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *lflag = bad;
+    }
+    __syncthreads();
+    return *lflag == 0;
+}
+
+#ifdef TCI_COOP_PROF  // phase sums of workgroup 0 (100 MHz ticks), printed at the end (A/B builds only)
+#define COOP_T(i) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); pacc[i] += t_ - tlast; tlast = t_; } } while (0)
+#else
+#define COOP_T(i) do { } while (0)
+#endif
+__global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, int r, int* __restrict__ piv,
+                                                        unsigned* count, int* fault) {
+#ifdef TCI_COOP_PROF
+    unsigned long long pacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
+#endif
+    constexpr int NBP = kCoopNBP, RPT = kCoopRPT, NT = kCoopNT, NW = NT / 64, CW = kCoopCW;
+    constexpr int LDB = NT * RPT;  // ld of the staged column block (rows jb..r-1 <= 1024)
+    __shared__ double sv[NW];
+    __shared__ int si[NW];
+    __shared__ double prow[NBP], crow[NBP];
+    __shared__ int spiv[NBP];
+    __shared__ double sL11[NBP * NBP];  // sL11[i NBP + c] = L(i, c) of the panel, i, c < nbp
+    __shared__ int pos[2 * NBP], src[2 * NBP];
+    __shared__ int naff, lflag;
+    constexpr int CT = 2 * CW;  // columns a workgroup owns at most (2 blocks: nblk <= 2 G at r <= 1024)
+    __shared__ double cb[CT * LDB];  // its right-of-panel columns, rows jb..r-1 (ld LDB)
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nblk = (r + CW - 1) / CW;
+    unsigned epoch = 0;
+    for (int jb = 0; jb < r; jb += NBP) {
+        const int nbp = min(NBP, r - jb), je = jb + nbp, rows = r - jb;
+        // 1. the panel, factorised in registers (every workgroup)
+        RegPanel<NBP, RPT, NT> S;
+        S.tid = tid;
+        S.rows = rows;
+        S.nbp = nbp;
+        S.jb = jb;
+        S.piv = spiv - jb;  // reg_panel_col stores piv[jb + C] = jb + p
+        S.sv = sv;
+        S.si = si;
+        S.prow = prow;
+        S.crow = crow;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int i = tid + u * NT;
+#pragma unroll
+            for (int c = 0; c < NBP; ++c)
+                S.v[u][c] = (i < rows && c < nbp) ? ld_wt(A + (int64_t)(jb + i) + (int64_t)(jb + c) * r) : 0.0;
+        }
+        S.bv = -1.0;
+        S.bi = 0x7fffffff;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int i = tid + u * NT;
+            if (i < rows) {
+                const double a = fabs(S.v[u][0]);
+                if (a > S.bv) { S.bv = a; S.bi = i; }
+            }
+        }
+        COOP_T(0);
+        reg_panel_col<NBP, RPT, 0, NT>(S);
+        COOP_T(1);
+        if (tid < nbp) {
+#pragma unroll
+            for (int c = 0; c < NBP; ++c) sL11[tid * NBP + c] = S.v[0][c];
+        }
+        __syncthreads();  // spiv (the last column's) and sL11
+        // 2. the interchanges
+        if (g == 0 && tid < nbp) piv[jb + tid] = spiv[tid];
+        // the owned blocks: b = g and b = g + G (nblk <= 2 G); left of the panel, the panel's own
+        // (stored in step 5) or right of it
+        const int b0 = g, b1 = g + G;
+        const int n0 = b0 < nblk ? min(CW, r - b0 * CW) : 0, n1 = b1 < nblk ? min(CW, r - b1 * CW) : 0;
+        const bool r0 = n0 > 0 && b0 * CW >= je, r1 = n1 > 0 && b1 * CW >= je;
+        const bool l0 = n0 > 0 && b0 * CW < jb, l1 = n1 > 0 && b1 * CW < jb;
+        // right blocks' staging loads go out first (the interchanges are not needed for them)
+        double sv_[CW][RPT];
+        auto stage_load = [&](int c0, int nc) {
+#pragma unroll
+            for (int k = 0; k < CW; ++k)
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const int i = tid + u * NT;
+                    sv_[k][u] = (k < nc && i < rows) ? ld_wt(A + (int64_t)(jb + i) + (int64_t)(c0 + k) * r) : 0.0;
+                }
+        };
+        auto stage_store = [&](int kofs) {
+#pragma unroll
+            for (int k = 0; k < CW; ++k)
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) cb[(kofs + k) * LDB + tid + u * NT] = sv_[k][u];
+        };
+        const int firstR = r0 ? b0 : b1;  // local columns 0..7: the first right block, 8..15: the second
+        const int nR = (r0 ? 1 : 0) + (r1 ? 1 : 0);
+        if (nR) stage_load(firstR * CW, firstR == b0 ? n0 : n1);
+        if (tid < 64) {  // compose the interchanges into <= 2 nbp (position, source) pairs (k_getrf_swap)
+            const int l = tid;
+            int pos0 = l < nbp ? jb + l : -1, src0 = pos0;
+            int pos1 = -1, src1 = -1;
+            int n = nbp;
+            const int pl = l < nbp ? spiv[l] : 0;
+            for (int k = 0; k < nbp; ++k) {
+                const int p = __builtin_amdgcn_readlane(pl, k);
+                const unsigned long long bb0 = __ballot(pos0 == p), bb1 = __ballot(pos1 == p);
+                int qp;
+                if (bb0) qp = __ffsll((long long)bb0) - 1;
+                else if (bb1) qp = 64 + __ffsll((long long)bb1) - 1;
+                else {
+                    qp = n++;
+                    if (qp < 64) { if (l == qp) { pos0 = p; src0 = p; } }
+                    else if (l == qp - 64) { pos1 = p; src1 = p; }
+                }
+                const int sk = __shfl(src0, k);
+                const int sp = qp < 64 ? __shfl(src0, qp) : __shfl(src1, qp - 64);
+                if (l == k) src0 = sp;
+                if (qp < 64) { if (l == qp) src0 = sk; }
+                else if (l == qp - 64) src1 = sk;
+            }
+            if (l < 2 * NBP) { pos[l] = pos0; src[l] = src0; }
+            if (l + 64 < 2 * NBP) { pos[l + 64] = pos1; src[l + 64] = src1; }
+            if (l == 0) naff = n;
+        }
+        if (nR) stage_store(0);
+        if (nR == 2) {
+            stage_load(b1 * CW, n1);
+            stage_store(CW);
+        }
+        __syncthreads();
+        const int na = naff;
+        COOP_T(2);
+        // 3. left blocks: the composed interchanges on global memory; right blocks: the same on the
+        // staged rows in LDS (all loads, one barrier, all stores)
+        const int nL = (l0 ? 1 : 0) + (l1 ? 1 : 0);
+        const int lcol0 = l0 ? b0 * CW : b1 * CW, lcol1 = b1 * CW;
+        const int lnc0 = l0 ? n0 : n1;
+        const int ne = CW * na;  // (column, slot) pairs per block, <= 2 NT
+        double lv[2][2], pv[4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = tid + h * NT, c0 = q == 0 ? lcol0 : lcol1, nc = q == 0 ? lnc0 : n1;
+                lv[q][h] = (q < nL && e < ne && e / na < nc) ? ld_wt(A + (int64_t)src[e % na] + (int64_t)(c0 + e / na) * r) : 0.0;
+            }
+        const int nck = nR * CW;  // staged local columns (padding columns of a short block included)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int e = tid + h * NT;
+            pv[h] = e < nck * na ? cb[(e / na) * LDB + src[e % na] - jb] : 0.0;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = tid + h * NT, c0 = q == 0 ? lcol0 : lcol1, nc = q == 0 ? lnc0 : n1;
+                if (q < nL && e < ne && e / na < nc) st_wt(A + (int64_t)pos[e % na] + (int64_t)(c0 + e / na) * r, lv[q][h]);
+            }
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int e = tid + h * NT;
+            if (e < nck * na) cb[(e / na) * LDB + pos[e % na] - jb] = pv[h];
+        }
+        __syncthreads();
+        if (nR) {
+            for (int k = wv; k < nck; k += NW) {  // U12 = L11^-1 A12: x_j -= L(j, c) x_c, c ascending
+                double x = lane < nbp ? cb[k * LDB + lane] : 0.0;
+#pragma unroll
+                for (int c = 0; c < NBP; ++c) {
+                    if (c < nbp) {
+                        const double xc = readlane_d(x, c);
+                        if (lane > c && lane < nbp) x = __dsub_rn(x, __dmul_rn(sL11[lane * NBP + c], xc));
+                    }
+                }
+                if (lane < nbp) cb[k * LDB + lane] = x;
+            }
+            __syncthreads();
+            // A22 -= L21 U12, L21 from the panel registers, U12 read once per (column, c) for all u
+            for (int k = 0; k < nck; ++k) {
+                const int blk = k < CW ? firstR : b1, kk = k & (CW - 1);
+                const int nc = blk == b0 ? n0 : n1;
+                if (kk >= nc) continue;
+                double a[RPT];
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) a[u] = cb[k * LDB + tid + u * NT];
+#pragma unroll
+                for (int c = 0; c < NBP; ++c) {
+                    if (c < nbp) {
+                        const double uc = cb[k * LDB + c];
+#pragma unroll
+                        for (int u = 0; u < RPT; ++u)
+                            if (tid + u * NT >= nbp) a[u] = __dsub_rn(a[u], __dmul_rn(S.v[u][c], uc));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const int i = tid + u * NT;
+                    if (i < rows) st_wt(A + (int64_t)(jb + i) + (int64_t)(blk * CW + kk) * r, a[u]);
+                }
+            }
+        }
+        COOP_T(3);
+        // 4. every column the next panel reads is stored: grid barrier
+        ++epoch;
+        if (je < r && !coop_grid_sync(count, epoch * (unsigned)G, fault, &lflag)) return;
+        COOP_T(4);
+        // 5. only now (every workgroup has loaded the panel) its owned column blocks are stored; the
+        // next panel's interchanges reach them through this workgroup's own step 3 (same CU: a
+        // drained store is visible to its other waves after the barrier)
+#pragma unroll
+        for (int c = 0; c < NBP; ++c) {
+            if (c < nbp && ((jb + c) / CW) % G == g) {
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const int i = tid + u * NT;
+                    if (i < rows) A[(int64_t)(jb + i) + (int64_t)(jb + c) * r] = S.v[u][c];
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        COOP_T(5);
+    }
+#ifdef TCI_COOP_PROF
+    if (tid == 0 && g == 0)
+        printf("coop getrf r %d G %d: load %.1f factor %.1f compose %.1f blocks %.1f barrier %.1f store %.1f us\n", r, G,
+               pacc[0] * 0.01, pacc[1] * 0.01, pacc[2] * 0.01, pacc[3] * 0.01, pacc[4] * 0.01, pacc[5] * 0.01);
+#endif
+}
+
+// sync: two words (arrival counter, fault), zeroed here
+void launch_getrf_coop(hipStream_t s, double* A, int r, int* piv, unsigned* sync) {
+    hipLaunchKernelGGL(k_transpose_sq, dim3(std::min(2048, std::max(1, (r * r + 255) / 256))), dim3(256), 0, s,
+                       A, r);
+    (void)hipMemsetAsync(sync, 0, 2 * sizeof(unsigned), s);
+    const int G = std::min(kCoopMaxG, (r + kCoopCW - 1) / kCoopCW);
+    hipLaunchKernelGGL(k_getrf_coop, dim3(G), dim3(kCoopNT), 0, s, A, r, piv, sync,
+                       reinterpret_cast<int*>(sync + 1));
 }
 
 // T (R x r) = Pi1 P^-1 given A = LU(P^T) and its interchanges: T's columns permuted as the rows of

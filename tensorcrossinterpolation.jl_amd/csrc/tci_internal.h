@@ -341,7 +341,8 @@ void launch_cache_rehash(hipStream_t s, const unsigned long long* ok, const doub
 // columns >= np (otherwise) are overwritten by the triangular solve.
 // dense: bit mask of the fp64 MFMA forms (tci_dense.hip) to use, kDense* below; 0 = the
 // round-1 scalar GEMMs / LDS TRSMs / single-workgroup getrf (kept for A/B)
-constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseGetrfReg = 8, kDenseAll = 15;
+constexpr int kDenseLuci = 1, kDenseGetrf = 2, kDenseGetrs = 4, kDenseGetrfReg = 8, kDenseGetrfCoop = 16,
+              kDenseAll = 31;
 void launch_luci_factors(hipStream_t s, double* L, int64_t ldl, double* U, int64_t ldu, int m,
                          int n, int np, int leftorth, const int64_t* rowperm,
                          const int64_t* colperm, double* left, double* right, int dense);
@@ -379,6 +380,7 @@ void launch_tt_eval(hipStream_t s, const double* cores, const int64_t* off, cons
 
 // site-tensor solve: T (R x r) = Pi1 (R x r) * P^-1; P overwritten by its LU (partial pivot of P^T)
 // piv: 2 r ints
+bool getrf_coop_fits(int r);
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
                              int* piv, int dense);
 

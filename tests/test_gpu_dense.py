@@ -108,10 +108,64 @@ def test_getrf_register_panel_bitwise(ctx, r, R):
             T.sitetensor_solve_device(dP, dPi1, dT)
             out[mask] = dT.to_host()
     finally:
-        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 15))
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
     ref = O.sitetensor_solve(P, Pi1).reshape((R, r), order="F")
     np.testing.assert_allclose(out[15], out[7], rtol=1e-11, atol=1e-13 * np.abs(ref).max())
     np.testing.assert_allclose(out[15], ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("r,R", [(1024, 4096), (1000, 300), (256, 2048), (97, 300), (70, 130), (24, 50),
+                                 (8, 9), (1, 5), (1100, 40)])
+def test_sitetensor_solve_coop_recursive(ctx, r, R):
+    """Round 6: the cooperative one-launch getrf (mask bit 16, r <= 1024) against the
+    launch-per-panel form (mask 15), the LDS panels (7) and the oracle. Every form factorises with
+    the same pivot rule; the sums run in other orders, so they agree to rounding. r = 1100 is past
+    the cooperative kernel's 1024 rows (the blocked getrf runs)."""
+    rng = np.random.default_rng(r * 5 + R)
+    P = rng.random((r, r)) + 0.5 * np.sqrt(r) * np.eye(r) * rng.choice([-1, 1], r)
+    Pi1 = rng.random((R, r))
+    ref = O.sitetensor_solve(P, Pi1).reshape((R, r), order="F")
+    out = {}
+    try:
+        for mask in (31, 15, 7):
+            ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+            dP, dPi1, dT = _dev(ctx, P, True), _dev(ctx, Pi1, True), T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+            T.sitetensor_solve_device(dP, dPi1, dT)
+            out[mask] = dT.to_host()
+    finally:
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
+    tol = dict(rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+    for mask, got in out.items():
+        np.testing.assert_allclose(got, ref, err_msg=f"mask {mask}", **tol)
+        np.testing.assert_allclose(got, out[15], err_msg=f"mask {mask} vs 15", **tol)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("r", [256, 1024])
+def test_sitetensor_solve_unweighted_backward_error(ctx, r):
+    """A plain U[0,1) pivot matrix (no diagonal weight: cond ~ 1e4-1e6, partial pivoting with real
+    row exchanges everywhere): the default solve's backward error ||T P - Pi1|| / (||T|| ||P||) stays
+    at the level of a LAPACK solve's, and it agrees with the launch-per-panel / left-looking forms to cond(P) eps."""
+    rng = np.random.default_rng(r + 1)
+    P = rng.random((r, r))
+    R = 3 * r
+    Pi1 = rng.random((R, r))
+    got = {}
+    try:
+        for mask in (31, 15):
+            ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+            dP, dPi1, dT = _dev(ctx, P, True), _dev(ctx, Pi1, True), T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+            T.sitetensor_solve_device(dP, dPi1, dT)
+            got[mask] = dT.to_host()
+    finally:
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
+    eps = np.finfo(float).eps
+    for mask, Tm in got.items():
+        berr = np.linalg.norm(Tm @ P - Pi1) / (np.linalg.norm(Tm) * np.linalg.norm(P))
+        assert berr < 64 * r * eps, (mask, berr)
+    cond = np.linalg.cond(P)
+    assert np.linalg.norm(got[31] - got[15]) <= 64 * r * eps * cond * np.linalg.norm(got[15])
 
 
 @pytest.mark.timeout(300)
