@@ -23,7 +23,6 @@ idx = [i for i, r in enumerate(rows) if "k_transpose_sq" in r["Kernel_Name"]]
 seg = rows[idx[-1]:]
 t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
-getrf_end = max(int(r["End_Timestamp"]) for r in seg if "getrf" in r["Kernel_Name"] or "dgemm" in r["Kernel_Name"] and int(r["Start_Timestamp"]) < int([x for x in seg if "k_piv_to_perm" in x["Kernel_Name"]][0]["Start_Timestamp"]))
 print(f"last solve: {len(seg)} kernels, span {(t1 - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us")
 gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(seg, seg[1:])]
 print("gap quantiles (us):", [round(sorted(gaps)[int(q * (len(gaps) - 1))], 2) for q in (0.1, 0.5, 0.9, 0.99)])

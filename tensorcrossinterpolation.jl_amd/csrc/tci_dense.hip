@@ -851,8 +851,11 @@ __global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, 
     __shared__ int naff, lflag;
     constexpr int CT = 2 * CW;  // columns a workgroup owns at most (2 blocks: nblk <= 2 G at r <= 1024)
     __shared__ double cb[CT * LDB];  // its right-of-panel columns, rows jb..r-1 (ld LDB)
+    __shared__ int sperm[LDB];        // workgroup 0: the permutation the interchanges compose to
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nblk = (r + CW - 1) / CW;
+    if (g == 0)
+        for (int a = tid; a < r; a += NT) sperm[a] = a;
     unsigned epoch = 0;
     for (int jb = 0; jb < r; jb += NBP) {
         const int nbp = min(NBP, r - jb), je = jb + nbp, rows = r - jb;
@@ -954,6 +957,11 @@ __global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, 
         }
         __syncthreads();
         const int na = naff;
+        if (g == 0) {  // perm[pos[q]] <- perm[src[q]] (k_piv_to_perm's result, without its serial loop)
+            const int pv0 = tid < na ? sperm[src[tid]] : 0;
+            __syncthreads();
+            if (tid < na) sperm[pos[tid]] = pv0;
+        }
         COOP_T(2);
         // 3. left blocks: the composed interchanges on global memory; right blocks: the same on the
         // staged rows in LDS (all loads, one barrier, all stores)
@@ -1049,6 +1057,10 @@ __global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, 
         __syncthreads();
         COOP_T(5);
     }
+    if (g == 0) {
+        __syncthreads();
+        for (int a = tid; a < r; a += NT) piv[r + a] = sperm[a];
+    }
 #ifdef TCI_COOP_PROF
     if (tid == 0 && g == 0)
         printf("coop getrf r %d G %d: load %.1f factor %.1f compose %.1f blocks %.1f barrier %.1f store %.1f us\n", r, G,
@@ -1115,8 +1127,8 @@ __global__ void k_gather_cols(const double* __restrict__ Pi1, int R, int r, cons
 }
 
 void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv, const double* Pi1,
-                          int R, double* T, int* perm) {
-    hipLaunchKernelGGL(k_piv_to_perm, dim3(1), dim3(256), 0, s, piv, r, perm);
+                          int R, double* T, int* perm, bool perm_ready) {
+    if (!perm_ready) hipLaunchKernelGGL(k_piv_to_perm, dim3(1), dim3(256), 0, s, piv, r, perm);
     const long long work = (long long)R * r;
     hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)std::min<long long>(8192, (work + 255) / 256)), dim3(256),
                        0, s, Pi1, R, r, perm, T);

@@ -1208,7 +1208,7 @@ bool getrf_blocked_fits(int r);
 void launch_getrf_coop(hipStream_t s, double* A, int r, int* piv, unsigned* sync);
 void launch_getrf_blocked(hipStream_t s, double* A, int r, int* piv, bool reg_panel);
 void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv, const double* Pi1,
-                          int R, double* T, int* perm);
+                          int R, double* T, int* perm, bool perm_ready);
 
 
 // piv: 2 r + 2 ints (interchanges, the permutation they compose to, the cooperative getrf's
@@ -1216,14 +1216,15 @@ void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv,
 void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
                              int* piv, int dense) {
     const int reg = kDenseGetrf | kDenseGetrfReg | kDenseGetrfCoop;
-    if ((dense & reg) == reg && getrf_coop_fits(r))
+    const bool coop = (dense & reg) == reg && getrf_coop_fits(r);  // also leaves the permutation at piv + r
+    if (coop)
         launch_getrf_coop(s, P, r, piv, reinterpret_cast<unsigned*>(piv + 2 * r));
     else if ((dense & kDenseGetrf) && getrf_blocked_fits(r))
         launch_getrf_blocked(s, P, r, piv, (dense & kDenseGetrfReg) != 0);
     else hipLaunchKernelGGL(k_getrf_transposed, dim3(1), dim3(1024), 0, s, P, r, piv);
     if (R <= 0) return;
     if (dense & kDenseGetrs) {
-        launch_getrs_blocked(s, P, r, piv, Pi1, R, T, piv + r);
+        launch_getrs_blocked(s, P, r, piv, Pi1, R, T, piv + r, coop);
         return;
     }
     if (r > 4096) {
