@@ -2183,8 +2183,14 @@ int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int6
 // setsitetensor!'s solve on device buffers (piv: c->dPiv, 2 r + 2 ints). The cooperative getrf
 // (tci_dense.hip k_getrf_coop) needs its workgroups co-resident; if one of them waited past its
 // timeout (another stream or process holding the CUs) every workgroup left and the fault word is
-// set: the solve is then redone from a copy of P on the launch-per-panel path. One host
-// synchronisation more per cooperative solve (the fault word), ~10 us against ms of solve.
+// set: the solve is then redone from a copy of P on the launch-per-panel path. The getrs is launched
+// only after the word is read (a getrf that gave up leaves no permutation for it to gather by): one
+// host synchronisation more per cooperative solve, ~10 us against ms of solve.
+namespace tci {
+void launch_sitetensor_solve_parts(hipStream_t s, double* P, int r, double* Pi1, int R, double* T, int* piv,
+                                   int dense, int parts);
+}
+
 static int solve_launch(tci_ctx* c, double* P, int64_t r, double* Pi1, int64_t R, double* T) {
     const int coopmask = tci::kDenseGetrf | tci::kDenseGetrfReg | tci::kDenseGetrfCoop;
     const bool coop = (c->dense & coopmask) == coopmask && tci::getrf_coop_fits((int)r);
@@ -2194,12 +2200,20 @@ static int solve_launch(tci_ctx* c, double* P, int64_t r, double* Pi1, int64_t R
         if (!c->hCoop) HIPCHK(c, hipHostMalloc((void**)&c->hCoop, 64, hipHostMallocDefault));
         HIPCHK(c, hipMemcpyAsync(c->dPbak, P, (size_t)(r * r) * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     }
-    tci::launch_sitetensor_solve(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense);
+    if (!coop) {
+        tci::launch_sitetensor_solve(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense);
+        HIPCHK(c, hipGetLastError());
+        return TCI_OK;
+    }
+    tci::launch_sitetensor_solve_parts(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense, 1);
     HIPCHK(c, hipGetLastError());
-    if (!coop) return TCI_OK;
     HIPCHK(c, hipMemcpyAsync(c->hCoop, c->dPiv + 2 * r + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (*c->hCoop == 0) return TCI_OK;
+    if (*c->hCoop == 0) {  // the permutation is in place: the getrs
+        tci::launch_sitetensor_solve_parts(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense, 2);
+        HIPCHK(c, hipGetLastError());
+        return TCI_OK;
+    }
     ++c->coop_faults;
     HIPCHK(c, hipMemcpyAsync(P, c->dPbak, (size_t)(r * r) * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     tci::launch_sitetensor_solve(c->stream, P, (int)r, Pi1, (int)R, T, c->dPiv, c->dense & ~tci::kDenseGetrfCoop);

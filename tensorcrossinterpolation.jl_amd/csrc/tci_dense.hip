@@ -836,7 +836,7 @@ __device__ __forceinline__ bool coop_grid_sync(unsigned* count, unsigned target,
 #define COOP_T(i) do { } while (0)
 #endif
 __global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, int r, int* __restrict__ piv,
-                                                        unsigned* count, int* fault) {
+                                                        unsigned* count, int* fault, int inject) {
 #ifdef TCI_COOP_PROF
     unsigned long long pacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
 #endif
@@ -1038,6 +1038,8 @@ __global__ __launch_bounds__(kCoopNT) void k_getrf_coop(double* __restrict__ A, 
         COOP_T(3);
         // 4. every column the next panel reads is stored: grid barrier
         ++epoch;
+        if (inject && g == 0 && epoch == 2 && tid == 0)  // test mode: a barrier timeout, simulated
+            __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (je < r && !coop_grid_sync(count, epoch * (unsigned)G, fault, &lflag)) return;
         COOP_T(4);
         // 5. only now (every workgroup has loaded the panel) its owned column blocks are stored; the
@@ -1074,8 +1076,12 @@ void launch_getrf_coop(hipStream_t s, double* A, int r, int* piv, unsigned* sync
                        A, r);
     (void)hipMemsetAsync(sync, 0, 2 * sizeof(unsigned), s);
     const int G = std::min(kCoopMaxG, (r + kCoopCW - 1) / kCoopCW);
+    // TCI_COOP_FAULT_TEST=1 (tests only): workgroup 0 raises the fault word at the second barrier,
+    // as a timed-out wait would, so the host's redo-from-a-copy path runs (read per launch)
+    const char* e = getenv("TCI_COOP_FAULT_TEST");
+    const int inject = e && atoi(e) != 0;
     hipLaunchKernelGGL(k_getrf_coop, dim3(G), dim3(kCoopNT), 0, s, A, r, piv, sync,
-                       reinterpret_cast<int*>(sync + 1));
+                       reinterpret_cast<int*>(sync + 1), inject);
 }
 
 // T (R x r) = Pi1 P^-1 given A = LU(P^T) and its interchanges: T's columns permuted as the rows of

@@ -1212,16 +1212,21 @@ void launch_getrs_blocked(hipStream_t s, const double* A, int r, const int* piv,
 
 
 // piv: 2 r + 2 ints (interchanges, the permutation they compose to, the cooperative getrf's
-// arrival counter and fault word -- the caller checks that word, tci_abi.cpp solve_launch)
-void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
-                             int* piv, int dense) {
+// arrival counter and fault word). parts: 1 = the getrf, 2 = the getrs, 3 = both. A cooperative
+// getrf that gave up leaves no permutation, so its caller launches part 1, checks the fault word,
+// and only then part 2 (tci_abi.cpp solve_launch)
+void launch_sitetensor_solve_parts(hipStream_t s, double* P, int r, double* Pi1, int R, double* T,
+                                   int* piv, int dense, int parts) {
     const int reg = kDenseGetrf | kDenseGetrfReg | kDenseGetrfCoop;
     const bool coop = (dense & reg) == reg && getrf_coop_fits(r);  // also leaves the permutation at piv + r
-    if (coop)
-        launch_getrf_coop(s, P, r, piv, reinterpret_cast<unsigned*>(piv + 2 * r));
-    else if ((dense & kDenseGetrf) && getrf_blocked_fits(r))
-        launch_getrf_blocked(s, P, r, piv, (dense & kDenseGetrfReg) != 0);
-    else hipLaunchKernelGGL(k_getrf_transposed, dim3(1), dim3(1024), 0, s, P, r, piv);
+    if (parts & 1) {
+        if (coop)
+            launch_getrf_coop(s, P, r, piv, reinterpret_cast<unsigned*>(piv + 2 * r));
+        else if ((dense & kDenseGetrf) && getrf_blocked_fits(r))
+            launch_getrf_blocked(s, P, r, piv, (dense & kDenseGetrfReg) != 0);
+        else hipLaunchKernelGGL(k_getrf_transposed, dim3(1), dim3(1024), 0, s, P, r, piv);
+    }
+    if (!(parts & 2)) return;
     if (R <= 0) return;
     if (dense & kDenseGetrs) {
         launch_getrs_blocked(s, P, r, piv, Pi1, R, T, piv + r, coop);
@@ -1246,6 +1251,11 @@ void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R
         go(k_getrs_blocked<8>, 8);
     else
         go(k_getrs_blocked<2>, 2);
+}
+
+void launch_sitetensor_solve(hipStream_t s, double* P, int r, double* Pi1, int R, double* T, int* piv,
+                             int dense) {
+    launch_sitetensor_solve_parts(s, P, r, Pi1, R, T, piv, dense, 3);
 }
 
 }  // namespace tci

@@ -142,6 +142,36 @@ def test_sitetensor_solve_coop_recursive(ctx, r, R):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("r,R", [(256, 512), (1024, 96)])
+def test_coop_getrf_fault_falls_back(ctx, monkeypatch, r, R):
+    """The cooperative getrf's give-up path (a workgroup waited past its timeout: every workgroup
+    leaves and sets the fault word), simulated by TCI_COOP_FAULT_TEST=1: solve_launch reads the
+    word, restores P from its copy and redoes the solve on the launch-per-panel path -- so the
+    result is bitwise that path's (mask 15), and the context keeps working afterwards."""
+    rng = np.random.default_rng(r + 3 * R)
+    P = rng.random((r, r)) + 0.5 * np.sqrt(r) * np.eye(r) * rng.choice([-1, 1], r)
+    Pi1 = rng.random((R, r))
+
+    def solve(mask):
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, mask))
+        dP, dPi1, dT = _dev(ctx, P, True), _dev(ctx, Pi1, True), T.DeviceMatrix(R, r, ctx=ctx, ld=R)
+        T.sitetensor_solve_device(dP, dPi1, dT)
+        return dT.to_host()
+
+    try:
+        monkeypatch.setenv("TCI_COOP_FAULT_TEST", "1")
+        fell_back = solve(31)
+        monkeypatch.delenv("TCI_COOP_FAULT_TEST")
+        blocked = solve(15)
+        coop = solve(31)
+    finally:
+        ctx.check(ctx.lib.tci_set_dense_mfma(ctx.h, 31))
+    assert np.array_equal(fell_back, blocked)
+    ref = O.sitetensor_solve(P, Pi1).reshape((R, r), order="F")
+    np.testing.assert_allclose(coop, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("r", [256, 1024])
 def test_sitetensor_solve_unweighted_backward_error(ctx, r):
     """A plain U[0,1) pivot matrix (no diagonal weight: cond ~ 1e4-1e6, partial pivoting with real
