@@ -2186,9 +2186,11 @@ int tci_update_pivots_h(tci_ctx* c, const tci_func* f, const int32_t* rows, int6
 // set: the solve is then redone from a copy of P on the launch-per-panel path. The getrs is launched
 // only after the word is read (a getrf that gave up leaves no permutation for it to gather by): one
 // host synchronisation more per cooperative solve, ~10 us against ms of solve.
+extern "C++" {  // (this file's ABI block is extern "C")
 namespace tci {
 void launch_sitetensor_solve_parts(hipStream_t s, double* P, int r, double* Pi1, int R, double* T, int* piv,
                                    int dense, int parts);
+}
 }
 
 static int solve_launch(tci_ctx* c, double* P, int64_t r, double* Pi1, int64_t R, double* T) {
